@@ -1,0 +1,76 @@
+"""ctypes binding of libcrosscoder_hip.so (the C ABI declared in include/crosscoder_hip.h).
+
+The library is built in-tree (`make -C crosscoder-model-diff-replication_amd/csrc`, or
+`__graft_entry__.build()`) and loaded from this package directory.  There is no fallback:
+if the library is missing every compute entry point raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcrosscoder_hip.so")
+
+CC_BF16 = 1
+CC_F32 = 2
+CC_LAYOUT_KC = 0
+CC_LAYOUT_MN = 1
+
+_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i = ctypes.c_int
+_f = ctypes.c_float
+
+# name -> (restype, argtypes); must list every symbol of include/crosscoder_hip.h
+SIGNATURES = {
+    "cc_version": (_i, []),
+    "cc_strerror": (ctypes.c_char_p, [_i]),
+    "cc_col_part_rows": (_i64, [_i64]),
+    "cc_wave_parts": (_i64, [_i64, _i64]),
+    "cc_prep_part_rows": (_i64, [_i64]),
+    "cc_loss_part_rows": (_i64, [_i64]),
+    "cc_loss_col_blocks": (_i64, [_i64]),
+    "cc_loss_scalars_len": (_i64, [_i64]),
+    "cc_gemm_f32out": (_i, [_p, _i, _i64, _p, _i, _i64, _p, _i64, _i64, _i64, _i64, _i, _p]),
+    "cc_prep_input": (_i, [_p, _i, _p, _i, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_reduce_rows": (_i, [_p, _i64, _i64, _i64, _f, _p, _p, _i, _p, _p]),
+    "cc_dec_norms": (_i, [_p, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_encode_fwd": (_i, [_p, _p, _p, _p, _p, _i, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_decode_fwd": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_loss_fwd_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i, _p]),
+    "cc_loss_finalize": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "cc_dacts_bwd": (_i, [_p, _p, _p, _p, _f, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_wgrad_dec": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
+    "cc_wgrad_enc": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_clip_finalize": (_i, [_p, ctypes.POINTER(_i64), _i, _f, _i, _p, _p]),
+    "cc_adam_step": (_i, [_p, _p, _p, _p, _i64, _p, _f, _f, _f, _f, _i64, _i, _p]),
+}
+
+_lib = None
+
+
+class HipLibraryMissing(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load (once) and type the library; raises HipLibraryMissing if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise HipLibraryMissing(
+            f"{path} not found: build it with `make -C {os.path.dirname(path)}/csrc` "
+            "(crosscoder_amd has no CPU fallback)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = load().cc_strerror(rc)
+        raise RuntimeError(f"crosscoder_hip error {rc}: {msg.decode() if msg else '?'}")

@@ -1,0 +1,227 @@
+"""Drop-in `CrossCoder` (reference: crosscoder.py:24-217) running on gfx950 HIP kernels.
+
+Same constructor cfg, same parameter names / shapes / dtypes / strides, same state_dict and
+checkpoint format, same `encode / decode / forward / get_losses / save / load` surface.
+The parameters are views of one flat HBM arena (engine.Arena) so the fused Adam can update
+all of them in one launch; `W_enc` keeps the reference's h-major strides (d, 1, n*d).
+"""
+import json
+import pprint
+from pathlib import Path
+from typing import NamedTuple, Optional, Union
+
+import torch
+from torch import nn
+
+from . import engine, ops
+
+DTYPES = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
+SAVE_DIR = Path("./checkpoints")
+
+
+class LossOutput(NamedTuple):
+    l2_loss: torch.Tensor
+    l1_loss: torch.Tensor
+    l0_loss: torch.Tensor
+    explained_variance: torch.Tensor
+    explained_variance_A: torch.Tensor
+    explained_variance_B: torch.Tensor
+
+
+def reference_init(cfg, n_models=2):
+    """Bit-exact restatement of the reference initialisation (crosscoder.py:31-62) on the CPU
+    generator: seed, W_dec drawn twice (the second draw wins), per-(h, model) rows scaled to
+    dec_init_norm, W_enc = rearranged clone (same values), zero biases."""
+    dtype = DTYPES[cfg["enc_dtype"]]
+    h, d = cfg["dict_size"], cfg["d_in"]
+    torch.manual_seed(cfg["seed"])
+    _ = torch.empty(n_models, d, h, dtype=dtype)  # W_enc placeholder (no RNG use)
+    torch.nn.init.normal_(torch.empty(h, n_models, d, dtype=dtype))  # first draw, discarded
+    W_dec = torch.nn.init.normal_(torch.empty(h, n_models, d, dtype=dtype))
+    W_dec = W_dec / W_dec.norm(dim=-1, keepdim=True) * cfg["dec_init_norm"]
+    return W_dec
+
+
+class CrossCoder(nn.Module):
+    def __init__(self, cfg, n_models: Optional[int] = None):
+        super().__init__()
+        self.cfg = cfg
+        d_hidden = cfg["dict_size"]
+        d_in = cfg["d_in"]
+        self.n_models = int(n_models if n_models is not None else cfg.get("n_models", 2))
+        self.dtype = DTYPES[cfg["enc_dtype"]]
+        if self.dtype not in (torch.float32, torch.bfloat16):
+            raise TypeError("crosscoder_amd kernels support enc_dtype 'bf16' and 'fp32'")
+        device = torch.device(cfg["device"])
+        W_dec = reference_init(cfg, self.n_models)
+        self._arena = engine.Arena(d_hidden, self.n_models, d_in, self.dtype, device)
+        with torch.no_grad():
+            self._arena.W_dec().copy_(W_dec)
+            self._arena.W_enc().copy_(W_dec.permute(1, 2, 0))
+        self._bind_params()
+        self.d_hidden = d_hidden
+        self.save_dir = None
+        self.save_version = 0
+        self._ws = None
+
+    # ------------------------------------------------------------------ arena plumbing
+    def _bind_params(self):
+        v = self._arena.views()
+        self.W_enc = nn.Parameter(v["W_enc"])
+        self.W_dec = nn.Parameter(v["W_dec"])
+        self.b_enc = nn.Parameter(v["b_enc"])
+        self.b_dec = nn.Parameter(v["b_dec"])
+
+    def _arena_ok(self):
+        a = self._arena
+        v = a.views()
+        for name in ("W_enc", "W_dec", "b_enc", "b_dec"):
+            p = getattr(self, name)
+            if p.data_ptr() != v[name].data_ptr() or p.stride() != v[name].stride() or p.device != a.data.device:
+                return False
+        return True
+
+    def arena(self):
+        """The flat parameter arena; re-packs the params if something (e.g. .to()) replaced them."""
+        if not self._arena_ok():
+            dev = self.W_dec.device
+            new = engine.Arena(self.d_hidden, self.n_models, self.cfg["d_in"], self.dtype, dev)
+            with torch.no_grad():
+                for name, dst in new.views().items():
+                    dst.copy_(getattr(self, name).data)
+            self._arena = new
+            grads = {n: getattr(self, n).grad for n in ("W_enc", "W_dec", "b_enc", "b_dec")}
+            self._bind_params()
+            for n, g in grads.items():
+                getattr(self, n).grad = g
+            self._ws = None
+        return self._arena
+
+    def _workspace(self, B):
+        a = self.arena()
+        ws = self._ws
+        if ws is None or ws.B != B or ws.x.device != a.data.device:
+            ws = engine.StepWorkspace(B, self.n_models, self.cfg["d_in"], self.d_hidden, self.dtype, a.data.device)
+            self._ws = ws
+        return ws
+
+    def _flat_x(self, x):
+        x = x.contiguous()
+        if x.dim() != 3 or x.shape[1] != self.n_models or x.shape[2] != self.cfg["d_in"]:
+            raise ValueError(f"expected x of shape [batch, {self.n_models}, {self.cfg['d_in']}], got {tuple(x.shape)}")
+        if x.dtype == self.dtype:
+            return x.view(x.shape[0], -1)
+        return ops.prep_input(x, None, self.dtype)
+
+    # ------------------------------------------------------------------ reference API
+    def encode(self, x, apply_relu=True):
+        """x [batch, n_models, d_model] -> acts [batch, d_hidden] (crosscoder.py:69-80)."""
+        a = self.arena()
+        xf = self._flat_x(x)
+        acts = torch.empty(xf.shape[0], self.d_hidden, dtype=self.dtype, device=xf.device)
+        ops.encode_fwd(xf, a.W_enc_hk, a.b_enc, acts, apply_relu)
+        return acts
+
+    def decode(self, acts):
+        """acts [batch, d_hidden] -> [batch, n_models, d_model] incl. b_dec (crosscoder.py:82-89)."""
+        a = self.arena()
+        acts = acts.to(self.dtype).contiguous()
+        B = acts.shape[0]
+        out = torch.empty(B, self.n_models * self.cfg["d_in"], dtype=self.dtype, device=acts.device)
+        ops.decode_fwd(acts, a.W_dec_hk, a.b_dec_flat, recon_t=out)
+        return out.view(B, self.n_models, self.cfg["d_in"])
+
+    def forward(self, x):
+        return self.decode(self.encode(x))
+
+    def get_losses(self, x):
+        """Same LossOutput as crosscoder.py:96-130; differentiable w.r.t. the four params
+        (backward runs the fused HIP backward kernels)."""
+        a = self.arena()
+        return LossOutput(*_LossFn.apply(self, x, a.data, self.W_enc, self.W_dec, self.b_enc, self.b_dec))
+
+    # ------------------------------------------------------------------ checkpoints
+    def create_save_dir(self):
+        SAVE_DIR.mkdir(parents=True, exist_ok=True)
+        versions = [int(f.name.split("_")[1]) for f in SAVE_DIR.iterdir() if "version" in str(f)]
+        version = 1 + max(versions) if versions else 0
+        self.save_dir = SAVE_DIR / f"version_{version}"
+        self.save_dir.mkdir(parents=True)
+
+    def save(self):
+        if self.save_dir is None:
+            self.create_save_dir()
+        weight_path = self.save_dir / f"{self.save_version}.pt"
+        cfg_path = self.save_dir / f"{self.save_version}_cfg.json"
+        torch.save(self.state_dict(), weight_path)
+        with open(cfg_path, "w") as f:
+            json.dump(self.cfg, f)
+        print(f"Saved as version {self.save_version} in {self.save_dir}")
+        self.save_version += 1
+
+    def _load_checked(self, state_dict):
+        self.load_state_dict(state_dict)
+        self.arena()
+
+    @classmethod
+    def load(cls, version_dir, checkpoint_version):
+        save_dir = Path("./checkpoints") / str(version_dir)
+        cfg = json.load(open(save_dir / f"{checkpoint_version}_cfg.json", "r"))
+        pprint.pprint(cfg)
+        self = cls(cfg=cfg)
+        self._load_checked(torch.load(save_dir / f"{checkpoint_version}.pt", map_location=cfg["device"],
+                                      weights_only=True))
+        return self
+
+    @classmethod
+    def load_from_path(cls, cfg_path, weights_path, device: Optional[Union[str, torch.device]] = None):
+        """Offline form of `load_from_hf` (crosscoder.py:160-205): a local cfg.json +
+        cc_weights.pt pair (no network in this framework)."""
+        with open(cfg_path, "r") as f:
+            cfg = json.load(f)
+        if device is not None:
+            cfg["device"] = str(device)
+        inst = cls(cfg)
+        inst._load_checked(torch.load(weights_path, map_location=cfg["device"], weights_only=True))
+        return inst
+
+    @classmethod
+    def load_from_hf(cls, repo_id="ckkissane/crosscoder-gemma-2-2b-model-diff", path="blocks.14.hook_resid_pre",
+                     device=None, local_dir=None):
+        """The reference downloads from the Hub; here only an already-present local copy
+        ({local_dir}/{path}/cfg.json + cc_weights.pt) is read."""
+        if local_dir is None:
+            raise RuntimeError("load_from_hf: no network; pass local_dir with {path}/cfg.json and cc_weights.pt")
+        base = Path(local_dir) / path
+        return cls.load_from_path(base / "cfg.json", base / "cc_weights.pt", device)
+
+
+class _LossFn(torch.autograd.Function):
+    """get_losses as one autograd node over the fused kernels."""
+
+    @staticmethod
+    def forward(ctx, cc, x, arena_data, W_enc, W_dec, b_enc, b_dec):
+        ws = cc._workspace(x.shape[0])
+        a = cc.arena()
+        engine.forward(ws, a, x.contiguous(), None)
+        s = ws.scalars
+        dt = cc.dtype
+        out = (s[0].clone(), s[1].to(dt, copy=True), s[2].clone(), ws.ev.clone(), ws.ev_a.to(dt, copy=True),
+               ws.ev_b.to(dt, copy=True))
+        ctx.cc = cc
+        ctx.ws = ws
+        ctx.mark_non_differentiable(out[2], out[3], out[4], out[5])
+        return out
+
+    @staticmethod
+    def backward(ctx, g_l2, g_l1, *_):
+        cc, ws = ctx.cc, ctx.ws
+        a = cc.arena()
+        w2 = 0.0 if g_l2 is None else float(g_l2)
+        w1 = 0.0 if g_l1 is None else float(g_l1)
+        if w2 != 1.0:  # g_recon was formed for d(l2)=1; re-form it for this upstream weight
+            engine.loss_from_recon(ws, a, grad_scale=2.0 * w2 / ws.B)
+        G = engine.Arena(cc.d_hidden, cc.n_models, cc.cfg["d_in"], cc.dtype, a.data.device)
+        engine.backward(ws, a, G, l1_coeff=w1)
+        v = G.views()
+        return None, None, None, v["W_enc"], v["W_dec"], v["b_enc"], v["b_dec"]

@@ -1,0 +1,92 @@
+// Shared device/host helpers for the crosscoder HIP kernels (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/crosscoder_hip.h"
+
+#define CC_DEV __device__ __forceinline__
+
+namespace cc {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) short bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef uint16_t bf16_t;  // raw bits
+
+// ---- bf16 <-> f32 (round-to-nearest-even, NaN preserving like torch) ----
+CC_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+CC_DEV bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+// Storage element type of params / activations: bf16 (CC_BF16) or fp32 (CC_F32).
+template <int DT> struct Elem;
+template <> struct Elem<CC_BF16> {
+  typedef bf16_t T;
+  static CC_DEV float load(const T* p) { return bf2f(*p); }
+  static CC_DEV float to_f(T v) { return bf2f(v); }
+  static CC_DEV T from_f(float f) { return f2bf(f); }
+  static CC_DEV float round(float f) { return bf2f(f2bf(f)); }
+};
+template <> struct Elem<CC_F32> {
+  typedef float T;
+  static CC_DEV float load(const T* p) { return *p; }
+  static CC_DEV float to_f(T v) { return v; }
+  static CC_DEV T from_f(float f) { return f; }
+  static CC_DEV float round(float f) { return f; }
+};
+
+// 8 consecutive elements as floats (16 B bf16 or 32 B fp32 vector access).
+template <int DT> CC_DEV void load8(const void* base, int64_t idx, float v[8]) {
+  if constexpr (DT == CC_BF16) {
+    bf16x8 r = *(const bf16x8*)((const bf16_t*)base + idx);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bf2f((bf16_t)r[j]);
+  } else {
+    const f32x4* p = (const f32x4*)((const float*)base + idx);
+    f32x4 a = p[0], b = p[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+  }
+}
+template <int DT> CC_DEV void store8(void* base, int64_t idx, const float v[8]) {
+  if constexpr (DT == CC_BF16) {
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(v[j]);
+    *(bf16x8*)((bf16_t*)base + idx) = r;
+  } else {
+    f32x4* p = (f32x4*)((float*)base + idx);
+    p[0] = f32x4{v[0], v[1], v[2], v[3]};
+    p[1] = f32x4{v[4], v[5], v[6], v[7]};
+  }
+}
+CC_DEV void load8f(const float* base, int64_t idx, float v[8]) {
+  const f32x4* p = (const f32x4*)(base + idx);
+  f32x4 a = p[0], b = p[1];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+}
+
+CC_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+CC_DEV double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace cc
+
+#define CC_LAUNCH_CHECK()                                \
+  do {                                                   \
+    hipError_t e__ = hipGetLastError();                  \
+    if (e__ != hipSuccess) return CC_ERR_HIP_BASE + (int)e__; \
+  } while (0)

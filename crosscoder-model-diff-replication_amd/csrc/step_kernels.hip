@@ -1,0 +1,518 @@
+// HBM-bound kernels of the crosscoder training step (gfx950): input normalisation, the
+// fused reconstruction loss + its gradient, decoder norms, deterministic slab reductions,
+// the loss/EV finalisation, clip_grad_norm_ finalisation and the fused clip+Adam update.
+// All vector accesses are 16 B per lane; every cross-block sum goes through a fixed-order
+// partial slab (bit-reproducible, no float atomics).
+#include "cc_common.h"
+
+namespace cc {
+
+constexpr int PREP_ROWS = 64;   // rows per prep block (column partial granularity)
+constexpr int LOSS_ROWS = 32;   // rows per loss block
+constexpr int LOSS_COLS = 512;  // columns per loss block (64 lanes x 8)
+
+// ---------------------------------------------------------------------------------------
+// x_out = dtype(x_in * factor[model]);  colsum_part[rb][k] = sum over the block's rows.
+// grid: (ceil(K/512), ceil(B/64)); block 256 = 4 waves; lane -> 8 columns, wave -> 16 rows.
+template <int DIN, int DF, int DT>
+__global__ __launch_bounds__(256) void prep_kernel(const void* __restrict__ x_in, const void* __restrict__ factor,
+                                                   void* __restrict__ x_out, float* __restrict__ colsum_part, int B,
+                                                   int n, int d) {
+  __shared__ float red[4][512];
+  const int K = n * d;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = blockIdx.x * 512 + lane * 8;
+  const int r0 = blockIdx.y * PREP_ROWS;
+  float cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (col < K) {
+    float f = 1.f;
+    if (factor) f = Elem<DF>::load((const typename Elem<DF>::T*)factor + col / d);
+    for (int r = r0 + wave; r < r0 + PREP_ROWS && r < B; r += 4) {
+      float v[8];
+      load8<DIN>(x_in, (int64_t)r * K + col, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = Elem<DT>::round(v[j] * f);
+      store8<DT>(x_out, (int64_t)r * K + col, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cs[j] += v[j];
+    }
+  }
+  if (!colsum_part) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = cs[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    int c = blockIdx.x * 512 + i;
+    if (c < K) colsum_part[(int64_t)blockIdx.y * K + c] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// out[j] = scale * sum_i part[i*ld + j]; optional dtype copy and squared-sum partial per block.
+template <int DT>
+__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ part, int R, int C, int64_t ld,
+                                                          float scale, float* __restrict__ out_f32,
+                                                          void* __restrict__ out_t, float* __restrict__ sq_part) {
+  __shared__ float red[4];
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  float sq = 0.f;
+  if (j < C) {
+    float s = 0.f;
+    for (int i = 0; i < R; ++i) s += part[(int64_t)i * ld + j];
+    s *= scale;
+    if (out_f32) out_f32[j] = s;
+    if (out_t) {
+      typename Elem<DT>::T q = Elem<DT>::from_f(s);
+      ((typename Elem<DT>::T*)out_t)[j] = q;
+      float vq = Elem<DT>::to_f(q);
+      sq = vq * vq;
+    }
+  }
+  if (!sq_part) return;
+  sq = wave_sum(sq);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
+  __syncthreads();
+  if (threadIdx.x == 0) sq_part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// ---------------------------------------------------------------------------------------
+// norms[h][m] = ||W_dec[h,m,:]||, total[h] = sum_m.  One wave per (h) row, all models.
+template <int DT>
+__global__ __launch_bounds__(256) void dec_norms_kernel(const void* __restrict__ W, float* __restrict__ norms,
+                                                        float* __restrict__ total, int h, int n, int d) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= h) return;
+  float tot = 0.f;
+  for (int m = 0; m < n; ++m) {
+    const int64_t base = ((int64_t)row * n + m) * d;
+    float s = 0.f;
+    for (int c = lane * 8; c < d; c += 512) {
+      float v[8];
+      load8<DT>(W, base + c, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j] * v[j];
+    }
+    s = wave_sum(s);
+    float nr = sqrtf(s);
+    if (lane == 0) norms[(int64_t)row * n + m] = nr;
+    tot += nr;
+  }
+  if (lane == 0) total[row] = tot;
+}
+
+// ---------------------------------------------------------------------------------------
+// Reconstruction loss + gradient.  grid: (n * ncb, ceil(B/32)); block 256 = 4 waves.
+// Block covers model m = blockIdx.x / ncb, columns [m*d + cb*512, +512) ∩ model, 32 rows.
+// lane -> 8 columns; wave w -> rows r0 + w + 4i.
+template <int DT>
+__global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ recon, const void* __restrict__ b_dec,
+                                                   const void* __restrict__ x, const float* __restrict__ x_mean,
+                                                   void* __restrict__ g_recon, float* __restrict__ row_part,
+                                                   float* __restrict__ col_part, float grad_scale, int B, int n,
+                                                   int d, int ncb) {
+  __shared__ float red[4][512];
+  using E = Elem<DT>;
+  const int K = n * d;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int m = blockIdx.x / ncb, cb = blockIdx.x % ncb;
+  const int jc = cb * LOSS_COLS + lane * 8;  // column within model
+  const bool cv = jc < d;
+  const int col = m * d + jc;
+  const int r0 = blockIdx.y * LOSS_ROWS;
+  float bd[8], mu[8], cs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bd[j] = mu[j] = cs[j] = 0.f;
+  if (cv) {
+    if (b_dec) load8<DT>(b_dec, col, bd);
+    if (x_mean) load8f(x_mean, col, mu);
+  }
+  const int64_t plane = (int64_t)n * ncb * B;  // row_part [2][n*ncb][B]
+  for (int i = 0; i < LOSS_ROWS / 4; ++i) {
+    const int r = r0 + wave + 4 * i;
+    if (r >= B) break;  // wave-uniform
+    float l2 = 0.f, tv = 0.f;
+    if (cv) {
+      float rv[8], xv[8], g[8];
+      load8f(recon, (int64_t)r * K + col, rv);
+      load8<DT>(x, (int64_t)r * K + col, xv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float diff = (rv[j] + bd[j]) - xv[j];
+        l2 += diff * diff;
+        float c = xv[j] - mu[j];
+        tv += c * c;
+        g[j] = E::round(grad_scale * diff);
+        cs[j] += g[j];
+      }
+      store8<DT>(g_recon, (int64_t)r * K + col, g);
+    }
+    l2 = wave_sum(l2);
+    tv = wave_sum(tv);
+    if (lane == 0) {
+      row_part[(int64_t)blockIdx.x * B + r] = l2;
+      row_part[plane + (int64_t)blockIdx.x * B + r] = tv;
+    }
+  }
+  if (!col_part) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = cs[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < LOSS_COLS; i += 256) {
+    int jj = cb * LOSS_COLS + i;
+    if (jj < d) col_part[(int64_t)blockIdx.y * K + m * d + jj] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+  }
+}
+
+// Per-row explained variances (crosscoder.py:110-121) + per-block partial sums of the row terms.
+// grid ceil(B/256), block 256. part_out[blk][4] = {sum l2_row, sum ev, sum ev_a, sum ev_b}.
+__global__ __launch_bounds__(256) void ev_kernel(const float* __restrict__ row_part, int B, int n, int ncb,
+                                                 float* __restrict__ ev, float* __restrict__ ev_a,
+                                                 float* __restrict__ ev_b, float* __restrict__ part_out) {
+  __shared__ float red[4][4];
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  float v[4] = {0, 0, 0, 0};
+  if (r < B) {
+    const int64_t plane = (int64_t)n * ncb * B;
+    const float eps = 1e-8f;
+    float l2 = 0.f, tv = 0.f, l2m[2] = {0, 0}, tvm[2] = {0, 0};
+    for (int m = 0; m < n; ++m) {
+      float a = 0.f, t = 0.f;
+      for (int cb = 0; cb < ncb; ++cb) {
+        a += row_part[(int64_t)(m * ncb + cb) * B + r];
+        t += row_part[plane + (int64_t)(m * ncb + cb) * B + r];
+      }
+      l2 += a;
+      tv += t;
+      if (m < 2) { l2m[m] = a; tvm[m] = t; }
+    }
+    float e = 1.f - l2 / (tv + eps);
+    float ea = 1.f - l2m[0] / (tvm[0] + eps);
+    float eb = n > 1 ? 1.f - l2m[1] / (tvm[1] + eps) : 0.f;
+    if (ev) ev[r] = e;
+    if (ev_a) ev_a[r] = ea;
+    if (ev_b) ev_b[r] = eb;
+    v[0] = l2; v[1] = e; v[2] = ea; v[3] = eb;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float s = wave_sum(v[q]);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    int q = threadIdx.x;
+    part_out[blockIdx.x * 4 + q] = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
+  }
+}
+
+// Single block: scalars = {l2, l1, l0, mean ev, mean ev_a, mean ev_b}.
+__global__ __launch_bounds__(256) void loss_scalars_kernel(const float* __restrict__ ev_part, int nblk,
+                                                           const float* __restrict__ l1_part,
+                                                           const float* __restrict__ l0_part, int64_t n_wave, int B,
+                                                           float* __restrict__ scalars) {
+  __shared__ double red[4][6];
+  double acc[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = threadIdx.x; i < nblk; i += 256) {
+    acc[0] += ev_part[i * 4 + 0];
+    acc[3] += ev_part[i * 4 + 1];
+    acc[4] += ev_part[i * 4 + 2];
+    acc[5] += ev_part[i * 4 + 3];
+  }
+  for (int64_t i = threadIdx.x; i < n_wave; i += 256) {
+    if (l1_part) acc[1] += l1_part[i];
+    if (l0_part) acc[2] += l0_part[i];
+  }
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    double s = wave_sum_d(acc[q]);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    int q = threadIdx.x;
+    double s = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
+    scalars[q] = (float)(s / (double)B);
+  }
+  if (threadIdx.x == 6) scalars[6] = 0.f;
+  if (threadIdx.x == 7) scalars[7] = 0.f;
+}
+
+// ---------------------------------------------------------------------------------------
+CC_DEV float bf16r(float f) { return bf2f(f2bf(f)); }
+
+struct ClipArgs {
+  const float* sq;
+  int64_t off[9];
+  int nparams;
+  float max_norm;
+  int emulate_bf16;
+  float* out;
+};
+__global__ __launch_bounds__(256) void clip_kernel(const ClipArgs a) {
+  __shared__ double red[4];
+  __shared__ float norms[8];
+  for (int p = 0; p < a.nparams; ++p) {
+    double s = 0.0;
+    for (int64_t i = a.off[p] + threadIdx.x; i < a.off[p + 1]; i += 256) s += (double)a.sq[i];
+    s = wave_sum_d(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float nr = (float)sqrt(((red[0] + red[1]) + red[2]) + red[3]);
+      if (a.emulate_bf16) nr = bf16r(nr);  // torch._foreach_norm on bf16 returns bf16
+      norms[p] = nr;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int p = 0; p < a.nparams; ++p) s += norms[p] * norms[p];
+    float total = sqrtf(s);
+    float coef;
+    if (a.emulate_bf16) {
+      total = bf16r(total);                       // vector_norm(stack(bf16 norms)) -> bf16
+      float den = bf16r(total + 1e-6f);           // bf16 tensor + python scalar
+      coef = bf16r(a.max_norm / den);
+      coef = fminf(coef, 1.f);
+    } else {
+      coef = fminf(a.max_norm / (total + 1e-6f), 1.f);
+    }
+    a.out[0] = coef;
+    a.out[1] = total;
+    for (int p = 0; p < a.nparams; ++p) a.out[2 + p] = norms[p];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused clip-multiply + Adam (torch/optim/adam.py _single_tensor_adam, no wd/amsgrad), with the
+// dtype rounding after each of torch's tensor ops:
+//   g = R(g*coef); m = R(lerp(m, g, 1-b1)); v = R(R(v*b2) + (1-b2)*g*g);
+//   den = R(R(R(sqrt v) / bc2s) + eps); p = R(p + (-step_size) * (m / den))
+struct AdamArgs {
+  void* p;
+  const void* g;
+  void* m;
+  void* v;
+  int64_t numel;
+  const float* coef;
+  float w1;         // 1 - beta1 (lerp weight)
+  float beta2, omb2, eps;
+  float bc2s;       // sqrt(1 - beta2^t)
+  float neg_step;   // -lr / (1 - beta1^t)
+};
+template <int DT>
+__global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
+  using E = Elem<DT>;
+  const float coef = a.coef ? *a.coef : 1.f;
+  const int64_t stride = (int64_t)gridDim.x * 256 * 8;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8; i < a.numel; i += stride) {
+    float p[8], g[8], m[8], v[8];
+    const bool full = i + 8 <= a.numel;
+    if (full) {
+      load8<DT>(a.p, i, p); load8<DT>(a.g, i, g); load8<DT>(a.m, i, m); load8<DT>(a.v, i, v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        int64_t k = i + j < a.numel ? i + j : a.numel - 1;
+        p[j] = E::load((const typename E::T*)a.p + k);
+        g[j] = E::load((const typename E::T*)a.g + k);
+        m[j] = E::load((const typename E::T*)a.m + k);
+        v[j] = E::load((const typename E::T*)a.v + k);
+      }
+    }
+    // torch's CPU/GPU kernels: lerp is an fma (Lerp.h vectorised path), every other op is a
+    // separately rounded fp32 multiply/add -> no contraction here.
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma clang fp contract(off)
+      float gj = E::round(g[j] * coef);
+      float w = a.w1;
+      float mj = w < 0.5f ? __builtin_fmaf(w, gj - m[j], m[j]) : __builtin_fmaf(-(gj - m[j]), 1.f - w, gj);
+      mj = E::round(mj);
+      float vj = E::round(v[j] * a.beta2);
+      vj = E::round(vj + a.omb2 * gj * gj);
+      float den = E::round(sqrtf(vj));
+      den = E::round(den / a.bc2s);
+      den = E::round(den + a.eps);
+      float pj = E::round(p[j] + a.neg_step * (mj / den));
+      p[j] = pj; m[j] = mj; v[j] = vj;
+    }
+    if (full) {
+      store8<DT>(a.p, i, p); store8<DT>(a.m, i, m); store8<DT>(a.v, i, v);
+    } else {
+      for (int j = 0; j < 8 && i + j < a.numel; ++j) {
+        ((typename E::T*)a.p)[i + j] = E::from_f(p[j]);
+        ((typename E::T*)a.m)[i + j] = E::from_f(m[j]);
+        ((typename E::T*)a.v)[i + j] = E::from_f(v[j]);
+      }
+    }
+  }
+}
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace cc
+
+using namespace cc;
+
+#define DISPATCH_DT(dtype, KERNEL_CALL)                                   \
+  do {                                                                    \
+    if ((dtype) == CC_BF16) { constexpr int DT_ = CC_BF16; KERNEL_CALL; } \
+    else if ((dtype) == CC_F32) { constexpr int DT_ = CC_F32; KERNEL_CALL; } \
+    else return CC_ERR_DTYPE;                                             \
+  } while (0)
+
+extern "C" {
+
+int cc_version(void) { return 100; }
+
+const char* cc_strerror(int code) {
+  switch (code) {
+    case CC_OK: return "ok";
+    case CC_ERR_NULL: return "crosscoder_hip: required pointer is NULL";
+    case CC_ERR_DTYPE: return "crosscoder_hip: unsupported dtype (expected CC_BF16 or CC_F32)";
+    case CC_ERR_SHAPE: return "crosscoder_hip: unsupported shape (d_model and dict_size must be multiples of 8)";
+    case CC_ERR_ALIGN: return "crosscoder_hip: pointer or leading dimension not 16-byte aligned";
+    case CC_ERR_TOO_LARGE: return "crosscoder_hip: operand panel exceeds 2 GiB buffer-descriptor range";
+    default: break;
+  }
+  if (code >= CC_ERR_HIP_BASE) return hipGetErrorString((hipError_t)(code - CC_ERR_HIP_BASE));
+  return "crosscoder_hip: unknown error";
+}
+
+int64_t cc_prep_part_rows(int64_t B) { return (B + PREP_ROWS - 1) / PREP_ROWS; }
+int64_t cc_loss_part_rows(int64_t B) { return (B + LOSS_ROWS - 1) / LOSS_ROWS; }
+int64_t cc_loss_col_blocks(int64_t d) { return (d + LOSS_COLS - 1) / LOSS_COLS; }
+int64_t cc_loss_scalars_len(int64_t B) { return 8 + 4 * ((B + 255) / 256); }
+
+int cc_prep_input(const void* x_in, int in_dtype, const void* factor, int factor_dtype, void* x_out,
+                  float* colsum_part, int64_t B, int64_t n, int64_t d, int dtype, void* stream) {
+  if (!x_in || !x_out) return CC_ERR_NULL;
+  if (B <= 0 || n <= 0 || d <= 0 || d % 8) return CC_ERR_SHAPE;
+  if (!al16(x_in) || !al16(x_out)) return CC_ERR_ALIGN;
+  if (factor && factor_dtype != CC_BF16 && factor_dtype != CC_F32) return CC_ERR_DTYPE;
+  if (in_dtype != CC_BF16 && in_dtype != CC_F32) return CC_ERR_DTYPE;
+  dim3 grid((unsigned)((n * d + 511) / 512), (unsigned)cc_prep_part_rows(B));
+  hipStream_t st = (hipStream_t)stream;
+#define PREP(DI, DF, DO) \
+  hipLaunchKernelGGL((prep_kernel<DI, DF, DO>), grid, dim3(256), 0, st, x_in, factor, x_out, colsum_part, (int)B, (int)n, (int)d)
+  int fdt = factor ? factor_dtype : CC_F32;
+  if (dtype != CC_BF16 && dtype != CC_F32) return CC_ERR_DTYPE;
+  if (in_dtype == CC_BF16) {
+    if (fdt == CC_BF16) { if (dtype == CC_BF16) PREP(CC_BF16, CC_BF16, CC_BF16); else PREP(CC_BF16, CC_BF16, CC_F32); }
+    else { if (dtype == CC_BF16) PREP(CC_BF16, CC_F32, CC_BF16); else PREP(CC_BF16, CC_F32, CC_F32); }
+  } else {
+    if (fdt == CC_BF16) { if (dtype == CC_BF16) PREP(CC_F32, CC_BF16, CC_BF16); else PREP(CC_F32, CC_BF16, CC_F32); }
+    else { if (dtype == CC_BF16) PREP(CC_F32, CC_F32, CC_BF16); else PREP(CC_F32, CC_F32, CC_F32); }
+  }
+#undef PREP
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+int cc_reduce_rows(const float* part, int64_t R, int64_t C, int64_t ld, float scale, float* out_f32, void* out_t,
+                   int dtype, float* sq_part, void* stream) {
+  if (!part) return CC_ERR_NULL;
+  if (R <= 0 || C <= 0) return CC_ERR_SHAPE;
+  if (sq_part && !out_t) return CC_ERR_NULL;
+  dim3 grid((unsigned)((C + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+  if (out_t) {
+    DISPATCH_DT(dtype, hipLaunchKernelGGL((reduce_rows_kernel<DT_>), grid, dim3(256), 0, st, part, (int)R, (int)C, ld,
+                                          scale, out_f32, out_t, sq_part));
+  } else {
+    hipLaunchKernelGGL((reduce_rows_kernel<CC_F32>), grid, dim3(256), 0, st, part, (int)R, (int)C, ld, scale, out_f32,
+                       nullptr, nullptr);
+  }
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+int cc_dec_norms(const void* W_dec, float* norms, float* total, int64_t h, int64_t n, int64_t d, int dtype,
+                 void* stream) {
+  if (!W_dec || !norms || !total) return CC_ERR_NULL;
+  if (h <= 0 || n <= 0 || d <= 0 || d % 8) return CC_ERR_SHAPE;
+  if (!al16(W_dec)) return CC_ERR_ALIGN;
+  dim3 grid((unsigned)((h + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_DT(dtype, hipLaunchKernelGGL((dec_norms_kernel<DT_>), grid, dim3(256), 0, st, W_dec, norms, total, (int)h,
+                                        (int)n, (int)d));
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+int cc_loss_fwd_bwd(const float* recon_f32, const void* b_dec, const void* x, const float* x_mean, void* g_recon,
+                    float* row_part, float* col_part, float grad_scale, int64_t B, int64_t n, int64_t d, int dtype,
+                    void* stream) {
+  if (!recon_f32 || !x || !g_recon || !row_part) return CC_ERR_NULL;
+  if (B <= 0 || n <= 0 || d <= 0 || d % 8) return CC_ERR_SHAPE;
+  if (!al16(recon_f32) || !al16(x) || !al16(g_recon) || (b_dec && !al16(b_dec)) || (x_mean && !al16(x_mean)))
+    return CC_ERR_ALIGN;
+  int ncb = (int)cc_loss_col_blocks(d);
+  dim3 grid((unsigned)(n * ncb), (unsigned)cc_loss_part_rows(B));
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_DT(dtype, hipLaunchKernelGGL((loss_kernel<DT_>), grid, dim3(256), 0, st, recon_f32, b_dec, x, x_mean,
+                                        g_recon, row_part, col_part, grad_scale, (int)B, (int)n, (int)d, ncb));
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+int cc_loss_finalize(const float* row_part, const float* l1_part, const float* l0_part, int64_t n_wave, float* ev,
+                     float* ev_a, float* ev_b, float* scalars, int64_t B, int64_t n, int64_t d, void* stream) {
+  if (!row_part || !scalars) return CC_ERR_NULL;
+  if (B <= 0 || n <= 0 || d <= 0) return CC_ERR_SHAPE;
+  // the per-block partials of the row terms use the tail of `scalars` (cc_loss_scalars_len)
+  int ncb = (int)cc_loss_col_blocks(d);
+  int nblk = (int)((B + 255) / 256);
+  float* ev_part = scalars + 8;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(ev_kernel, dim3(nblk), dim3(256), 0, st, row_part, (int)B, (int)n, ncb, ev, ev_a, ev_b, ev_part);
+  hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(256), 0, st, ev_part, nblk, l1_part, l0_part, n_wave, (int)B,
+                     scalars);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+int cc_clip_finalize(const float* sq, const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* out,
+                     void* stream) {
+  if (!sq || !off || !out) return CC_ERR_NULL;
+  if (nparams <= 0 || nparams > 8) return CC_ERR_SHAPE;
+  ClipArgs a = {};
+  a.sq = sq;
+  for (int i = 0; i <= nparams; ++i) a.off[i] = off[i];
+  a.nparams = nparams;
+  a.max_norm = max_norm;
+  a.emulate_bf16 = emulate_bf16;
+  a.out = out;
+  hipLaunchKernelGGL(clip_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, a);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, float lr, float beta1,
+                 float beta2, float eps, int64_t step, int dtype, void* stream) {
+  if (!p || !g || !m || !v) return CC_ERR_NULL;
+  if (numel <= 0 || step <= 0) return CC_ERR_SHAPE;
+  if (!al16(p) || !al16(g) || !al16(m) || !al16(v)) return CC_ERR_ALIGN;
+  AdamArgs a = {};
+  a.p = p; a.g = g; a.m = m; a.v = v; a.numel = numel; a.coef = coef;
+  // host-side scalars in double, as torch computes them from python floats (adam.py)
+  double b1 = beta1, b2 = beta2;
+  a.w1 = (float)(1.0 - b1);
+  a.beta2 = beta2;
+  a.omb2 = (float)(1.0 - b2);
+  a.eps = eps;
+  double bc1 = 1.0 - pow(b1, (double)step), bc2 = 1.0 - pow(b2, (double)step);
+  a.bc2s = (float)sqrt(bc2);
+  a.neg_step = (float)(-((double)lr / bc1));
+  int64_t work = (numel + 7) / 8;
+  int64_t blocks = (work + 255) / 256;
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_DT(dtype, hipLaunchKernelGGL((adam_kernel<DT_>), dim3((unsigned)blocks), dim3(256), 0, st, a));
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,162 @@
+"""The crosscoder training step as a fixed sequence of HIP launches over resident HBM buffers.
+
+Data layout in HBM (one arena per role, all views of single allocations):
+  params  [ W_enc h-major [h][K] | W_dec [h][K] | b_enc [h] | b_dec [K] ]   (dtype)
+  grads   same layout (dtype)        exp_avg / exp_avg_sq   same layout (dtype)
+  x [B][K], acts [B][h], g_recon [B][K], g_pre [B][h] (dtype); recon [B][K] fp32.
+W_enc's logical shape is [n, d, h] with strides (d, 1, K) exactly like the reference's
+rearranged view (crosscoder.py:55-58), so both weight matrices are [h][K] row-major and
+every GEMM streams 128-byte rows.
+
+Step (reference trainer.py:41-63 -> crosscoder.py:96-130 -> autograd -> clip -> Adam):
+  prep      x = dtype(buf * factor), column sums for x.mean(0)             buffer.py:124, crosscoder.py:99
+  norms     ||W_dec[h,m]||, sum over m                                     crosscoder.py:123-125
+  G1        acts = relu(x W_enc + b_enc) (+ l1/l0/colsum partials)         crosscoder.py:69-80,126,128
+  G2        recon = acts W_dec  (fp32)                                     crosscoder.py:82-89
+  loss      r = recon + b_dec; g_recon = 2(r-x)/B; l2/tv row terms          crosscoder.py:104-121
+  finalize  l2, l1, l0, EV vectors and means                               crosscoder.py:106-128
+  G3        g_pre = (g_recon W_dec^T + l1c tn/B) * (acts>0)                 autograd
+  G4        dW_dec = acts^T g_recon + l1c/B colsum(acts) W_dec/||W_dec||    autograd
+  G5        dW_enc = g_pre^T x                                              autograd
+  bias      db_enc = colsum(g_pre), db_dec = colsum(g_recon)               autograd
+  clip      coef = min(1, 1/(||g||+1e-6))                                  trainer.py:46
+  adam      fused over the whole arena                                     trainer.py:47
+"""
+import contextlib
+
+import torch
+
+from . import ops
+
+# Optional per-launch timer (bench.py installs one): an object with .span(name) -> context
+# manager recording HIP events on torch's current stream around the launch.
+TIMER = None
+
+
+def _span(name):
+    return TIMER.span(name) if TIMER is not None else contextlib.nullcontext()
+
+
+class Arena:
+    """Flat storage for the four parameters (or their grads / Adam moments)."""
+
+    def __init__(self, h, n, d, dtype, device, data=None):
+        self.h, self.n, self.d = h, n, d
+        K = n * d
+        self.K = K
+        self.numel = 2 * h * K + h + K
+        self.data = data if data is not None else torch.zeros(self.numel, dtype=dtype, device=device)
+        o = 0
+        self.W_enc_hk = self.data[o:o + h * K].view(h, K)
+        o += h * K
+        self.W_dec_hk = self.data[o:o + h * K].view(h, K)
+        o += h * K
+        self.b_enc = self.data[o:o + h]
+        o += h
+        self.b_dec_flat = self.data[o:o + K]
+
+    # reference-shaped views
+    def W_enc(self):  # [n, d, h], strides (d, 1, K)
+        return self.W_enc_hk.view(self.h, self.n, self.d).permute(1, 2, 0)
+
+    def W_dec(self):  # [h, n, d]
+        return self.W_dec_hk.view(self.h, self.n, self.d)
+
+    def b_dec(self):  # [n, d]
+        return self.b_dec_flat.view(self.n, self.d)
+
+    def views(self):
+        return {"W_enc": self.W_enc(), "W_dec": self.W_dec(), "b_enc": self.b_enc, "b_dec": self.b_dec()}
+
+    def param_sizes(self):
+        """numel of W_enc, W_dec, b_enc, b_dec (the reference's parameters() order)."""
+        hk = self.h * self.K
+        return [hk, hk, self.h, self.K]
+
+
+class StepWorkspace:
+    """All activations / partial-sum slabs of one step, allocated once per (B, shape, dtype)."""
+
+    def __init__(self, B, n, d, h, dtype, device):
+        f32 = torch.float32
+        K = n * d
+        self.B, self.n, self.d, self.h, self.K, self.dtype = B, n, d, h, K, dtype
+        E = lambda *s, dt=f32: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
+        self.x = E(B, K, dt=dtype)
+        self.x_colpart = E(ops.prep_part_rows(B), K)
+        self.x_mean = E(K)
+        self.norms = E(h, n)
+        self.tn = E(h)
+        self.acts = E(B, h, dt=dtype)
+        self.acts_colpart = E(ops.col_part_rows(B), h)
+        self.colsum_acts = E(h)
+        self.n_wave = ops.wave_parts(B, h)
+        self.l1_part = E(self.n_wave)
+        self.l0_part = E(self.n_wave)
+        self.recon = E(B, K)
+        self.g_recon = E(B, K, dt=dtype)
+        self.ncb = ops.loss_col_blocks(d)
+        self.row_part = E(2, n * self.ncb, B)
+        self.loss_colpart = E(ops.loss_part_rows(B), K)
+        self.ev = E(B)
+        self.ev_a = E(B)
+        self.ev_b = E(B)
+        self.scalars = E(ops.loss_scalars_len(B))
+        self.g_pre = E(B, h, dt=dtype)
+        self.gpre_colpart = E(ops.col_part_rows(B), h)
+        nw_w = ops.wave_parts(h, K)
+        sizes = [nw_w, nw_w, (h + 255) // 256, (K + 255) // 256]
+        self.sq_off = [0]
+        for s in sizes:
+            self.sq_off.append(self.sq_off[-1] + s)
+        self.sq = E(self.sq_off[-1])
+        self.clip_out = E(8)
+
+    def sq_slice(self, i):
+        return self.sq[self.sq_off[i]:self.sq_off[i + 1]]
+
+
+def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True):
+    """Forward + reconstruction-loss gradient.  P: params Arena.  x_in [B, n, d] any of
+    fp32/bf16, factor [n] or None.  Leaves losses in ws.scalars / ws.ev*, g_recon ready."""
+    B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
+    ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart)
+    ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
+    ops.dec_norms(P.W_dec_hk, h, n, d, norms=ws.norms, total=ws.tn)
+    with _span("G1_encode"):
+        ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, tn=ws.tn, colsum_part=ws.acts_colpart,
+                       l1_part=ws.l1_part, l0_part=ws.l0_part)
+    with _span("G2_decode"):
+        ops.decode_fwd(ws.acts, P.W_dec_hk, None, recon_f32=ws.recon)
+    return loss_from_recon(ws, P, grad_scale)
+
+
+def loss_from_recon(ws, P, grad_scale=None):
+    B, n, d = ws.B, ws.n, ws.d
+    gs = 2.0 / B if grad_scale is None else grad_scale
+    ops.loss_fwd_bwd(ws.recon, P.b_dec_flat, ws.x, ws.x_mean, ws.g_recon, ws.row_part, ws.loss_colpart, gs, B, n, d)
+    ops.loss_finalize(ws.row_part, ws.l1_part, ws.l0_part, ws.n_wave, ws.ev, ws.ev_a, ws.ev_b, ws.scalars, B, n, d)
+
+
+def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0):
+    """Gradients of l2 + l1_coeff * l1 into the grads Arena G (+ squared-sum partials)."""
+    B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
+    l1_scale = float(l1_coeff) * l1_grad_weight / B
+    with _span("G3_dacts"):
+        ops.dacts_bwd(ws.g_recon, P.W_dec_hk, ws.acts, ws.tn, l1_scale, ws.g_pre, colsum_part=ws.gpre_colpart)
+    if l1_scale != 0.0:
+        ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts)
+    with _span("G4_wgrad_dec"):
+        ops.wgrad_dec(ws.acts, ws.g_recon, P.W_dec_hk, ws.norms, ws.colsum_acts, l1_scale, G.W_dec_hk,
+                      ws.sq_slice(1), n, d)
+    with _span("G5_wgrad_enc"):
+        ops.wgrad_enc(ws.g_pre, ws.x, G.W_enc_hk, ws.sq_slice(0))
+    ops.reduce_rows(ws.gpre_colpart, ws.gpre_colpart.shape[0], h, out_t=G.b_enc, sq_part=ws.sq_slice(2))
+    ops.reduce_rows(ws.loss_colpart, ws.loss_colpart.shape[0], K, out_t=G.b_dec_flat, sq_part=ws.sq_slice(3))
+
+
+def clip_and_adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, max_norm=1.0):
+    emulate = ws.dtype == torch.bfloat16
+    ops.clip_finalize(ws.sq, ws.sq_off, max_norm, emulate, ws.clip_out)
+    with _span("adam"):
+        ops.adam_step(P.data, G.data, M.data, V.data, ws.clip_out[0:1], lr, beta1, beta2, eps, step)

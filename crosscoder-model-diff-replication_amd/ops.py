@@ -1,0 +1,171 @@
+"""Tensor-level wrappers over the C ABI (include/crosscoder_hip.h).
+
+Every function takes torch tensors that already live on a ROCm device, checks shapes on
+the host, and launches on torch's current stream.  Nothing here computes on the CPU.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import CC_BF16, CC_F32, CC_LAYOUT_KC, CC_LAYOUT_MN
+
+_DT = {torch.bfloat16: CC_BF16, torch.float32: CC_F32}
+
+
+def dtype_code(dtype):
+    try:
+        return _DT[dtype]
+    except KeyError:
+        raise TypeError(f"crosscoder_amd supports bf16 and fp32 storage, got {dtype}") from None
+
+
+def lib():
+    return _lib.load()
+
+
+def _stream(t):
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"crosscoder_amd kernels run on a ROCm GPU; got a tensor on {t.device} "
+            "(the CPU restatement lives in oracle/ and is test-only)")
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _contig(t, name):
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if t.data_ptr() % 16:
+        raise ValueError(f"{name} must be 16-byte aligned")
+    return t
+
+
+def check(rc):
+    _lib.check(rc)
+
+
+# ---------------------------------------------------------------- sizing helpers
+def col_part_rows(M):
+    return int(lib().cc_col_part_rows(M))
+
+
+def wave_parts(M, N):
+    return int(lib().cc_wave_parts(M, N))
+
+
+def prep_part_rows(B):
+    return int(lib().cc_prep_part_rows(B))
+
+
+def loss_part_rows(B):
+    return int(lib().cc_loss_part_rows(B))
+
+
+def loss_col_blocks(d):
+    return int(lib().cc_loss_col_blocks(d))
+
+
+def loss_scalars_len(B):
+    return int(lib().cc_loss_scalars_len(B))
+
+
+# ---------------------------------------------------------------- kernels
+def gemm_f32out(A, a_layout, Bm, b_layout, M, N, K, out=None):
+    """Generic MFMA GEMM (test/diagnostic): see cc_gemm_f32out."""
+    lda = A.shape[-1]
+    ldb = Bm.shape[-1]
+    if out is None:
+        out = torch.empty(M, N, device=A.device, dtype=torch.float32)
+    check(lib().cc_gemm_f32out(_ptr(A), a_layout, lda, _ptr(Bm), b_layout, ldb, _ptr(out), out.shape[-1],
+                               M, N, K, dtype_code(A.dtype), _stream(A)))
+    return out
+
+
+def prep_input(x_in, factor, dtype, out=None, colsum_part=None):
+    """x_out[B, n*d] = dtype(x_in * factor[model]) (Buffer.next normalisation + get_losses cast)."""
+    B, n, d = x_in.shape
+    _contig(x_in, "x")
+    if out is None:
+        out = torch.empty(B, n * d, device=x_in.device, dtype=dtype)
+    fdt = dtype_code(factor.dtype) if factor is not None else CC_F32
+    check(lib().cc_prep_input(_ptr(x_in), dtype_code(x_in.dtype), _ptr(factor), fdt, _ptr(out),
+                              _ptr(colsum_part), B, n, d, dtype_code(dtype), _stream(x_in)))
+    return out
+
+
+def reduce_rows(part, R, C, scale=1.0, out_f32=None, out_t=None, sq_part=None, ld=None):
+    dt = dtype_code(out_t.dtype) if out_t is not None else CC_F32
+    check(lib().cc_reduce_rows(_ptr(part), R, C, C if ld is None else ld, scale, _ptr(out_f32), _ptr(out_t),
+                               dt, _ptr(sq_part), _stream(part)))
+
+
+def dec_norms(W_dec_hk, h, n, d, norms=None, total=None):
+    if norms is None:
+        norms = torch.empty(h, n, device=W_dec_hk.device, dtype=torch.float32)
+    if total is None:
+        total = torch.empty(h, device=W_dec_hk.device, dtype=torch.float32)
+    check(lib().cc_dec_norms(_ptr(W_dec_hk), _ptr(norms), _ptr(total), h, n, d, dtype_code(W_dec_hk.dtype),
+                             _stream(W_dec_hk)))
+    return norms, total
+
+
+def encode_fwd(x, W_enc_hk, b_enc, acts, apply_relu=True, tn=None, colsum_part=None, l1_part=None,
+               l0_part=None):
+    B, K = x.shape
+    h = W_enc_hk.shape[0]
+    check(lib().cc_encode_fwd(_ptr(x), _ptr(W_enc_hk), _ptr(b_enc), _ptr(tn), _ptr(acts), int(apply_relu),
+                              _ptr(colsum_part), _ptr(l1_part), _ptr(l0_part), B, K, h, dtype_code(x.dtype),
+                              _stream(x)))
+    return acts
+
+
+def decode_fwd(acts, W_dec_hk, b_dec=None, recon_f32=None, recon_t=None):
+    B, h = acts.shape
+    K = W_dec_hk.shape[1]
+    check(lib().cc_decode_fwd(_ptr(acts), _ptr(W_dec_hk), _ptr(b_dec), _ptr(recon_f32), _ptr(recon_t), B, h, K,
+                              dtype_code(acts.dtype), _stream(acts)))
+
+
+def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_scale, B, n, d):
+    check(lib().cc_loss_fwd_bwd(_ptr(recon_f32), _ptr(b_dec), _ptr(x), _ptr(x_mean), _ptr(g_recon), _ptr(row_part),
+                                _ptr(col_part), grad_scale, B, n, d, dtype_code(x.dtype), _stream(x)))
+
+
+def loss_finalize(row_part, l1_part, l0_part, n_wave, ev, ev_a, ev_b, scalars, B, n, d):
+    check(lib().cc_loss_finalize(_ptr(row_part), _ptr(l1_part), _ptr(l0_part), n_wave, _ptr(ev), _ptr(ev_a),
+                                 _ptr(ev_b), _ptr(scalars), B, n, d, _stream(row_part)))
+
+
+def dacts_bwd(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre, colsum_part=None):
+    B, K = g_recon.shape
+    h = W_dec_hk.shape[0]
+    check(lib().cc_dacts_bwd(_ptr(g_recon), _ptr(W_dec_hk), _ptr(acts), _ptr(tn), l1_scale, _ptr(g_pre),
+                             _ptr(colsum_part), B, K, h, dtype_code(g_recon.dtype), _stream(g_recon)))
+
+
+def wgrad_dec(acts, g_recon, W_dec_hk, norms, colsum_acts, l1_scale, grad, sq_part, n, d):
+    B, h = acts.shape
+    check(lib().cc_wgrad_dec(_ptr(acts), _ptr(g_recon), _ptr(W_dec_hk), _ptr(norms), _ptr(colsum_acts), l1_scale,
+                             _ptr(grad), _ptr(sq_part), B, h, n, d, dtype_code(acts.dtype), _stream(acts)))
+
+
+def wgrad_enc(g_pre, x, grad, sq_part):
+    B, h = g_pre.shape
+    K = x.shape[1]
+    check(lib().cc_wgrad_enc(_ptr(g_pre), _ptr(x), _ptr(grad), _ptr(sq_part), B, h, K, dtype_code(g_pre.dtype),
+                             _stream(g_pre)))
+
+
+def clip_finalize(sq, offsets, max_norm, emulate_bf16, out):
+    arr = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
+    check(lib().cc_clip_finalize(_ptr(sq), arr, len(offsets) - 1, max_norm, int(emulate_bf16), _ptr(out),
+                                 _stream(sq)))
+
+
+def adam_step(p, g, m, v, coef, lr, beta1, beta2, eps, step):
+    check(lib().cc_adam_step(_ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(coef), lr, beta1, beta2, eps,
+                             int(step), dtype_code(p.dtype), _stream(p)))

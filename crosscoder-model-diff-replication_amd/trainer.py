@@ -1,0 +1,143 @@
+"""Drop-in `Trainer` (reference: trainer.py:7-82) whose `step()` is the fused HIP step.
+
+`step()` returns the reference's 9-key loss dict.  Per step it issues the fixed launch
+sequence of engine.py on one stream and copies the 6 loss scalars to the host once (the
+reference does 7 `.item()` syncs).  Adam state (exp_avg / exp_avg_sq, bf16 like the
+reference's) lives in arenas mirroring the parameter arena, exposed through
+`optimizer.state[param]` for inspection.
+"""
+import torch
+import tqdm
+
+from . import engine
+from .buffer import Buffer
+from .crosscoder import CrossCoder
+
+
+class FusedAdam:
+    """State holder with torch.optim.Adam's observable surface (param_groups, state)."""
+
+    def __init__(self, cc, lr, betas, eps=1e-8):
+        a = cc.arena()
+        self.cc = cc
+        self.exp_avg = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
+        self.exp_avg_sq = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
+        self.grads = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
+        self.param_groups = [{"lr": lr, "initial_lr": lr, "betas": betas, "eps": eps, "weight_decay": 0.0}]
+        self.t = 0
+
+    @property
+    def state(self):
+        m, v = self.exp_avg.views(), self.exp_avg_sq.views()
+        st = {}
+        for name in ("W_enc", "W_dec", "b_enc", "b_dec"):
+            p = getattr(self.cc, name)
+            st[p] = {"step": torch.tensor(float(self.t)), "exp_avg": m[name], "exp_avg_sq": v[name]}
+        return st
+
+    def zero_grad(self, set_to_none=True):
+        pass  # grads are overwritten (never accumulated) by the backward kernels
+
+
+class LambdaLRHost:
+    """torch.optim.lr_scheduler.LambdaLR over one group, evaluated on the host."""
+
+    def __init__(self, optimizer, lr_lambda):
+        self.optimizer = optimizer
+        self.lr_lambda = lr_lambda
+        self.base_lr = optimizer.param_groups[0]["initial_lr"]
+        self.last_epoch = 0
+        optimizer.param_groups[0]["lr"] = self.base_lr * lr_lambda(0)
+        self._last_lr = [optimizer.param_groups[0]["lr"]]
+
+    def step(self):
+        self.last_epoch += 1
+        lr = self.base_lr * self.lr_lambda(self.last_epoch)
+        self.optimizer.param_groups[0]["lr"] = lr
+        self._last_lr = [lr]
+
+    def get_last_lr(self):
+        return list(self._last_lr)
+
+
+class Trainer:
+    def __init__(self, cfg, model_A=None, model_B=None, all_tokens=None, buffer=None, crosscoder=None, logger=None):
+        self.cfg = cfg
+        self.model_A = model_A
+        self.model_B = model_B
+        self.crosscoder = crosscoder if crosscoder is not None else CrossCoder(cfg)
+        self.buffer = buffer if buffer is not None else Buffer(cfg, model_A, model_B, all_tokens)
+        self.total_steps = cfg["num_tokens"] // cfg["batch_size"]
+        self.optimizer = FusedAdam(self.crosscoder, cfg["lr"], (cfg["beta1"], cfg["beta2"]))
+        self.scheduler = LambdaLRHost(self.optimizer, self.lr_lambda)
+        self.step_counter = 0
+        self.logger = logger
+
+    def lr_lambda(self, step):
+        if step < 0.8 * self.total_steps:
+            return 1.0
+        return 1.0 - (step - 0.8 * self.total_steps) / (0.2 * self.total_steps)
+
+    def get_l1_coeff(self):
+        if self.step_counter < 0.05 * self.total_steps:
+            return self.cfg["l1_coeff"] * self.step_counter / (0.05 * self.total_steps)
+        return self.cfg["l1_coeff"]
+
+    def step_async(self):
+        """Launch one full step; returns the device scalars tensor (no host sync)."""
+        cc = self.crosscoder
+        raw, factor = self.buffer.next_raw()
+        ws = cc._workspace(raw.shape[0])
+        P = cc.arena()
+        opt = self.optimizer
+        engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None)
+        l1c = self.get_l1_coeff()
+        engine.backward(ws, P, opt.grads, l1c)
+        g = opt.param_groups[0]
+        opt.t += 1
+        b1, b2 = g["betas"]
+        engine.clip_and_adam(ws, P, opt.grads, opt.exp_avg, opt.exp_avg_sq, g["lr"], b1, b2, g["eps"], opt.t)
+        self.scheduler.step()
+        self._last_l1c = l1c
+        return ws.scalars
+
+    def step(self):
+        scalars = self.step_async()
+        l1c = self._last_l1c
+        s = scalars[:6].tolist()  # the step's single device->host copy
+        dt = self.crosscoder.dtype
+        rd = (lambda v: float(torch.tensor(v, dtype=dt))) if dt != torch.float32 else float
+        l2, l1, l0 = s[0], rd(s[1]), s[2]
+        loss_dict = {
+            "loss": l2 + l1c * l1,
+            "l2_loss": l2,
+            "l1_loss": l1,
+            "l0_loss": l0,
+            "l1_coeff": l1c,
+            "lr": self.scheduler.get_last_lr()[0],
+            "explained_variance": s[3],
+            "explained_variance_A": rd(s[4]),
+            "explained_variance_B": rd(s[5]),
+        }
+        self.step_counter += 1
+        return loss_dict
+
+    def log(self, loss_dict):
+        if self.logger is not None:
+            self.logger(loss_dict, self.step_counter)
+        print(loss_dict)
+
+    def save(self):
+        self.crosscoder.save()
+
+    def train(self):
+        self.step_counter = 0
+        try:
+            for i in tqdm.trange(self.total_steps):
+                loss_dict = self.step()
+                if i % self.cfg["log_every"] == 0:
+                    self.log(loss_dict)
+                if (i + 1) % self.cfg["save_every"] == 0:
+                    self.save()
+        finally:
+            self.save()

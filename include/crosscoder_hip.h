@@ -1,0 +1,154 @@
+/* crosscoder_hip.h — C ABI of libcrosscoder_hip.so (gfx950 / MI355X).
+ *
+ * The drop-in boundary for ONE crosscoder training step (fwd + bwd + grad-clip + Adam) of
+ * mitroitskii/crosscoder-model-diff-replication.  The reference has no FFI: its "operators"
+ * are the torch calls inside CrossCoder / Trainer.  Each entry point below names the
+ * reference code it replaces (file:line under the reference tree).
+ *
+ * Conventions
+ *  - Every pointer is a DEVICE pointer (hipMalloc / torch tensor .data_ptr()), 16-byte aligned,
+ *    row-major, rows contiguous.  The library never allocates or frees caller memory.
+ *  - `dtype` selects the storage type of params / activations / grads: CC_BF16 or CC_F32
+ *    (the reference's cfg["enc_dtype"] "bf16" / "fp32", crosscoder.py:12,30).
+ *    All accumulations are fp32 (bf16 inputs go through bf16 MFMA with fp32 accumulate,
+ *    fp32 inputs through the exact-f32 MFMA).
+ *  - Shapes: B batch rows, n models, d d_model, h dict_size, K = n*d.
+ *    Requirements: d % 8 == 0, h % 8 == 0 (16-byte vector rows); any B >= 1.
+ *  - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream); all launches are
+ *    asynchronous on it.  No entry point synchronises, allocates, or keeps global state.
+ *  - Return value: 0 = CC_OK, else a CC_ERR_* code (>= CC_ERR_HIP_BASE: hipError_t + base).
+ *    cc_strerror() maps it to a message.
+ *  - Partial-sum slabs ("*_part") are caller-allocated fp32 workspaces whose sizes come from
+ *    cc_col_part_rows() / cc_wave_parts(); they make every reduction deterministic
+ *    (fixed summation order, no float atomics).
+ */
+#ifndef CROSSCODER_HIP_H
+#define CROSSCODER_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CC_BF16 1
+#define CC_F32 2
+
+#define CC_LAYOUT_KC 0 /* operand stored with the contraction index contiguous   */
+#define CC_LAYOUT_MN 1 /* operand stored with the M (or N) index contiguous      */
+
+enum {
+  CC_OK = 0,
+  CC_ERR_NULL = 1,
+  CC_ERR_DTYPE = 2,
+  CC_ERR_SHAPE = 3,
+  CC_ERR_ALIGN = 4,
+  CC_ERR_TOO_LARGE = 5,
+  CC_ERR_HIP_BASE = 1000
+};
+
+int cc_version(void);
+const char* cc_strerror(int code);
+
+/* Workspace sizing.  Column-partial slabs written by GEMM epilogues have
+ * cc_col_part_rows(M) rows of N floats; per-wave scalar partials have cc_wave_parts(M, N)
+ * floats.  Row-block slabs of the elementwise kernels: cc_prep_part_rows(B) x K and
+ * cc_loss_part_rows(B) x K; loss row stats: 2 * n * cc_loss_col_blocks(d) x B. */
+int64_t cc_col_part_rows(int64_t M);
+int64_t cc_wave_parts(int64_t M, int64_t N);
+int64_t cc_prep_part_rows(int64_t B);
+int64_t cc_loss_part_rows(int64_t B);
+int64_t cc_loss_col_blocks(int64_t d);
+int64_t cc_loss_scalars_len(int64_t B); /* floats in the `scalars` buffer of cc_loss_finalize */
+
+/* Generic MFMA GEMM, fp32 output: C[M,N] = sum_k A(m,k) B(k,n).
+ * a_layout KC: A at A[m*lda+k]; MN: A at A[k*lda+m].  b_layout KC: B at B[n*ldb+k];
+ * MN: B at B[k*ldb+n].  (Test/diagnostic entry; the fused entries below use the same kernel.) */
+int cc_gemm_f32out(const void* A, int a_layout, int64_t lda, const void* Bm, int b_layout, int64_t ldb,
+                   float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, int dtype, void* stream);
+
+/* Buffer.next normalisation + CrossCoder.get_losses cast (buffer.py:115-124, crosscoder.py:99):
+ * x_out[b, m*d+j] = dtype( float(x_in[b,m,j]) * float(factor[m]) ), factor may be NULL (=1).
+ * in_dtype / factor_dtype in {CC_BF16, CC_F32}.  colsum_part (optional): per 64-row block
+ * column sums of x_out -> reduced by cc_reduce_rows into x.mean(0) (crosscoder.py:112). */
+int cc_prep_input(const void* x_in, int in_dtype, const void* factor, int factor_dtype, void* x_out,
+                  float* colsum_part, int64_t B, int64_t n, int64_t d, int dtype, void* stream);
+
+/* out[j] = scale * sum_{i<R} part[i*ld + j] (fixed order).  Optional: out_f32, out_t (dtype),
+ * sq_part (per 256-column block: sum of dtype-rounded out^2, for clip_grad_norm_). */
+int cc_reduce_rows(const float* part, int64_t R, int64_t C, int64_t ld, float scale, float* out_f32,
+                   void* out_t, int dtype, float* sq_part, void* stream);
+
+/* W_dec.norm(dim=-1) and its sum over models (crosscoder.py:123-125):
+ * norms[h*n + m] = ||W_dec[h,m,:]||_2, total[h] = sum_m norms.  fp32 results. */
+int cc_dec_norms(const void* W_dec, float* norms, float* total, int64_t h, int64_t n, int64_t d, int dtype,
+                 void* stream);
+
+/* CrossCoder.encode (crosscoder.py:69-80): acts[B,h] = act(x[B,K] . W_enc + b_enc), W_enc stored
+ * h-major [h][K] (its physical layout, crosscoder.py:55-58).  act = ReLU if apply_relu.
+ * Optional fused side outputs (NULL to skip), all from the dtype-rounded acts:
+ *   colsum_part [cc_col_part_rows(B) x h]  column sums  (-> sum_b acts, for dL1/dW_dec)
+ *   l1_part     [cc_wave_parts(B,h)]        sum acts*tn  (l1_loss numerator, crosscoder.py:126)
+ *   l0_part     [cc_wave_parts(B,h)]        count acts>0 (l0_loss numerator, crosscoder.py:128) */
+int cc_encode_fwd(const void* x, const void* W_enc, const void* b_enc, const float* tn, void* acts,
+                  int apply_relu, float* colsum_part, float* l1_part, float* l0_part, int64_t B, int64_t K,
+                  int64_t h, int dtype, void* stream);
+
+/* CrossCoder.decode (crosscoder.py:82-89): recon = acts[B,h] . W_dec[h][K] (+ b_dec).
+ * recon_f32 (optional): fp32 [B][K]; b_dec NULL -> partial sum without bias (latent-sharded use).
+ * recon_t (optional): dtype [B][K] = dtype(acc + b_dec). */
+int cc_decode_fwd(const void* acts, const void* W_dec, const void* b_dec, float* recon_f32, void* recon_t,
+                  int64_t B, int64_t h, int64_t K, int dtype, void* stream);
+
+/* get_losses reconstruction terms + their backward (crosscoder.py:104-121, autograd):
+ * r = recon_f32 + b_dec; g_recon = dtype(grad_scale * (r - x)) with grad_scale = 2/B.
+ * row_part [2][n*cc_loss_col_blocks(d)][B]: [0] sum (r-x)^2, [1] sum (x - x_mean)^2 per
+ * (model, column block, row).  col_part [cc_loss_part_rows(B)][K]: column sums of g_recon. */
+int cc_loss_fwd_bwd(const float* recon_f32, const void* b_dec, const void* x, const float* x_mean,
+                    void* g_recon, float* row_part, float* col_part, float grad_scale, int64_t B, int64_t n,
+                    int64_t d, int dtype, void* stream);
+
+/* Loss reduction (crosscoder.py:106-128, trainer.py:51-61): per-row explained variances
+ * ev/ev_a/ev_b [B] (fp32) and scalars[0:8] = {l2, l1, l0, mean ev, mean ev_a, mean ev_b, 0, 0};
+ * `scalars` holds cc_loss_scalars_len(B) floats (the tail is workspace).
+ * l1_part / l0_part: the per-wave partials of cc_encode_fwd (n_wave entries each), scaled
+ * by 1/B (NULL -> 0). */
+int cc_loss_finalize(const float* row_part, const float* l1_part, const float* l0_part, int64_t n_wave,
+                     float* ev, float* ev_a, float* ev_b, float* scalars, int64_t B, int64_t n, int64_t d,
+                     void* stream);
+
+/* Backward through decode + L1 + ReLU (autograd of crosscoder.py:77,84-89,126):
+ * g_pre[B,h] = (g_recon . W_dec^T + l1_scale * tn[h]) * (acts > 0),  l1_scale = l1_coeff / B.
+ * colsum_part [cc_col_part_rows(B) x h]: column sums of g_pre (-> b_enc.grad). */
+int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
+                 void* g_pre, float* colsum_part, int64_t B, int64_t K, int64_t h, int dtype, void* stream);
+
+/* W_dec.grad [h][K] = acts^T . g_recon + l1_scale * sum_b(acts[:,h]) * W_dec[h,m,:]/||W_dec[h,m,:]||
+ * (norm backward is 0 where the norm is 0).  sq_part [cc_wave_parts(h,K)]: sum of grad^2. */
+int cc_wgrad_dec(const void* acts, const void* g_recon, const void* W_dec, const float* norms,
+                 const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_part, int64_t B,
+                 int64_t h, int64_t n, int64_t d, int dtype, void* stream);
+
+/* W_enc.grad, h-major [h][K] (the param's physical layout) = g_pre^T . x.  sq_part as above. */
+int cc_wgrad_enc(const void* g_pre, const void* x, void* grad_W_enc, float* sq_part, int64_t B, int64_t h,
+                 int64_t K, int dtype, void* stream);
+
+/* clip_grad_norm_(params, max_norm) (trainer.py:46; torch/nn/utils/clip_grad.py): per-param
+ * norms from the squared-sum partials sq[off[i] .. off[i+1]) (nparams <= 8, off on the HOST),
+ * total = ||(norm_i)||, coef = min(1, max_norm / (total + 1e-6)).  emulate_bf16 rounds the
+ * intermediate norms/coef to bf16 as torch does for bf16 grads.
+ * out[0] = coef, out[1] = total norm, out[2 + i] = norm_i  (fp32, device). */
+int cc_clip_finalize(const float* sq, const int64_t* off, int nparams, float max_norm, int emulate_bf16,
+                     float* out, void* stream);
+
+/* torch.optim.Adam step (trainer.py:16-20,47; torch/optim/adam.py single-tensor path, no weight
+ * decay / amsgrad) fused with the clip multiply: g' = dtype(g * coef[0]); m, v, p updated in place
+ * over `numel` flat elements; step = the Adam step count AFTER increment; lr from LambdaLR.
+ * dtype-rounding between torch's ops is reproduced (bf16 state like the reference). */
+int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, float lr,
+                 float beta1, float beta2, float eps, int64_t step, int dtype, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

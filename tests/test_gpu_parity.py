@@ -1,0 +1,306 @@
+"""GPU parity: the HIP path (through the C-ABI library) against the oracle and the
+reference's golden fixtures.
+
+Tolerance contract (BASELINE.json north_star):
+  * fp32 mode: relative Frobenius error <= 2e-5 vs an fp64 evaluation of the same inputs;
+    the active set (acts > 0) and, on the dyadic known-answer test, pre/acts/recon/l0 are
+    bit-exact.
+  * bf16 mode: every tensor's error vs fp64 is at most 2x the reference's own bf16 error
+    (computed here from the fixture) plus a floor of 2e-3; active-set flips <= 0.2 %.
+"""
+import math
+
+import pytest
+import torch
+
+import crosscoder_amd as ca
+from crosscoder_amd import engine, ops
+from oracle import cpu_reference as O
+from tests._golden import load, step_fixtures
+
+pytestmark = pytest.mark.gpu
+
+STEP_FIXTURES = step_fixtures()
+FIXTURES_2 = [f for f in STEP_FIXTURES if "_n2_" in f]
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return (a - b).norm().item() / max(b.norm().item(), 1e-30)
+
+
+def truth_fp64(x, P, l1c):
+    """fp64 evaluation (oracle math) on the exact same (dtype-rounded) inputs."""
+    dt = P["W_dec"].dtype
+    P64 = {k: v.detach().to(torch.float64).clone().requires_grad_(True) for k, v in P.items()}
+    x64 = x.to(dt).to(torch.float64)
+    lo = O.get_losses(x64, P64, torch.float64)
+    (lo["l2_loss"] + l1c * lo["l1_loss"]).backward()
+    with torch.no_grad():
+        pre = O.encode(x64, P64, apply_relu=False)
+    return lo, {k: P64[k].grad for k in O.PARAM_ORDER}, pre
+
+
+def envelope_ok(ours, ref, truth, floor=2e-3):
+    e_ours, e_ref = rel(ours, truth), rel(ref, truth)
+    return e_ours <= 2 * e_ref + floor, (e_ours, e_ref)
+
+
+def make_cc(cfg, P, device, n_models):
+    cfg = dict(cfg, device=str(device))
+    cc = ca.CrossCoder(cfg, n_models=n_models)
+    cc.load_state_dict({k: v for k, v in P.items()})
+    return cc
+
+
+# ----------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(256, 256, 64), (296, 520, 72), (96, 200, 80), (512, 768, 1000)])
+@pytest.mark.parametrize("layouts", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_layouts(gpu, dtype, shape, layouts):
+    M, N, K = shape
+    al, bl = layouts
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, generator=g).to(dtype)  # logical A[m][k]
+    Bm = torch.randn(K, N, generator=g).to(dtype)  # logical B[k][n]
+    A_st = A.contiguous() if al == 0 else A.t().contiguous()
+    B_st = Bm.t().contiguous() if bl == 0 else Bm.contiguous()
+    C = ops.gemm_f32out(A_st.to(gpu), al, B_st.to(gpu), bl, M, N, K)
+    torch.cuda.synchronize()
+    ref = A.double() @ Bm.double()
+    assert rel(C, ref) < 1e-5
+
+
+# ----------------------------------------------------------------------------- forward
+@pytest.mark.parametrize("name", STEP_FIXTURES)
+def test_forward_parity(gpu, name):
+    r = load(name)
+    cfg, P, x = r["cfg"], r["init"], r["x"][0]
+    n = r["n_models"]
+    dt = O.DTYPES[cfg["enc_dtype"]]
+    cc = make_cc(cfg, P, gpu, n)
+    xg = x.to(gpu)
+    with torch.no_grad():
+        acts = cc.encode(xg.to(dt)).cpu()
+        pre = cc.encode(xg.to(dt), apply_relu=False).cpu()
+        recon = cc.decode(acts.to(gpu)).cpu()
+        lo = cc.get_losses(xg)
+    torch.cuda.synchronize()
+    tlo, _, tpre = truth_fp64(x, P, 0.0)
+    fw = r["fwd"]
+    if dt == torch.float32:
+        assert rel(pre, tpre) < 2e-5
+        assert rel(recon, fw["recon"]) < 2e-5
+        # active set bit-exact outside a 1e-5 guard band around 0 (fp32 rounding of the sum)
+        band = tpre.abs() > 1e-5 * tpre.abs().max()
+        assert torch.equal((acts > 0)[band], (fw["acts"] > 0)[band])
+        assert band.float().mean().item() > (0.99 if "dyadic" in name else 0.999)
+        for k in ("l2_loss", "l1_loss", "l0_loss", "explained_variance"):
+            assert rel(getattr(lo, k), tlo[k]) < 2e-5, k
+    else:
+        ok, e = envelope_ok(pre, fw["pre"], tpre)
+        assert ok, ("pre", e)
+        flips = ((acts > 0) != (tpre > 0)).float().mean().item()
+        assert flips <= 2e-3
+        for k in ("l2_loss", "l1_loss", "explained_variance", "explained_variance_A", "explained_variance_B"):
+            ok, e = envelope_ok(getattr(lo, k).float(), fw[k].float(), tlo[k])
+            assert ok, (k, e)
+        assert abs(lo.l0_loss.item() - fw["l0_loss"].item()) <= 2e-3 * cfg["dict_size"] + 1
+    for k in ("l2_loss", "l1_loss", "l0_loss", "explained_variance", "explained_variance_A", "explained_variance_B"):
+        assert getattr(lo, k).dtype == fw[k].dtype, k
+        assert getattr(lo, k).shape == fw[k].shape, k
+
+
+def test_dyadic_known_answer_bit_exact(gpu):
+    """Dyadic data: every fp32 sum is exact, so the GPU must match the reference bit for bit."""
+    r = load("dyadic_b64_n2_d32_h128_fp32")
+    cc = make_cc(r["cfg"], r["init"], gpu, 2)
+    xg = r["x"][0].to(gpu)
+    with torch.no_grad():
+        pre = cc.encode(xg, apply_relu=False).cpu()
+        acts = cc.encode(xg).cpu()
+        recon = cc.decode(acts.to(gpu)).cpu()
+        lo = cc.get_losses(xg)
+    fw = r["fwd"]
+    assert torch.equal(pre, fw["pre"])
+    assert torch.equal(acts, fw["acts"])
+    assert torch.equal(recon, fw["recon"])
+    assert torch.equal(lo.l0_loss.cpu(), fw["l0_loss"])
+    assert torch.equal(lo.l2_loss.cpu(), fw["l2_loss"])
+
+
+# ----------------------------------------------------------------------------- backward
+@pytest.mark.parametrize("name", STEP_FIXTURES)
+def test_backward_parity(gpu, name):
+    r = load(name)
+    cfg, P, x = r["cfg"], r["init"], r["x"][0]
+    dt = O.DTYPES[cfg["enc_dtype"]]
+    cc = make_cc(cfg, P, gpu, r["n_models"])
+    lo = cc.get_losses(x.to(gpu))
+    (lo.l2_loss + 2.0 * lo.l1_loss).backward()
+    torch.cuda.synchronize()
+    _, tg, _ = truth_fp64(x, P, 2.0)
+    for k in O.PARAM_ORDER:
+        g = getattr(cc, k).grad
+        ref = r["grads_l1c2"][k]
+        assert g.shape == ref.shape and g.dtype == ref.dtype and g.stride() == ref.stride(), k
+        if dt == torch.float32:
+            assert rel(g, tg[k]) < 2e-5, (k, rel(g, tg[k]))
+        else:
+            ok, e = envelope_ok(g, ref, tg[k], floor=5e-3)
+            assert ok, (k, e)
+
+
+# ----------------------------------------------------------------------------- trainer
+class _Replay:
+    normalize = True
+
+    def __init__(self, bufs, factors, device):
+        self.bufs = [b.to(device) for b in bufs]
+        self.factors = [f.to(device) for f in factors]
+        self.i = 0
+
+    def next_raw(self):
+        b, f = self.bufs[self.i], self.factors[self.i]
+        self.i += 1
+        return b, f
+
+
+@pytest.mark.parametrize("name", FIXTURES_2)
+def test_trainer_steps(gpu, name):
+    r = load(name)
+    cfg = dict(r["cfg"], device=str(gpu))
+    dt = O.DTYPES[cfg["enc_dtype"]]
+    cc = make_cc(cfg, r["init"], gpu, r["n_models"])
+    tr = ca.Trainer(cfg, buffer=_Replay(r["buf"], r["factor"], gpu), crosscoder=cc)
+    steps = len(r["x"])
+    tol = 2e-5 if dt == torch.float32 else 2e-2
+    for s in range(steps):
+        d = tr.step()
+        ref = r["steps"]["loss_dicts"][s]
+        assert d.keys() == ref.keys()
+        assert d["l1_coeff"] == ref["l1_coeff"] and d["lr"] == ref["lr"]
+        for k in ("l2_loss", "l1_loss", "explained_variance"):
+            assert math.isclose(d[k], ref[k], rel_tol=tol, abs_tol=tol), (s, k, d[k], ref[k])
+        assert abs(d["l0_loss"] - ref["l0_loss"]) <= (1e-6 if dt == torch.float32 else 2e-3 * cfg["dict_size"] + 1)
+    last = r["steps"]["after"][steps - 1]
+    lr = cfg["lr"]
+    for k in O.PARAM_ORDER:
+        p = getattr(cc, k).detach().cpu().float()
+        ref = last["params"][k].float()
+        ulp = ref.abs().max().item() * (2 ** -7 if dt == torch.bfloat16 else 2 ** -22)
+        assert (p - ref).abs().max().item() <= 2 * lr * steps + 2 * ulp, k
+
+
+# ----------------------------------------------------------------------------- adam / clip
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_adam_matches_torch(gpu, dtype):
+    g = torch.Generator().manual_seed(3)
+    n = 100003
+    p = (torch.randn(n, generator=g) * 0.05).to(dtype)
+    gr = (torch.randn(n, generator=g) * 1e-3).to(dtype)
+    m = (torch.randn(n, generator=g) * 1e-4).to(dtype)
+    v = (torch.rand(n, generator=g) * 1e-6).to(dtype)
+    coef = torch.tensor([0.5])
+    step, lr = 7, 5e-5
+    # reference: clip multiply then Adam (trainer.py:46-47)
+    pr, gref, mr, vr = p.clone(), gr.clone(), m.clone(), v.clone()
+    gref.mul_(coef.to(dtype))
+    O.adam_update(pr, gref, mr, vr, float(step), lr, 0.9, 0.999, 1e-8)
+    pg, gg, mg, vg = (t.to(gpu) for t in (p, gr, m, v))
+    ops.adam_step(pg, gg, mg, vg, coef.to(gpu), lr, 0.9, 0.999, 1e-8, step)
+    torch.cuda.synchronize()
+    for ours, ref in ((pg, pr), (mg, mr), (vg, vr)):
+        ours = ours.cpu()
+        if dtype == torch.float32:
+            assert rel(ours, ref) < 1e-6
+        else:
+            exact = (ours == ref).float().mean().item()
+            assert exact > 0.999, exact
+            ulp = ref.float().abs() * 2 ** -7 + 1e-30
+            assert ((ours.float() - ref.float()).abs() <= ulp).all()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_clip_matches_torch(gpu, dtype):
+    g = torch.Generator().manual_seed(5)
+    grads = [torch.randn(s, generator=g).to(dtype) for s in (1000, 3000, 16, 40)]
+    total = O.clip_grad_norm([t.clone() for t in grads])
+    sq = torch.cat([t.float().pow(2) for t in grads]).to(gpu)
+    off = [0]
+    for t in grads:
+        off.append(off[-1] + t.numel())
+    out = torch.empty(8, device=gpu)
+    ops.clip_finalize(sq, off, 1.0, dtype == torch.bfloat16, out)
+    torch.cuda.synchronize()
+    assert math.isclose(out[1].item(), total.float().item(), rel_tol=1e-6 if dtype == torch.float32 else 8e-3)
+    coef = min(1.0, 1.0 / (total.float().item() + 1e-6))
+    assert math.isclose(out[0].item(), coef, rel_tol=1e-6 if dtype == torch.float32 else 8e-3)
+
+
+# ----------------------------------------------------------------------------- full size
+@pytest.fixture(scope="module")
+def full_size_case():
+    B, n, d, h = 4096, 2, 2304, 16384
+    cfg = {"seed": 49, "dict_size": h, "d_in": d, "enc_dtype": "bf16", "dec_init_norm": 0.08, "device": "cpu"}
+    P = O.init_params(cfg)
+    g = torch.Generator().manual_seed(0)
+    raw = torch.randn(B, n, d, generator=g) * torch.tensor([1 / 0.2759, 1 / 0.2442])[None, :, None]
+    buf = raw.to(torch.bfloat16)
+    factor = torch.tensor([(d ** 0.5) / buf[:, i].float().norm(dim=-1).mean().item() for i in range(n)]).to(
+        torch.bfloat16)
+    x = O.buffer_next(buf, factor)
+    return cfg, P, buf, factor, x
+
+
+def test_full_size_config2_bf16(gpu, full_size_case):
+    """BASELINE config 2 (2x2304->16384, batch 4096, bf16): one fwd+bwd vs the oracle in fp32
+    on the same bf16-valued inputs (fp32 stands in for fp64 at this size)."""
+    cfg, P, buf, factor, x = full_size_case
+    cc = make_cc(cfg, P, gpu, 2)
+    ws = cc._workspace(buf.shape[0])
+    a = cc.arena()
+    G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+    engine.forward(ws, a, buf.to(gpu), factor.to(gpu))
+    engine.backward(ws, a, G, l1_coeff=2.0)
+    torch.cuda.synchronize()
+    acts_ours = ws.acts.cpu()
+    x_ours = ws.x.cpu()
+    # oracle in fp32 on the same rounded inputs
+    torch.set_num_threads(max(1, torch.get_num_threads()))
+    P32 = {k: v.float().clone().requires_grad_(True) for k, v in P.items()}
+    x32 = x.to(torch.bfloat16).float()
+    assert torch.equal(x_ours.float().view_as(x32), x32)
+    lo = O.get_losses(x32, P32, torch.float32)
+    (lo["l2_loss"] + 2.0 * lo["l1_loss"]).backward()
+    with torch.no_grad():
+        pre32 = O.encode(x32, P32, apply_relu=False)
+    flips = ((acts_ours > 0) != (pre32 > 0)).float().mean().item()
+    assert flips <= 2e-3, flips
+    s = ws.scalars[:6].cpu()
+    assert math.isclose(s[0].item(), lo["l2_loss"].item(), rel_tol=1e-2)
+    assert math.isclose(s[1].item(), lo["l1_loss"].item(), rel_tol=1e-2)
+    assert abs(s[2].item() - lo["l0_loss"].item()) <= 2e-3 * cfg["dict_size"]
+    assert math.isclose(s[3].item(), lo["explained_variance"].mean().item(), rel_tol=1e-2, abs_tol=1e-2)
+    Gv = G.views()
+    bounds = {"W_enc": 1e-1, "W_dec": 1e-2, "b_enc": 1e-2, "b_dec": 1e-2}
+    for k in O.PARAM_ORDER:
+        e = rel(Gv[k].cpu(), P32[k].grad)
+        assert e <= bounds[k], (k, e)
+
+
+def test_full_size_step_deterministic(gpu, full_size_case):
+    """Two identical fused steps produce bit-identical params (no atomics anywhere)."""
+    cfg, P, buf, factor, _ = full_size_case
+    outs = []
+    for _ in range(2):
+        cc = make_cc(dict(cfg, batch_size=4096, num_tokens=4096 * 100, lr=5e-5, beta1=0.9, beta2=0.999,
+                          l1_coeff=2), P, gpu, 2)
+        tr = ca.Trainer(dict(cc.cfg), buffer=_Replay([buf, buf], [factor, factor], gpu), crosscoder=cc)
+        d0 = tr.step()
+        d1 = tr.step()
+        torch.cuda.synchronize()
+        outs.append((d0, d1, cc.arena().data.clone()))
+    assert outs[0][0] == outs[1][0] and outs[0][1] == outs[1][1]
+    assert torch.equal(outs[0][2], outs[1][2])
+    assert outs[0][1]["l2_loss"] < outs[0][0]["l2_loss"]
