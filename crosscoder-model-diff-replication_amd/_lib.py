@@ -19,6 +19,7 @@ _p = ctypes.c_void_p
 _i64 = ctypes.c_int64
 _i = ctypes.c_int
 _f = ctypes.c_float
+_d = ctypes.c_double
 
 # name -> (restype, argtypes); must list every symbol of include/crosscoder_hip.h
 SIGNATURES = {
@@ -26,6 +27,7 @@ SIGNATURES = {
     "cc_strerror": (ctypes.c_char_p, [_i]),
     "cc_col_part_rows": (_i64, [_i64]),
     "cc_wave_parts": (_i64, [_i64, _i64]),
+    "cc_wgrad_parts": (_i64, [_i64, _i64, _i]),
     "cc_prep_part_rows": (_i64, [_i64]),
     "cc_loss_part_rows": (_i64, [_i64]),
     "cc_loss_col_blocks": (_i64, [_i64]),
@@ -42,7 +44,7 @@ SIGNATURES = {
     "cc_wgrad_dec": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_enc": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_clip_finalize": (_i, [_p, ctypes.POINTER(_i64), _i, _f, _i, _p, _p]),
-    "cc_adam_step": (_i, [_p, _p, _p, _p, _i64, _p, _f, _f, _f, _f, _i64, _i, _p]),
+    "cc_adam_step": (_i, [_p, _p, _p, _p, _i64, _p, _d, _d, _d, _d, _i64, _i, _p]),
 }
 
 _lib = None

@@ -7,27 +7,29 @@
 //   G4 dW_dec   [h][K]      = acts^T . g_recon + norm-grad term      A:MN  B:MN
 //   G5 dW_enc   [h][K]      = g_pre^T . x                            A:MN  B:MN
 //
-// Geometry: 256x256 output tile per 512-thread workgroup (8 waves = 2 per SIMD, 2(M) x 4(N)),
-// each wave 128x64 = 8x4 tiles of v_mfma_f32_16x16x32_bf16 (bf16) or v_mfma_f32_16x16x4_f32
-// (fp32 mode, exact-f32 MFMA).  K-step: 64 bf16 / 32 fp32 elements = 128 B per KC row, so
-// every operand tile is 32 KB; two stages (A+B) = 128 KB of the CU's 160 KB LDS.
-// Staging is LDS-DMA (buffer_load ... lds, 16 B per lane) through a buffer descriptor whose
-// range check zero-fills out-of-range lanes (M/N/K tails: the offset is pushed past the
-// descriptor's record count).  The LDS image is lane-linear per 1 KB wave-instruction, so the
-// bank-conflict swizzle lives in the per-lane SOURCE address and the matching read address:
-//   KC tile  [256 rows][8 x 16 B chunks]:   phys chunk = chunk ^ (row & 7)        (ds_read_b128)
-//   MN tile  [k rows][rows/8 x 16 B chunks]: phys chunk = chunk ^ f(k)            (ds_read_b64_tr_b16)
+// Geometry: 512-thread workgroups (8 waves = 2 per SIMD), output tile 256 x BN with
+//   BN = 256: waves 2(M) x 4(N), 128 x 64 per wave (8 x 4 MFMA tiles)
+//   BN = 288: waves 4(M) x 2(N),  64 x 144 per wave (4 x 9 MFMA tiles) -- used when N = n*d is a
+//             multiple of 288 (n*2304 at the Gemma-2-2b width): 4096 x 4608 -> exactly 256 tiles.
+// MFMA: v_mfma_f32_16x16x32_bf16 (bf16) / v_mfma_f32_16x16x4_f32 (fp32 mode, exact f32), issued
+// with the operands swapped (B fragment as src A) so each lane's 4 accumulator registers are 4
+// CONSECUTIVE output columns of one row: 8-16 B vector epilogue loads/stores.
+// K-step: 64 bf16 / 32 fp32 elements = 128 B per KC row.  Two LDS stages (A+B).
+// Staging is LDS-DMA (buffer_load ... lds, 16 B per lane) through buffer descriptors whose range
+// check zero-fills out-of-range lanes (M/N/K tails: the offset is pushed past the record count).
+// The LDS image is lane-linear per 1 KB wave-instruction, so the bank-conflict swizzle lives in
+// the per-lane SOURCE address and the matching read address:
+//   KC tile [rows][8 x 16 B]:   phys chunk = chunk ^ (row & 7)                  (ds_read_b128)
+//   MN tile [k][cols]:          phys chunk = (chunk + rot(k)) mod chunks/row      (ds_read_b64_tr_b16
+//                               bf16 / ds_read_b32 fp32), rot chosen conflict-free per geometry.
 // One s_barrier per K-step: wait own DMA (vmcnt 0) -> barrier -> issue DMA of step t+1 into the
-// other stage -> MFMA on stage t.  All LDS is one __shared__ array (no vmcnt(0) before ds_read).
+// other stage -> MFMA on stage t.  All LDS is one __shared__ array.
 #include "cc_common.h"
 
 namespace cc {
 
-constexpr int BM = 256, BN = 256, NTHR = 512;
-constexpr int TILE_BYTES = 256 * 128;           // one operand tile per stage
-constexpr int STAGE_BYTES = 2 * TILE_BYTES;     // A + B
-constexpr int LDS_BYTES = 2 * STAGE_BYTES;      // 128 KB
-constexpr uint32_t OOB = 0x7ffffff0u;           // voffset that the range check always rejects
+constexpr int BM = 256, NTHR = 512;
+constexpr uint32_t OOB = 0x7ffffff0u;  // voffset that the range check always rejects
 constexpr uint32_t MAX_RECORDS = 0x7fffffe0u;
 
 enum Epi { EPI_F32 = 0, EPI_ENC = 1, EPI_DEC = 2, EPI_DACTS = 3, EPI_WGDEC = 4, EPI_WGENC = 5 };
@@ -47,7 +49,7 @@ struct GemmArgs {
   const void* w_src;    // W_dec (EPI_WGDEC), indexed like out
   const float* norms;   // [h][n]
   const float* colsum;  // [h] sum_b acts
-  float* col_part;      // [2*nbm][N]
+  float* col_part;      // [nbm * WARPS_M][N]
   float* wave_part0;    // [nbm*nbn*8]
   float* wave_part1;
   float scale0;
@@ -67,95 +69,113 @@ CC_DEV void dma16(__amdgpu_buffer_rsrc_t r, char* lds_base, uint32_t voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_base, 16, (int)voff, 0, 0, 0);
 }
 
-// MN-tile swizzle (16-B chunk index XOR, depends on the k row); conflict-free for the
-// ds_read_b64_tr_b16 fragment reads of the 16x16x32 operands (bf16), and for the fp32
-// ds_read_b32 reads (toggles 64 B by k row bit 2).
-CC_DEV int mn_swz_bf16(int k) { return 2 * ((k & 3) | ((k >> 1) & 4)); }
-CC_DEV int mn_swz_f32(int k) { return ((k >> 2) & 1) << 2; }
+// ---- MN-tile geometry: [BK k rows][COLS columns], row bytes RB, CH 16-B chunks per row ----
+template <int DT, int COLS>
+struct MnTile {
+  static constexpr int ES = DT == CC_BF16 ? 2 : 4;
+  static constexpr int EPC = 16 / ES;                 // elements per chunk
+  static constexpr int BK = DT == CC_BF16 ? 64 : 32;
+  static constexpr int RB = COLS * ES;
+  static constexpr int CH = RB / 16;
+  static constexpr int BYTES = BK * RB;
+  static constexpr int NDMA = BYTES / 1024;
+  // chunk rotation per k row: conflict-free fragment reads (checked exhaustively offline for
+  // the 16x16x32 bf16 / 16x16x4 f32 read patterns of both column counts)
+  static CC_DEV int rot(int k) {
+    if constexpr (DT == CC_BF16) {
+      if constexpr (COLS == 256) return 2 * ((k & 3) | ((k >> 1) & 4));
+      else return 2 * ((k >> 3) & 1);
+    } else {
+      return 4 * ((k >> 2) & 1);
+    }
+  }
+};
 
-// ---- global -> LDS staging of one operand tile (4 x 1 KB DMA per thread) ----
-// KC: tile rows = the operand's M (or N) rows [row0, row0+256), 128 B of contraction each.
-template <int DT>
+// ---- global -> LDS staging ----
+// KC: tile rows [row0, row0+ROWS), 128 B of contraction each; 1 KB DMA = 8 rows.
+template <int DT, int ROWS>
 CC_DEV void stage_kc(__amdgpu_buffer_rsrc_t r, char* lds, int rows_left, int k0, int K, int64_t ld, int wave,
                      int lane) {
-  constexpr int EPC = DT == CC_BF16 ? 8 : 4;  // elements per 16-B chunk
+  constexpr int EPC = DT == CC_BF16 ? 8 : 4;
   constexpr int ES = DT == CC_BF16 ? 2 : 4;
+  constexpr int NDMA = ROWS / 8;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < (NDMA + 7) / 8; ++i) {
     int ci = i * 8 + wave;
-    int row = ci * 8 + (lane >> 3);
-    int c = (lane & 7) ^ (row & 7);
-    int k = k0 + c * EPC;
-    bool ok = row < rows_left && k < K;
-    uint32_t voff = ok ? (uint32_t)(((int64_t)row * ld + k) * ES) : OOB;
-    dma16(r, lds + ci * 1024, voff);
+    if (ci < NDMA) {
+      int row = ci * 8 + (lane >> 3);
+      int c = (lane & 7) ^ (row & 7);
+      int k = k0 + c * EPC;
+      bool ok = row < rows_left && k < K;
+      uint32_t voff = ok ? (uint32_t)(((int64_t)row * ld + k) * ES) : OOB;
+      dma16(r, lds + ci * 1024, voff);
+    }
   }
 }
-// MN: tile = contraction rows [k0, k0+BK) x 256 contiguous columns [col0, col0+256).
-template <int DT>
+// MN: contraction rows [k0, k0+BK) x COLS contiguous columns, lane-linear image.
+template <int DT, int COLS>
 CC_DEV void stage_mn(__amdgpu_buffer_rsrc_t r, char* lds, int cols_left, int k0, int K, int64_t ld, int wave,
                      int lane) {
+  using G = MnTile<DT, COLS>;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < (G::NDMA + 7) / 8; ++i) {
     int ci = i * 8 + wave;
-    int k, q, col;
-    if constexpr (DT == CC_BF16) {  // 1 KB = 2 k rows of 512 B
-      k = ci * 2 + (lane >> 5);
-      q = (lane & 31) ^ mn_swz_bf16(k);
-      col = q * 8;
-    } else {  // 1 KB = 1 k row of 256 fp32
-      k = ci;
-      q = lane ^ mn_swz_f32(k);
-      col = q * 4;
+    if (ci < G::NDMA) {
+      int b = ci * 1024 + lane * 16;
+      int k = b / G::RB;
+      int cph = (b - k * G::RB) >> 4;
+      int clog = cph - G::rot(k);
+      clog += clog < 0 ? G::CH : 0;
+      int col = clog * G::EPC;
+      bool ok = (k0 + k) < K && col < cols_left;
+      uint32_t voff = ok ? (uint32_t)(((int64_t)(k0 + k) * ld + col) * G::ES) : OOB;
+      dma16(r, lds + ci * 1024, voff);
     }
-    constexpr int ES = DT == CC_BF16 ? 2 : 4;
-    bool ok = (k0 + k) < K && col < cols_left;
-    uint32_t voff = ok ? (uint32_t)(((int64_t)(k0 + k) * ld + col) * ES) : OOB;
-    dma16(r, lds + ci * 1024, voff);
   }
 }
 
-// ---- fragment reads (bf16, v_mfma_f32_16x16x32_bf16 operand maps) ----
-// lane l holds X[row = l&15][k = 8*(l>>4) + j], j = 0..7, for the 16-row tile at `row0`,
-// k half `kk` (k 0..31 or 32..63 of the step).
+// ---- fragment reads, bf16 (16x16x32 operand map: lane l holds X[r = l&15][k = 8*(l>>4) + j]) ----
 CC_DEV bf16x8 frag_kc_bf16(const char* tile, int row0, int kk, int lane) {
   int row = row0 + (lane & 15);
   int c = (lane >> 4) + 4 * kk;
-  int off = row * 128 + ((c ^ (row & 7)) << 4);
-  return *(const bf16x8*)(tile + off);
+  return *(const bf16x8*)(tile + row * 128 + ((c ^ (row & 7)) << 4));
 }
+template <int COLS>
 CC_DEV bf16x8 frag_mn_bf16(const char* tile, int col0, int kk, int lane) {
+  using G = MnTile<CC_BF16, COLS>;
   int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
-  int col = col0 + 4 * pp;
+  int clog = (col0 + 4 * pp) >> 3;
   bf16x8 out;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     int k = 32 * kk + 8 * g + 4 * t + qq;
-    int off = k * 512 + ((((col >> 3) ^ mn_swz_bf16(k))) << 4) + 8 * (pp & 1);
-    bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(tile + off));
+    int cph = clog + G::rot(k);
+    cph -= cph >= G::CH ? G::CH : 0;
+    bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(tile + k * G::RB + cph * 16 + 8 * (pp & 1)));
 #pragma unroll
     for (int e = 0; e < 4; ++e) out[4 * t + e] = v[e];
   }
   return out;
 }
-// ---- fragment reads (fp32, v_mfma_f32_16x16x4_f32: lane holds X[l&15][k = l>>4]) ----
-// The 32-k step is consumed as 8 MFMAs (kk = 0..1, e = 0..3); lane group g = l>>4 supplies
-// k = 4*(g + 4*kk) + e, the same mapping on both operands.
+// ---- fragment reads, fp32 (16x16x4: lane holds X[l&15][k = l>>4]); a 32-k step is 8 MFMAs
+// (kk = 0..1, e = 0..3), lane group g = l>>4 supplies k = 4*(g + 4*kk) + e on both operands.
 CC_DEV f32x4 frag_kc_f32(const char* tile, int row0, int kk, int lane) {
   int row = row0 + (lane & 15);
   int c = (lane >> 4) + 4 * kk;
-  int off = row * 128 + ((c ^ (row & 7)) << 4);
-  return *(const f32x4*)(tile + off);
+  return *(const f32x4*)(tile + row * 128 + ((c ^ (row & 7)) << 4));
 }
+template <int COLS>
 CC_DEV f32x4 frag_mn_f32(const char* tile, int col0, int kk, int lane) {
+  using G = MnTile<CC_F32, COLS>;
   int g = lane >> 4;
   int col = col0 + (lane & 15);
   f32x4 out;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     int k = 4 * (g + 4 * kk) + e;
-    int off = k * 1024 + ((((col >> 2) ^ mn_swz_f32(k))) << 4) + 4 * (col & 3);
-    out[e] = *(const float*)(tile + off);
+    int cph = (col >> 2) + G::rot(k);
+    cph -= cph >= G::CH ? G::CH : 0;
+    out[e] = *(const float*)(tile + k * G::RB + cph * 16 + 4 * (col & 3));
   }
   return out;
 }
@@ -176,23 +196,58 @@ CC_DEV void tile_of_block(int bid, int nbm, int nbn, int& tm, int& tn) {
   tn = w / gm;
 }
 
-template <int DT, bool AKC, bool BKC, int EPI>
+template <int BNT>
+struct WaveGeom {
+  static constexpr int WARPS_M = BNT == 256 ? 2 : 4;
+  static constexpr int WARPS_N = 8 / WARPS_M;
+  static constexpr int WTM = BM / WARPS_M;    // wave tile rows
+  static constexpr int WTN = BNT / WARPS_N;   // wave tile cols
+  static constexpr int TM = WTM / 16, TN = WTN / 16;
+};
+
+// bf16x4 / f32x4 vector access of 4 consecutive elements
+template <int DT> CC_DEV void ld4(const void* p, int64_t idx, float v[4]) {
+  if constexpr (DT == CC_BF16) {
+    bf16x4 r = *(const bf16x4*)((const bf16_t*)p + idx);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = bf2f((bf16_t)r[e]);
+  } else {
+    f32x4 r = *(const f32x4*)((const float*)p + idx);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = r[e];
+  }
+}
+template <int DT> CC_DEV void st4(void* p, int64_t idx, const float v[4]) {
+  if constexpr (DT == CC_BF16) {
+    bf16x4 r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[e] = (short)f2bf(v[e]);
+    *(bf16x4*)((bf16_t*)p + idx) = r;
+  } else {
+    *(f32x4*)((float*)p + idx) = f32x4{v[0], v[1], v[2], v[3]};
+  }
+}
+
+template <int DT, bool AKC, bool BKC, int EPI, int BNT>
 __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   using E = Elem<DT>;
-  using T = typename E::T;
+  using WG = WaveGeom<BNT>;
   constexpr int BK = DT == CC_BF16 ? 64 : 32;
   constexpr int ES = DT == CC_BF16 ? 2 : 4;
+  constexpr int A_BYTES = AKC ? BM * 128 : MnTile<DT, BM>::BYTES;
+  constexpr int B_BYTES = BKC ? BNT * 128 : MnTile<DT, BNT>::BYTES;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  static_assert(!BKC || BNT == 256, "BN=288 tiles are built for MN-contiguous B only");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
+  const int wr = wave / WG::WARPS_N, wc = wave % WG::WARPS_N;
   int tm, tn;
   tile_of_block(blockIdx.x, args.nbm, args.nbn, tm, tn);
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * BM, n0 = tn * BNT;
   const int M = args.M, N = args.N, K = args.K;
 
-  // descriptors based at the block's panel; offsets stay < 2^31 for every supported shape
   __amdgpu_buffer_rsrc_t ra, rb;
   {
     const char* a = (const char*)args.A;
@@ -214,20 +269,21 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
   }
 
   auto stage = [&](int kt, int s) {
-    char* la = smem + s * STAGE_BYTES;
-    char* lb = la + TILE_BYTES;
+    char* la = smem + s * STAGE;
+    char* lb = la + A_BYTES;
     int k0 = kt * BK;
-    if constexpr (AKC) stage_kc<DT>(ra, la, M - m0, k0, K, args.lda, wave, lane);
-    else stage_mn<DT>(ra, la, M - m0, k0, K, args.lda, wave, lane);
-    if constexpr (BKC) stage_kc<DT>(rb, lb, N - n0, k0, K, args.ldb, wave, lane);
-    else stage_mn<DT>(rb, lb, N - n0, k0, K, args.ldb, wave, lane);
+    if constexpr (AKC) stage_kc<DT, BM>(ra, la, M - m0, k0, K, args.lda, wave, lane);
+    else stage_mn<DT, BM>(ra, la, M - m0, k0, K, args.lda, wave, lane);
+    if constexpr (BKC) stage_kc<DT, BNT>(rb, lb, N - n0, k0, K, args.ldb, wave, lane);
+    else stage_mn<DT, BNT>(rb, lb, N - n0, k0, K, args.ldb, wave, lane);
   };
 
-  f32x4 acc[8][4];
+  // acc[i][j][e] = C[row = m0 + wr*WTM + 16i + (lane&15)][col = n0 + wc*WTN + 16j + 4*(lane>>4) + e]
+  f32x4 acc[WG::TM][WG::TN];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < WG::TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < WG::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (K + BK - 1) / BK;
   stage(0, 0);
@@ -235,129 +291,135 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (kt + 1 < nk) stage(kt + 1, (kt + 1) & 1);
-    const char* la = smem + (kt & 1) * STAGE_BYTES;
-    const char* lb = la + TILE_BYTES;
-    if constexpr (DT == CC_BF16) {
+    const char* la = smem + (kt & 1) * STAGE;
+    const char* lb = la + A_BYTES;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 a[8], b[4];
+    for (int kk = 0; kk < 2; ++kk) {
+      if constexpr (DT == CC_BF16) {
+        bf16x8 a[WG::TM], b[WG::TN];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-          a[i] = AKC ? frag_kc_bf16(la, wr * 128 + i * 16, kk, lane) : frag_mn_bf16(la, wr * 128 + i * 16, kk, lane);
+        for (int i = 0; i < WG::TM; ++i) {
+          const int r0 = wr * WG::WTM + i * 16;
+          a[i] = AKC ? frag_kc_bf16(la, r0, kk, lane) : frag_mn_bf16<BM>(la, r0, kk, lane);
+        }
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          b[j] = BKC ? frag_kc_bf16(lb, wc * 64 + j * 16, kk, lane) : frag_mn_bf16(lb, wc * 64 + j * 16, kk, lane);
+        for (int j = 0; j < WG::TN; ++j) {
+          const int c0 = wc * WG::WTN + j * 16;
+          b[j] = BKC ? frag_kc_bf16(lb, c0, kk, lane) : frag_mn_bf16<BNT>(lb, c0, kk, lane);
+        }
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < WG::TM; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-      }
-    } else {
+          for (int j = 0; j < WG::TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+      } else {
+        f32x4 a[WG::TM], b[WG::TN];
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        f32x4 a[8], b[4];
+        for (int i = 0; i < WG::TM; ++i) {
+          const int r0 = wr * WG::WTM + i * 16;
+          a[i] = AKC ? frag_kc_f32(la, r0, kk, lane) : frag_mn_f32<BM>(la, r0, kk, lane);
+        }
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-          a[i] = AKC ? frag_kc_f32(la, wr * 128 + i * 16, kk, lane) : frag_mn_f32(la, wr * 128 + i * 16, kk, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          b[j] = BKC ? frag_kc_f32(lb, wc * 64 + j * 16, kk, lane) : frag_mn_f32(lb, wc * 64 + j * 16, kk, lane);
+        for (int j = 0; j < WG::TN; ++j) {
+          const int c0 = wc * WG::WTN + j * 16;
+          b[j] = BKC ? frag_kc_f32(lb, c0, kk, lane) : frag_mn_f32<BNT>(lb, c0, kk, lane);
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e)
 #pragma unroll
-          for (int i = 0; i < 8; ++i)
+          for (int i = 0; i < WG::TM; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < WG::TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[j][e], a[i][e], acc[i][j], 0, 0, 0);
       }
     }
   }
 
-  // ------------------------------- epilogue (C-fragment layout) ------------------------------
-  // acc[i][j][e] = C[row = m0 + wr*128 + i*16 + 4*(lane>>4) + e][col = n0 + wc*64 + j*16 + (lane&15)]
-  const int rbase = m0 + wr * 128 + 4 * (lane >> 4);
-  const int cbase = n0 + wc * 64 + (lane & 15);
+  // ------------------------------- epilogue (transposed C fragments) -------------------------
+  const int rbase = m0 + wr * WG::WTM + (lane & 15);
+  const int cbase = n0 + wc * WG::WTN + 4 * (lane >> 4);
   const int wave_slot = blockIdx.x * 8 + wave;
+  // N % 4 == 0 (checked on the host), so a lane's 4 columns are all valid or all invalid.
 
-  if constexpr (EPI == EPI_F32) {
-    float* C = (float*)args.out;
+  if constexpr (EPI == EPI_F32 || EPI == EPI_DEC) {
+    const typename E::T* bias = (const typename E::T*)args.bias;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int col = cbase + j * 16;
+    for (int j = 0; j < WG::TN; ++j) {
+      const int col = cbase + j * 16;
       if (col >= N) continue;
+      float bc[4] = {0.f, 0.f, 0.f, 0.f};
+      if (EPI == EPI_DEC && bias) ld4<DT>(bias, col, bc);
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < WG::TM; ++i) {
+        const int row = rbase + i * 16;
+        if (row >= M) continue;
+        const int64_t o = (int64_t)row * args.ldo + col;
+        float v[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          int row = rbase + i * 16 + e;
-          if (row < M) C[(int64_t)row * args.ldo + col] = acc[i][j][e];
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bc[e];
+        if constexpr (EPI == EPI_F32) {
+          st4<CC_F32>(args.out, o, v);
+        } else {
+          if (args.out_f32) st4<CC_F32>(args.out_f32, o, v);
+          if (args.out) st4<DT>(args.out, o, v);
         }
-    }
-  } else if constexpr (EPI == EPI_DEC) {
-    const T* bias = (const T*)args.bias;
-    T* out = (T*)args.out;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int col = cbase + j * 16;
-      if (col >= N) continue;
-      float bc = bias ? E::to_f(bias[col]) : 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          int row = rbase + i * 16 + e;
-          if (row >= M) continue;
-          float v = acc[i][j][e] + bc;
-          int64_t o = (int64_t)row * args.ldo + col;
-          if (args.out_f32) args.out_f32[o] = v;
-          if (out) out[o] = E::from_f(v);
-        }
+      }
     }
   } else if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
-    const T* bias = (const T*)args.bias;
-    const T* mask = (const T*)args.mask_src;
-    T* out = (T*)args.out;
     float s_l1 = 0.f, s_l0 = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int col = cbase + j * 16;
-      bool cv = col < N;
-      float csum = 0.f;
-      float add = 0.f, tnc = 0.f;
+    for (int j = 0; j < WG::TN; ++j) {
+      const int col = cbase + j * 16;
+      const bool cv = col < N;
+      float add[4] = {0.f, 0.f, 0.f, 0.f}, tnc[4] = {0.f, 0.f, 0.f, 0.f}, csum[4] = {0.f, 0.f, 0.f, 0.f};
       if (cv) {
         if constexpr (EPI == EPI_ENC) {
-          add = bias ? E::to_f(bias[col]) : 0.f;
-          tnc = args.tn ? args.tn[col] : 0.f;
+          if (args.bias) ld4<DT>(args.bias, col, add);
+          if (args.tn) ld4<CC_F32>(args.tn, col, tnc);
         } else {
-          add = args.tn ? args.scale0 * args.tn[col] : 0.f;
+          if (args.tn) {
+            ld4<CC_F32>(args.tn, col, add);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) add[e] *= args.scale0;
+          }
         }
       }
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < WG::TM; ++i) {
+        const int row = rbase + i * 16;
+        if (!cv || row >= M) continue;
+        const int64_t o = (int64_t)row * args.ldo + col;
+        float v[4], mk[4];
+        if constexpr (EPI == EPI_DACTS) ld4<DT>(args.mask_src, o, mk);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          int row = rbase + i * 16 + e;
-          if (!cv || row >= M) continue;
-          int64_t o = (int64_t)row * args.ldo + col;
-          float v = acc[i][j][e] + add;
+          float t = acc[i][j][e] + add[e];
           if constexpr (EPI == EPI_ENC) {
-            if (args.flag) v = fmaxf(v, 0.f);
+            if (args.flag) t = fmaxf(t, 0.f);
           } else {
-            v = E::to_f(mask[o]) > 0.f ? v : 0.f;
+            t = mk[e] > 0.f ? t : 0.f;
           }
-          T q = E::from_f(v);
-          out[o] = q;
-          float vq = E::to_f(q);
-          csum += vq;
+          v[e] = E::round(t);
+          csum[e] += v[e];
           if constexpr (EPI == EPI_ENC) {
-            s_l1 += vq * tnc;
-            s_l0 += vq > 0.f ? 1.f : 0.f;
+            s_l1 += v[e] * tnc[e];
+            s_l0 += v[e] > 0.f ? 1.f : 0.f;
           }
         }
-      if (args.col_part) {
-        csum += __shfl_xor(csum, 16, 64);
-        csum += __shfl_xor(csum, 32, 64);
-        if (lane < 16 && cv) args.col_part[(int64_t)(2 * tm + wr) * N + col] = csum;
+        st4<DT>(args.out, o, v);
+      }
+      if (args.col_part) {  // reduce over the 16 lanes (rows) that share these 4 columns
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float s = csum[e];
+          s += __shfl_xor(s, 1, 64);
+          s += __shfl_xor(s, 2, 64);
+          s += __shfl_xor(s, 4, 64);
+          s += __shfl_xor(s, 8, 64);
+          csum[e] = s;
+        }
+        if ((lane & 15) == 0 && cv)
+          st4<CC_F32>(args.col_part, (int64_t)(tm * WG::WARPS_M + wr) * N + col, csum);
       }
     }
     if constexpr (EPI == EPI_ENC) {
@@ -371,33 +433,37 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
       }
     }
   } else if constexpr (EPI == EPI_WGDEC || EPI == EPI_WGENC) {
-    T* out = (T*)args.out;
-    const T* w = (const T*)args.w_src;
     float sq = 0.f;
     const bool l1term = EPI == EPI_WGDEC && args.scale0 != 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < WG::TM; ++i) {
+      const int row = rbase + i * 16;
+      if (row >= M) continue;
+      const float cs = l1term ? args.scale0 * args.colsum[row] : 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        int row = rbase + i * 16 + e;
-        if (row >= M) continue;
-        float cs = l1term ? args.scale0 * args.colsum[row] : 0.f;
+      for (int j = 0; j < WG::TN; ++j) {
+        const int col = cbase + j * 16;
+        if (col >= N) continue;
+        const int64_t o = (int64_t)row * args.ldo + col;
+        float v[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          int col = cbase + j * 16;
-          if (col >= N) continue;
-          int64_t o = (int64_t)row * args.ldo + col;
-          float v = acc[i][j][e];
-          if (l1term) {
-            float nrm = args.norms[(int64_t)row * args.n_models + col / args.d_model];
-            v += nrm > 0.f ? cs * E::to_f(w[o]) / nrm : 0.f;
-          }
-          T q = E::from_f(v);
-          out[o] = q;
-          float vq = E::to_f(q);
-          sq += vq * vq;
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e];
+        if (l1term) {
+          const float nrm = args.norms[(int64_t)row * args.n_models + col / args.d_model];
+          const float c = nrm > 0.f ? cs / nrm : 0.f;
+          float w[4];
+          ld4<DT>(args.w_src, o, w);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += c * w[e];
         }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = E::round(v[e]);
+          sq += v[e] * v[e];
+        }
+        st4<DT>(args.out, o, v);
       }
+    }
     if (args.wave_part0) {
       float t = wave_sum(sq);
       if (lane == 0) args.wave_part0[wave_slot] = t;
@@ -405,20 +471,30 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
   }
 }
 
-template <int DT, bool AKC, bool BKC, int EPI>
+// N = n*d multiple of 288 (and an MN-contiguous bf16 B operand): 256 x 288 tiles.  (The fp32
+// parity mode keeps 256 x 256: its 288-wide variant exceeds 256 VGPRs.)
+static int pick_bn(int64_t N, bool bkc, int dtype) {
+  return (!bkc && dtype == CC_BF16 && N % 288 == 0) ? 288 : 256;
+}
+static int64_t n_blocks(int64_t M, int64_t N, int bn) { return ((M + BM - 1) / BM) * ((N + bn - 1) / bn); }
+
+template <int DT, bool AKC, bool BKC, int EPI, int BNT>
 static int launch(GemmArgs a, hipStream_t st) {
   a.nbm = (a.M + BM - 1) / BM;
-  a.nbn = (a.N + BN - 1) / BN;
+  a.nbn = (a.N + BNT - 1) / BNT;
   dim3 grid(a.nbm * a.nbn), block(NTHR);
-  hipLaunchKernelGGL((gemm_kernel<DT, AKC, BKC, EPI>), grid, block, 0, st, a);
+  hipLaunchKernelGGL((gemm_kernel<DT, AKC, BKC, EPI, BNT>), grid, block, 0, st, a);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }
 
 template <int EPI, bool AKC, bool BKC>
 static int launch_dt(int dtype, GemmArgs a, hipStream_t st) {
-  if (dtype == CC_BF16) return launch<CC_BF16, AKC, BKC, EPI>(a, st);
-  if (dtype == CC_F32) return launch<CC_F32, AKC, BKC, EPI>(a, st);
+  if constexpr (!BKC) {
+    if (pick_bn(a.N, BKC, dtype) == 288) return launch<CC_BF16, AKC, BKC, EPI, 288>(a, st);
+  }
+  if (dtype == CC_BF16) return launch<CC_BF16, AKC, BKC, EPI, 256>(a, st);
+  if (dtype == CC_F32) return launch<CC_F32, AKC, BKC, EPI, 256>(a, st);
   return CC_ERR_DTYPE;
 }
 
@@ -430,17 +506,17 @@ static int check_gemm(const GemmArgs& a, int dtype, bool akc, bool bkc) {
   if (dtype != CC_BF16 && dtype != CC_F32) return CC_ERR_DTYPE;
   if (a.M <= 0 || a.N <= 0 || a.K <= 0) return CC_ERR_SHAPE;
   int epc = dtype == CC_BF16 ? 8 : 4;
-  // vector (16 B) granularity: contiguous dims and leading dims
+  // vector (16 B) granularity of contiguous dims / leading dims; epilogue vectors of 4 columns
   if (akc && (a.K % epc)) return CC_ERR_SHAPE;
   if (!akc && (a.M % epc)) return CC_ERR_SHAPE;
   if (bkc && (a.K % epc)) return CC_ERR_SHAPE;
   if (!bkc && (a.N % epc)) return CC_ERR_SHAPE;
+  if (a.N % 4 || a.ldo % 4) return CC_ERR_SHAPE;
   if ((a.lda % epc) || (a.ldb % epc)) return CC_ERR_ALIGN;
   if (!al16(a.A) || !al16(a.B)) return CC_ERR_ALIGN;
   int es = dtype == CC_BF16 ? 2 : 4;
-  // per-block descriptor ranges must fit the 31-bit offsets
   uint64_t ra = akc ? (uint64_t)BM * a.lda * es : (uint64_t)a.K * a.lda * es;
-  uint64_t rb = bkc ? (uint64_t)BN * a.ldb * es : (uint64_t)a.K * a.ldb * es;
+  uint64_t rb = bkc ? (uint64_t)288 * a.ldb * es : (uint64_t)a.K * a.ldb * es;
   if (ra >= MAX_RECORDS || rb >= MAX_RECORDS) return CC_ERR_TOO_LARGE;
   return CC_OK;
 }
@@ -452,7 +528,8 @@ using namespace cc;
 extern "C" {
 
 int64_t cc_col_part_rows(int64_t M) { return 2 * ((M + BM - 1) / BM); }
-int64_t cc_wave_parts(int64_t M, int64_t N) { return 8 * ((M + BM - 1) / BM) * ((N + BN - 1) / BN); }
+int64_t cc_wave_parts(int64_t M, int64_t N) { return 8 * n_blocks(M, N, 256); }
+int64_t cc_wgrad_parts(int64_t h, int64_t K, int dtype) { return 8 * n_blocks(h, K, pick_bn(K, false, dtype)); }
 
 int cc_gemm_f32out(const void* A, int a_layout, int64_t lda, const void* Bm, int b_layout, int64_t ldb, float* C,
                    int64_t ldc, int64_t M, int64_t N, int64_t K, int dtype, void* stream) {
@@ -460,6 +537,7 @@ int cc_gemm_f32out(const void* A, int a_layout, int64_t lda, const void* Bm, int
   a.A = A; a.B = Bm; a.lda = lda; a.ldb = ldb; a.M = (int)M; a.N = (int)N; a.K = (int)K;
   a.out = C; a.ldo = ldc;
   if (!C) return CC_ERR_NULL;
+  if (((uintptr_t)C & 15) != 0) return CC_ERR_ALIGN;
   bool akc = a_layout == CC_LAYOUT_KC, bkc = b_layout == CC_LAYOUT_KC;
   int rc = check_gemm(a, dtype, akc, bkc);
   if (rc) return rc;

@@ -490,8 +490,8 @@ int cc_clip_finalize(const float* sq, const int64_t* off, int nparams, float max
   return CC_OK;
 }
 
-int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, float lr, float beta1,
-                 float beta2, float eps, int64_t step, int dtype, void* stream) {
+int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, double lr, double beta1,
+                 double beta2, double eps, int64_t step, int dtype, void* stream) {
   if (!p || !g || !m || !v) return CC_ERR_NULL;
   if (numel <= 0 || step <= 0) return CC_ERR_SHAPE;
   if (!al16(p) || !al16(g) || !al16(m) || !al16(v)) return CC_ERR_ALIGN;

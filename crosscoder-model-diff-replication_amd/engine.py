@@ -104,7 +104,7 @@ class StepWorkspace:
         self.scalars = E(ops.loss_scalars_len(B))
         self.g_pre = E(B, h, dt=dtype)
         self.gpre_colpart = E(ops.col_part_rows(B), h)
-        nw_w = ops.wave_parts(h, K)
+        nw_w = ops.wgrad_parts(h, K, dtype)
         sizes = [nw_w, nw_w, (h + 255) // 256, (K + 255) // 256]
         self.sq_off = [0]
         for s in sizes:

@@ -57,6 +57,10 @@ def wave_parts(M, N):
     return int(lib().cc_wave_parts(M, N))
 
 
+def wgrad_parts(h, K, dtype):
+    return int(lib().cc_wgrad_parts(h, K, dtype_code(dtype)))
+
+
 def prep_part_rows(B):
     return int(lib().cc_prep_part_rows(B))
 

@@ -55,7 +55,8 @@ const char* cc_strerror(int code);
  * floats.  Row-block slabs of the elementwise kernels: cc_prep_part_rows(B) x K and
  * cc_loss_part_rows(B) x K; loss row stats: 2 * n * cc_loss_col_blocks(d) x B. */
 int64_t cc_col_part_rows(int64_t M);
-int64_t cc_wave_parts(int64_t M, int64_t N);
+int64_t cc_wave_parts(int64_t M, int64_t N);    /* encode (B, h) per-wave partial count       */
+int64_t cc_wgrad_parts(int64_t h, int64_t K, int dtype); /* wgrad_dec / wgrad_enc per-wave partials */
 int64_t cc_prep_part_rows(int64_t B);
 int64_t cc_loss_part_rows(int64_t B);
 int64_t cc_loss_col_blocks(int64_t d);
@@ -124,7 +125,7 @@ int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const
                  void* g_pre, float* colsum_part, int64_t B, int64_t K, int64_t h, int dtype, void* stream);
 
 /* W_dec.grad [h][K] = acts^T . g_recon + l1_scale * sum_b(acts[:,h]) * W_dec[h,m,:]/||W_dec[h,m,:]||
- * (norm backward is 0 where the norm is 0).  sq_part [cc_wave_parts(h,K)]: sum of grad^2. */
+ * (norm backward is 0 where the norm is 0).  sq_part [cc_wgrad_parts(h,K,dtype)]: sum of grad^2. */
 int cc_wgrad_dec(const void* acts, const void* g_recon, const void* W_dec, const float* norms,
                  const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_part, int64_t B,
                  int64_t h, int64_t n, int64_t d, int dtype, void* stream);
@@ -145,8 +146,8 @@ int cc_clip_finalize(const float* sq, const int64_t* off, int nparams, float max
  * decay / amsgrad) fused with the clip multiply: g' = dtype(g * coef[0]); m, v, p updated in place
  * over `numel` flat elements; step = the Adam step count AFTER increment; lr from LambdaLR.
  * dtype-rounding between torch's ops is reproduced (bf16 state like the reference). */
-int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, float lr,
-                 float beta1, float beta2, float eps, int64_t step, int dtype, void* stream);
+int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, double lr,
+                 double beta1, double beta2, double eps, int64_t step, int dtype, void* stream);
 
 #ifdef __cplusplus
 }
