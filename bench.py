@@ -76,7 +76,8 @@ def cpu_baseline(seconds_budget=20.0):
     """Oracle (reference PyTorch fp32 step restated, CPU) on a bounded sample of config 1."""
     from oracle import cpu_reference as O
 
-    cores = len(os.sched_getaffinity(0))
+    # this process's CPU share: OMP_NUM_THREADS (16 per GPU on the box), else the affinity mask
+    cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
     torch.set_num_threads(cores)
     cfg = {"seed": 49, "dict_size": H_LOCAL, "d_in": D_MODEL, "enc_dtype": "fp32", "dec_init_norm": 0.08,
            "batch_size": B, "num_tokens": 400_000_000, "lr": 5e-5, "beta1": 0.9, "beta2": 0.999, "l1_coeff": 2}

@@ -84,7 +84,11 @@ class Buffer(_BufferProtocol):
         out = self.buffer[self.buffer_pointer: self.buffer_pointer + B]
         self.buffer_pointer += B
         if self.buffer_pointer > self.buffer.shape[0] // 2 - B:
-            out = out.clone()  # refresh overwrites the first half of the buffer
+            # refresh overwrites the first half of the buffer in place.  The reference's
+            # `.float()` (buffer.py:117) copies only when enc_dtype is not fp32; for fp32 it
+            # aliases and the returned batch sees the overwrite -- kept for identical batches.
+            if out.dtype != torch.float32:
+                out = out.clone()
             self.refresh()
         return out, self.normalisation_factor
 

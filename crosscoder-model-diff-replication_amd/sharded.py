@@ -1,0 +1,169 @@
+"""Latent (dictionary) sharding of the training step across ranks — one process per GPU,
+RCCL (torch.distributed "nccl") over xGMI.
+
+Rank r owns latents [r*h/G, (r+1)*h/G): its slice of W_enc / W_dec / b_enc and their Adam
+moments; b_dec is replicated.  Per step (reference Trainer.step, trainer.py:41-63):
+  1. every rank reads the SAME batch (replicated x), encodes its latents and decodes them into
+     an fp32 partial reconstruction [B, n*d] (no bias)                     -> G1, G2 local
+  2. all_reduce(SUM) of the partial reconstructions (the only bulk exchange)   RCCL, 4*B*n*d bytes
+  3. b_dec + loss + g_recon on the full reconstruction: identical on all ranks
+  4. all_reduce of the two latent-local loss sums (l1, l0)                 8 bytes
+  5. backward is local (g_recon is replicated): G3, G4, G5, db_enc local; db_dec replicated
+  6. clip_grad_norm_: per-parameter squared sums all-reduced (b_dec counted once)   16 bytes
+  7. Adam on the local arena (b_dec updates are identical on every rank).
+
+`ShardedStep` holds the orchestration (the collectives and how partial results combine) and
+drives a backend that does the local compute: `HipShardBackend` (the product, engine.py
+kernels on one GPU).  The CPU tests drive the same `ShardedStep` with a torch-CPU backend over
+gloo to check the decomposition.
+"""
+import torch
+import torch.distributed as dist
+
+from . import engine, ops
+from .crosscoder import CrossCoder
+
+
+def shard_range(h_total, world, rank):
+    """Contiguous latent slice of `rank`; every shard keeps h % 8 == 0 (16-byte rows)."""
+    if h_total % world:
+        raise ValueError(f"dict_size {h_total} is not divisible by world size {world}")
+    h = h_total // world
+    if h % 8:
+        raise ValueError(f"per-rank dict slice {h} must be a multiple of 8")
+    return rank * h, (rank + 1) * h
+
+
+def clip_sums_for_allreduce(sums, rank):
+    """Per-parameter squared-gradient sums [W_enc, W_dec, b_enc, b_dec] of this rank, with the
+    replicated b_dec term kept on rank 0 only so the all-reduced vector counts it once."""
+    out = sums.clone()
+    if rank != 0:
+        out[3] = 0.0
+    return out
+
+
+class ShardedStep:
+    def __init__(self, backend, group=None):
+        self.b = backend
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    def step(self, raw, factor, l1c, lr, betas, eps, t, max_norm=1.0):
+        b = self.b
+        recon = b.forward_partial(raw, factor)
+        dist.all_reduce(recon, op=dist.ReduceOp.SUM, group=self.group)
+        scalars = b.loss_from_full_recon()           # [l2, l1_local, l0_local, ev, ev_a, ev_b, ...]
+        dist.all_reduce(scalars[1:3], op=dist.ReduceOp.SUM, group=self.group)
+        sums = b.backward(l1c)                       # [4] local squared sums
+        gs = clip_sums_for_allreduce(sums, self.rank)
+        dist.all_reduce(gs, op=dist.ReduceOp.SUM, group=self.group)
+        b.clip_and_adam_from_sums(gs, lr, betas, eps, t, max_norm)
+        return scalars
+
+
+class HipShardBackend:
+    """Local compute of one rank on its GPU (engine.py kernels)."""
+
+    def __init__(self, cc):
+        self.cc = cc
+        a = cc.arena()
+        self.G = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
+        self.M = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
+        self.V = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
+        self.sums = torch.zeros(4, dtype=torch.float32, device=a.data.device)
+        self.ws = None
+
+    def forward_partial(self, raw, factor):
+        cc = self.cc
+        ws = self.ws = cc._workspace(raw.shape[0])
+        P = cc.arena()
+        B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
+        ops.prep_input(raw, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart)
+        ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
+        ops.dec_norms(P.W_dec_hk, h, n, d, norms=ws.norms, total=ws.tn)
+        with engine._span("G1_encode"):
+            ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, tn=ws.tn, colsum_part=ws.acts_colpart,
+                           l1_part=ws.l1_part, l0_part=ws.l0_part)
+        with engine._span("G2_decode"):
+            ops.decode_fwd(ws.acts, P.W_dec_hk, None, recon_f32=ws.recon)
+        return ws.recon
+
+    def loss_from_full_recon(self):
+        engine.loss_from_recon(self.ws, self.cc.arena())
+        return self.ws.scalars
+
+    def backward(self, l1c):
+        ws = self.ws
+        engine.backward(ws, self.cc.arena(), self.G, l1c)
+        for i in range(4):
+            self.sums[i] = ws.sq_slice(i).sum()
+        return self.sums
+
+    def clip_and_adam_from_sums(self, sums, lr, betas, eps, t, max_norm):
+        ws = self.ws
+        ops.clip_finalize(sums, [0, 1, 2, 3, 4], max_norm, ws.dtype == torch.bfloat16, ws.clip_out)
+        with engine._span("adam"):
+            ops.adam_step(self.cc.arena().data, self.G.data, self.M.data, self.V.data, ws.clip_out[0:1], lr,
+                          betas[0], betas[1], eps, t)
+
+
+class ShardedTrainer:
+    """Trainer.step contract over latent shards (the whole job is one crosscoder with
+    cfg["dict_size"] latents; this rank trains its slice)."""
+
+    def __init__(self, cfg, buffer, group=None, crosscoder=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.cfg = cfg
+        lo, hi = shard_range(cfg["dict_size"], self.world, self.rank)
+        self.lo, self.hi = lo, hi
+        if crosscoder is None:
+            # per-shard seeded init (the reference's construction applied to the slice)
+            local = dict(cfg, dict_size=hi - lo, seed=cfg["seed"] + self.rank)
+            crosscoder = CrossCoder(local)
+        self.crosscoder = crosscoder
+        self.buffer = buffer
+        self.backend = HipShardBackend(crosscoder)
+        self.engine = ShardedStep(self.backend, group)
+        self.total_steps = cfg["num_tokens"] // cfg["batch_size"]
+        self.step_counter = 0
+        self.t = 0
+        self.lr = cfg["lr"] * self.lr_lambda(0)
+
+    def lr_lambda(self, step):
+        if step < 0.8 * self.total_steps:
+            return 1.0
+        return 1.0 - (step - 0.8 * self.total_steps) / (0.2 * self.total_steps)
+
+    def get_l1_coeff(self):
+        if self.step_counter < 0.05 * self.total_steps:
+            return self.cfg["l1_coeff"] * self.step_counter / (0.05 * self.total_steps)
+        return self.cfg["l1_coeff"]
+
+    def step(self):
+        raw, factor = self.buffer.next_raw()
+        l1c = self.get_l1_coeff()
+        self.t += 1
+        scalars = self.engine.step(raw, factor, l1c, self.lr, (self.cfg["beta1"], self.cfg["beta2"]), 1e-8, self.t)
+        self.lr = self.cfg["lr"] * self.lr_lambda(self.t)
+        s = scalars[:6].tolist()
+        d = {"loss": s[0] + l1c * s[1], "l2_loss": s[0], "l1_loss": s[1], "l0_loss": s[2], "l1_coeff": l1c,
+             "lr": self.lr, "explained_variance": s[3], "explained_variance_A": s[4], "explained_variance_B": s[5]}
+        self.step_counter += 1
+        return d
+
+    def gather_state_dict(self):
+        """Full reference-layout state_dict on every rank (all_gather of the latent slices)."""
+        a = self.crosscoder.arena()
+        out = {}
+        for name, t in (("W_dec", a.W_dec_hk), ("W_enc", a.W_enc_hk), ("b_enc", a.b_enc)):
+            parts = [torch.empty_like(t) for _ in range(self.world)]
+            dist.all_gather(parts, t.contiguous(), group=self.group)
+            out[name] = torch.cat(parts, 0)
+        h, n, d = self.cfg["dict_size"], a.n, a.d
+        W_enc = out["W_enc"].view(h, n, d).permute(1, 2, 0)
+        return {"W_enc": W_enc, "W_dec": out["W_dec"].view(h, n, d), "b_enc": out["b_enc"],
+                "b_dec": a.b_dec().clone()}

@@ -1,0 +1,160 @@
+"""CPU: the C-ABI library loads and exports every declared symbol, argument validation runs
+without a GPU, and the host-side logic (drop-in CrossCoder surface, checkpoints, schedules,
+Buffer protocol) matches the reference."""
+import ctypes
+import json
+import os
+import re
+import shutil
+
+import numpy as np
+import pytest
+import torch
+
+import crosscoder_amd as ca
+from crosscoder_amd import _lib, trainer as ca_trainer
+from oracle import cpu_reference as O
+from tests._golden import GOLDEN, load
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "crosscoder_hip.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(cc_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert s in _lib.SIGNATURES, f"{s} declared in the header but not typed in _lib.py"
+        getattr(lib, s)  # raises AttributeError if the .so does not export it
+    assert set(_lib.SIGNATURES) == set(syms)
+    assert lib.cc_version() >= 100
+
+
+def test_argument_validation_without_gpu():
+    lib = _lib.load()
+    null = ctypes.c_void_p(0)
+    assert lib.cc_prep_input(null, 1, null, 1, null, null, 4, 2, 8, 1, null) == 1          # NULL
+    assert lib.cc_gemm_f32out(null, 0, 8, null, 0, 8, null, 8, 8, 8, 8, 1, null) == 1        # NULL
+    fake = ctypes.c_void_p(1 << 20)
+    assert lib.cc_gemm_f32out(fake, 0, 8, fake, 0, 8, fake, 8, 8, 8, 8, 7, null) == 2        # dtype
+    assert lib.cc_gemm_f32out(fake, 0, 12, fake, 0, 12, fake, 12, 8, 8, 12, 1, null) == 3    # K % 8
+    assert lib.cc_dec_norms(fake, fake, fake, 8, 2, 12, 1, null) == 3                          # d % 8
+    assert lib.cc_clip_finalize(fake, (ctypes.c_int64 * 2)(0, 1), 9, 1.0, 0, fake, null) == 3
+    assert b"NULL" in lib.cc_strerror(1)
+    assert lib.cc_col_part_rows(4096) == 32 and lib.cc_wave_parts(4096, 16384) == 8 * 16 * 64
+    assert lib.cc_wgrad_parts(16384, 4608, 1) == 8 * 64 * 16  # 256 x 288 tiles
+    assert lib.cc_wgrad_parts(16384, 4608, 2) == 8 * 64 * 18  # fp32: 256 x 256
+    assert lib.cc_loss_col_blocks(2304) == 5
+
+
+def _cfg(dtype="bf16", h=256, d=32, device="cpu"):
+    return {"seed": 49, "batch_size": 64, "buffer_mult": 128, "lr": 5e-5, "num_tokens": 640, "l1_coeff": 2,
+            "beta1": 0.9, "beta2": 0.999, "dict_size": h, "seq_len": 1024, "enc_dtype": dtype, "device": device,
+            "dec_init_norm": 0.08, "d_in": d, "log_every": 100, "save_every": 30000}
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_crosscoder_params_match_reference_layout(dtype):
+    cc = ca.CrossCoder(_cfg(dtype))
+    r = load(f"step_b64_n2_d32_h256_{dtype}")
+    sd = cc.state_dict()
+    assert list(sd.keys()) == ["W_enc", "W_dec", "b_enc", "b_dec"]
+    for k, v in r["init"].items():
+        assert sd[k].shape == v.shape and sd[k].dtype == v.dtype and sd[k].stride() == v.stride(), k
+        assert torch.equal(sd[k], v), k
+    # parameters() order = the reference's (clip / Adam iterate in this order)
+    assert [p.shape for p in cc.parameters()] == [v.shape for v in r["init"].values()]
+
+
+def test_loads_reference_checkpoint(tmp_path):
+    src = os.path.join(GOLDEN, "ckpt", "version_0")
+    cfg = json.load(open(os.path.join(src, "0_cfg.json")))
+    cwd = os.getcwd()
+    try:
+        os.chdir(tmp_path)
+        shutil.copytree(src, tmp_path / "checkpoints" / "version_0")
+        cc = ca.CrossCoder.load("version_0", 0)
+        ref = torch.load(os.path.join(src, "0.pt"), weights_only=True)
+        for k, v in ref.items():
+            assert torch.equal(cc.state_dict()[k], v), k
+            assert cc.state_dict()[k].stride() == v.stride(), k
+        # our save() writes the same two-file layout, reloadable by torch alone
+        cc.save()
+        out = tmp_path / "checkpoints" / "version_1"
+        assert sorted(os.listdir(out)) == ["0.pt", "0_cfg.json"]
+        sd = torch.load(out / "0.pt", weights_only=True)
+        for k, v in ref.items():
+            assert torch.equal(sd[k], v) and sd[k].stride() == v.stride(), k
+        assert json.load(open(out / "0_cfg.json")) == cfg
+    finally:
+        os.chdir(cwd)
+
+
+def test_arena_repacks_after_param_replacement():
+    cc = ca.CrossCoder(_cfg())
+    before = cc.W_dec.detach().clone()
+    cc.W_dec.data = cc.W_dec.data.clone()  # breaks the arena aliasing
+    a = cc.arena()
+    assert a.W_dec().data_ptr() == cc.W_dec.data_ptr()
+    assert torch.equal(cc.W_dec.detach(), before)
+    assert cc.W_enc.stride() == (32, 1, 64)
+
+
+def test_compute_refuses_cpu_tensors():
+    cc = ca.CrossCoder(_cfg())
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        cc.encode(torch.zeros(4, 2, 32, dtype=torch.bfloat16))
+
+
+def test_schedules_match_reference():
+    r = load("step_b32_n2_d32_h128_fp32")
+    cfg = r["cfg"]
+
+    class _NoBuf:
+        normalize = True
+
+    tr = ca_trainer.Trainer.__new__(ca_trainer.Trainer)
+    tr.cfg = cfg
+    tr.total_steps = cfg["num_tokens"] // cfg["batch_size"]
+    tr.step_counter = 0
+
+    class _Opt:
+        param_groups = [{"lr": cfg["lr"], "initial_lr": cfg["lr"]}]
+
+    sched = ca_trainer.LambdaLRHost(_Opt(), tr.lr_lambda)
+    for s, d in enumerate(r["steps"]["loss_dicts"]):
+        tr.step_counter = s
+        assert tr.get_l1_coeff() == d["l1_coeff"] == O.l1_coeff(s, tr.total_steps, cfg["l1_coeff"])
+        sched.step()
+        assert sched.get_last_lr()[0] == d["lr"]
+
+
+def test_buffer_matches_reference_with_fake_lms():
+    r = torch.load(os.path.join(GOLDEN, "buffer_fake_lm.pt"), weights_only=True)
+    cfg = json.loads(r["cfg"])
+
+    class FakeLM:
+        class _C:
+            pass
+
+        def __init__(self, table, pos):
+            self.table, self.pos = table, pos
+            self.cfg = FakeLM._C()
+            self.cfg.d_model = table.shape[1]
+
+        def run_with_cache(self, tokens, names_filter=None, return_type=None):
+            return None, {names_filter: self.table[tokens] + self.pos[None, : tokens.shape[1]]}
+
+    torch.manual_seed(49)
+    buf = ca.Buffer(cfg, FakeLM(r["A_table"], r["A_pos"]), FakeLM(r["B_table"], r["B_pos"]), r["tokens"])
+    assert torch.equal(buf.normalisation_factor, r["normalisation_factor"])
+    assert buf.buffer.shape[0] == r["buffer_size"]
+    for want in r["next"]:
+        assert torch.equal(buf.next(), want)

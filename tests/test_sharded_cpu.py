@@ -1,0 +1,146 @@
+"""CPU, world_size 2 over gloo: the latent-sharded step orchestration (sharded.ShardedStep —
+the same collectives and combine rules the GPU path uses) driven by a torch-CPU backend must
+reproduce the unsharded oracle step."""
+import os
+import random
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from crosscoder_amd import sharded
+from oracle import cpu_reference as O
+
+B, N_MODELS, D, H, STEPS = 32, 2, 16, 64, 3
+
+
+class CpuShardBackend:
+    """Local compute of one latent shard with torch autograd (test-side stand-in for the GPU)."""
+
+    def __init__(self, P):
+        self.P = {k: torch.nn.Parameter(v.detach().clone()) for k, v in P.items()}
+        self.m = {k: torch.zeros_like(v) for k, v in self.P.items()}
+        self.v = {k: torch.zeros_like(v) for k, v in self.P.items()}
+
+    def forward_partial(self, raw, factor):
+        self.x = O.buffer_next(raw, factor)
+        self.acts = torch.relu(torch.einsum("bnd,ndh->bh", self.x, self.P["W_enc"]) + self.P["b_enc"])
+        self.partial = torch.einsum("bh,hnd->bnd", self.acts, self.P["W_dec"])
+        self.recon = self.partial.detach().clone().contiguous()
+        return self.recon
+
+    def loss_from_full_recon(self):
+        self.R = self.recon.clone().requires_grad_(True)
+        full = self.R + self.P["b_dec"]
+        x = self.x
+        l2_row = (full - x).pow(2).sum(dim=(1, 2))
+        self.l2 = l2_row.mean()
+        tv = (x - x.mean(0)).pow(2).sum(dim=(1, 2))
+        ev = 1 - l2_row / (tv + 1e-8)
+        tn = self.P["W_dec"].norm(dim=-1).sum(1)
+        self.l1 = (self.acts * tn[None]).sum(-1).mean(0)
+        l0 = (self.acts > 0).float().sum(-1).mean()
+        return torch.stack([self.l2.detach(), self.l1.detach(), l0, ev.mean().detach(), ev.mean().detach(),
+                            ev.mean().detach()])
+
+    def backward(self, l1c):
+        for p in self.P.values():
+            p.grad = None
+        gl2 = torch.autograd.grad(self.l2, [self.R, self.P["b_dec"]], retain_graph=True)
+        (self.partial * gl2[0]).sum().add(l1c * self.l1).backward()
+        self.P["b_dec"].grad = gl2[1]
+        return torch.stack([self.P[k].grad.pow(2).sum() for k in O.PARAM_ORDER])
+
+    def clip_and_adam_from_sums(self, sums, lr, betas, eps, t, max_norm):
+        total = sums.sqrt().norm()
+        coef = min(1.0, max_norm / (total.item() + 1e-6))
+        with torch.no_grad():
+            for k in O.PARAM_ORDER:
+                g = self.P[k].grad * coef
+                O.adam_update(self.P[k].data, g, self.m[k], self.v[k], float(t), lr, betas[0], betas[1], eps)
+
+
+def _setup():
+    cfg = {"seed": 49, "dict_size": H, "d_in": D, "enc_dtype": "fp32", "dec_init_norm": 0.08, "batch_size": B,
+           "num_tokens": B * 10, "lr": 1e-3, "beta1": 0.9, "beta2": 0.999, "l1_coeff": 2}
+    P = O.init_params(cfg)
+    g = torch.Generator().manual_seed(0)
+    raws = [torch.randn(B, N_MODELS, D, generator=g) * 3 for _ in range(STEPS)]
+    factor = torch.tensor([0.5, 0.25])
+    return cfg, P, raws, factor
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg, P, raws, factor = _setup()
+        lo, hi = sharded.shard_range(H, world, rank)
+        Ps = {"W_enc": P["W_enc"][:, :, lo:hi], "W_dec": P["W_dec"][lo:hi], "b_enc": P["b_enc"][lo:hi],
+              "b_dec": P["b_dec"]}
+        backend = CpuShardBackend(Ps)
+        step = sharded.ShardedStep(backend)
+        outs = []
+        for t in range(STEPS):
+            l1c = 2.0 if t else 0.0
+            s = step.step(raws[t], factor, l1c, cfg["lr"], (0.9, 0.999), 1e-8, t + 1)
+            outs.append(s[:3].clone())
+        q.put((rank, [o.tolist() for o in outs], {k: v.detach().clone() for k, v in backend.P.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_step_matches_unsharded(world):
+    port = 29500 + random.randint(0, 2000)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, outs, Pl = q.get(timeout=300)
+        res[r] = (outs, Pl)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+    cfg, P, raws, factor = _setup()
+    ref = {k: torch.nn.Parameter(v.detach().clone()) for k, v in P.items()}
+    m = {k: torch.zeros_like(v) for k, v in ref.items()}
+    v = {k: torch.zeros_like(v) for k, v in ref.items()}
+    for t in range(STEPS):
+        l1c = 2.0 if t else 0.0
+        x = O.buffer_next(raws[t], factor)
+        lo = O.get_losses(x, ref, torch.float32)
+        for p in ref.values():
+            p.grad = None
+        (lo["l2_loss"] + l1c * lo["l1_loss"]).backward()
+        with torch.no_grad():
+            O.clip_grad_norm([ref[k].grad for k in O.PARAM_ORDER])
+            for k in O.PARAM_ORDER:
+                O.adam_update(ref[k].data, ref[k].grad, m[k], v[k], float(t + 1), cfg["lr"], 0.9, 0.999, 1e-8)
+        for r in range(world):
+            l2, l1, l0 = res[r][0][t]
+            assert abs(l2 - lo["l2_loss"].item()) <= 1e-5 * abs(lo["l2_loss"].item())
+            assert abs(l1 - lo["l1_loss"].item()) <= 1e-5 * abs(lo["l1_loss"].item()) + 1e-7
+            assert abs(l0 - lo["l0_loss"].item()) <= 1e-6
+    for r in range(world):
+        lo_, hi_ = sharded.shard_range(H, world, r)
+        Pl = res[r][1]
+        torch.testing.assert_close(Pl["W_dec"], ref["W_dec"].detach()[lo_:hi_], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(Pl["W_enc"], ref["W_enc"].detach()[:, :, lo_:hi_], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(Pl["b_enc"], ref["b_enc"].detach()[lo_:hi_], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(Pl["b_dec"], ref["b_dec"].detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_shard_range_and_clip_combine():
+    assert sharded.shard_range(131072, 8, 3) == (49152, 65536)
+    with pytest.raises(ValueError):
+        sharded.shard_range(100, 8, 0)
+    s = torch.tensor([1.0, 2.0, 3.0, 4.0])
+    assert sharded.clip_sums_for_allreduce(s, 0).tolist() == [1, 2, 3, 4]
+    assert sharded.clip_sums_for_allreduce(s, 1).tolist() == [1, 2, 3, 0]
