@@ -35,7 +35,8 @@ SIGNATURES = {
     "cc_gemm_f32out": (_i, [_p, _i, _i64, _p, _i, _i64, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_prep_input": (_i, [_p, _i, _p, _i, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_reduce_rows": (_i, [_p, _i64, _i64, _i64, _f, _p, _p, _i, _p, _p]),
-    "cc_dec_norms": (_i, [_p, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_reduce_parts": (_i64, [_i64]),
+    "cc_dec_norms": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_encode_fwd": (_i, [_p, _p, _p, _p, _p, _i, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_decode_fwd": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_loss_fwd_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i, _p]),

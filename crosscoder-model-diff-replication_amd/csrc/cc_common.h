@@ -65,6 +65,31 @@ template <int DT> CC_DEV void store8(void* base, int64_t idx, const float v[8]) 
     p[1] = f32x4{v[4], v[5], v[6], v[7]};
   }
 }
+// Non-temporal (streamed-once) variants for the HBM-bound optimizer pass.
+template <int DT> CC_DEV void load8_nt(const void* base, int64_t idx, float v[8]) {
+  if constexpr (DT == CC_BF16) {
+    bf16x8 r = __builtin_nontemporal_load((const bf16x8*)((const bf16_t*)base + idx));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bf2f((bf16_t)r[j]);
+  } else {
+    const f32x4* p = (const f32x4*)((const float*)base + idx);
+    f32x4 a = __builtin_nontemporal_load(p), b = __builtin_nontemporal_load(p + 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+  }
+}
+template <int DT> CC_DEV void store8_nt(void* base, int64_t idx, const float v[8]) {
+  if constexpr (DT == CC_BF16) {
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(v[j]);
+    __builtin_nontemporal_store(r, (bf16x8*)((bf16_t*)base + idx));
+  } else {
+    f32x4* p = (f32x4*)((float*)base + idx);
+    __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, p);
+    __builtin_nontemporal_store(f32x4{v[4], v[5], v[6], v[7]}, p + 1);
+  }
+}
 CC_DEV void load8f(const float* base, int64_t idx, float v[8]) {
   const f32x4* p = (const f32x4*)(base + idx);
   f32x4 a = p[0], b = p[1];

@@ -47,7 +47,7 @@ struct GemmArgs {
   const float* tn;      // per-column total decoder norm
   const void* mask_src; // acts (EPI_DACTS), indexed like out
   const void* w_src;    // W_dec (EPI_WGDEC), indexed like out
-  const float* norms;   // [h][n]
+  const float* norms;   // [h][n] inverse decoder norms (0 where the norm is 0)
   const float* colsum;  // [h] sum_b acts
   float* col_part;      // [nbm * WARPS_M][N]
   float* wave_part0;    // [nbm*nbn*8]
@@ -66,15 +66,20 @@ CC_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint64_t bytes) {
 }
 
 CC_DEV void dma16(__amdgpu_buffer_rsrc_t r, char* lds_base, uint32_t voff) {
+#ifdef CC_EXP_NOLOAD  // timing-only experiment build (never shipped): every lane out of range
+  voff = OOB;
+#endif
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_base, 16, (int)voff, 0, 0, 0);
 }
 
-// ---- MN-tile geometry: [BK k rows][COLS columns], row bytes RB, CH 16-B chunks per row ----
-template <int DT, int COLS>
+// ---- Pipeline geometry.  KROW = bytes of contraction per KC row per K-step (64 or 128);
+// BK = KROW / element size; NST = LDS stages (prefetch distance NST-1 K-steps).
+// MN tile: [BK k rows][COLS columns], row bytes RB, CH 16-B chunks per row.
+template <int DT, int COLS, int KROW>
 struct MnTile {
   static constexpr int ES = DT == CC_BF16 ? 2 : 4;
   static constexpr int EPC = 16 / ES;                 // elements per chunk
-  static constexpr int BK = DT == CC_BF16 ? 64 : 32;
+  static constexpr int BK = KROW / ES;
   static constexpr int RB = COLS * ES;
   static constexpr int CH = RB / 16;
   static constexpr int BYTES = BK * RB;
@@ -90,59 +95,64 @@ struct MnTile {
     }
   }
 };
+// KC tile: [ROWS][KROW bytes]; phys chunk = chunk ^ swz(row), conflict-free for ds_read_b128
+template <int KROW>
+struct KcTile {
+  static constexpr int CPR = KROW / 16;     // chunks per row
+  static constexpr int RPD = 1024 / KROW;   // rows per 1 KB DMA
+  static CC_DEV int swz(int row) { return KROW == 128 ? (row & 7) : ((row >> 1) & 3); }
+};
 
-// ---- global -> LDS staging ----
-// KC: tile rows [row0, row0+ROWS), 128 B of contraction each; 1 KB DMA = 8 rows.
-template <int DT, int ROWS>
-CC_DEV void stage_kc(__amdgpu_buffer_rsrc_t r, char* lds, int rows_left, int k0, int K, int64_t ld, int wave,
-                     int lane) {
+// ---- global -> LDS staging: the q-th 1 KB DMA of this wave for one operand tile ----
+// KC: tile rows [row0, row0+ROWS), KROW bytes of contraction each.
+template <int DT, int ROWS, int KROW>
+CC_DEV void dma_kc(__amdgpu_buffer_rsrc_t r, char* lds, char* junk, int q, bool live, int rows_left, int k0, int K,
+                   int64_t ld, int wave, int lane) {
+  using T = KcTile<KROW>;
   constexpr int EPC = DT == CC_BF16 ? 8 : 4;
   constexpr int ES = DT == CC_BF16 ? 2 : 4;
-  constexpr int NDMA = ROWS / 8;
-#pragma unroll
-  for (int i = 0; i < (NDMA + 7) / 8; ++i) {
-    int ci = i * 8 + wave;
-    if (ci < NDMA) {
-      int row = ci * 8 + (lane >> 3);
-      int c = (lane & 7) ^ (row & 7);
-      int k = k0 + c * EPC;
-      bool ok = row < rows_left && k < K;
-      uint32_t voff = ok ? (uint32_t)(((int64_t)row * ld + k) * ES) : OOB;
-      dma16(r, lds + ci * 1024, voff);
-    }
-  }
+  constexpr int NDMA = ROWS * KROW / 1024;
+  const int ci = q * 8 + wave;
+  // branch-free: a DMA beyond the tile (or of a step past the end) lands in the junk slot,
+  // so every wave issues the same count every step (uniform counted vmcnt)
+  const bool use = live && (NDMA % 8 == 0 || ci < NDMA);
+  const int row = ci * T::RPD + lane / T::CPR;
+  const int c = (lane % T::CPR) ^ T::swz(row);
+  const int k = k0 + c * EPC;
+  const bool ok = use && row < rows_left && k < K;
+  const uint32_t voff = ok ? (uint32_t)(((int64_t)row * ld + k) * ES) : OOB;
+  dma16(r, use ? lds + ci * 1024 : junk, voff);
 }
 // MN: contraction rows [k0, k0+BK) x COLS contiguous columns, lane-linear image.
-template <int DT, int COLS>
-CC_DEV void stage_mn(__amdgpu_buffer_rsrc_t r, char* lds, int cols_left, int k0, int K, int64_t ld, int wave,
-                     int lane) {
-  using G = MnTile<DT, COLS>;
-#pragma unroll
-  for (int i = 0; i < (G::NDMA + 7) / 8; ++i) {
-    int ci = i * 8 + wave;
-    if (ci < G::NDMA) {
-      int b = ci * 1024 + lane * 16;
-      int k = b / G::RB;
-      int cph = (b - k * G::RB) >> 4;
-      int clog = cph - G::rot(k);
-      clog += clog < 0 ? G::CH : 0;
-      int col = clog * G::EPC;
-      bool ok = (k0 + k) < K && col < cols_left;
-      uint32_t voff = ok ? (uint32_t)(((int64_t)(k0 + k) * ld + col) * G::ES) : OOB;
-      dma16(r, lds + ci * 1024, voff);
-    }
-  }
+template <int DT, int COLS, int KROW>
+CC_DEV void dma_mn(__amdgpu_buffer_rsrc_t r, char* lds, char* junk, int q, bool live, int cols_left, int k0, int K,
+                   int64_t ld, int wave, int lane) {
+  using G = MnTile<DT, COLS, KROW>;
+  const int ci = q * 8 + wave;
+  const bool use = live && (G::NDMA % 8 == 0 || ci < G::NDMA);
+  const int b = ci * 1024 + lane * 16;
+  const int k = b / G::RB;
+  const int cph = (b - k * G::RB) >> 4;
+  int clog = cph - G::rot(k);
+  clog += clog < 0 ? G::CH : 0;
+  const int col = clog * G::EPC;
+  const bool ok = use && (k0 + k) < K && col < cols_left;
+  const uint32_t voff = ok ? (uint32_t)(((int64_t)(k0 + k) * ld + col) * G::ES) : OOB;
+  dma16(r, use ? lds + ci * 1024 : junk, voff);
 }
 
-// ---- fragment reads, bf16 (16x16x32 operand map: lane l holds X[r = l&15][k = 8*(l>>4) + j]) ----
+// ---- fragment reads, bf16 (16x16x32 operand map: lane l holds X[r = l&15][k = 8*(l>>4) + j]);
+// kk selects the 32-k slice of the K-step.
+template <int KROW>
 CC_DEV bf16x8 frag_kc_bf16(const char* tile, int row0, int kk, int lane) {
+  using T = KcTile<KROW>;
   int row = row0 + (lane & 15);
   int c = (lane >> 4) + 4 * kk;
-  return *(const bf16x8*)(tile + row * 128 + ((c ^ (row & 7)) << 4));
+  return *(const bf16x8*)(tile + row * KROW + ((c ^ T::swz(row)) << 4));
 }
-template <int COLS>
+template <int COLS, int KROW>
 CC_DEV bf16x8 frag_mn_bf16(const char* tile, int col0, int kk, int lane) {
-  using G = MnTile<CC_BF16, COLS>;
+  using G = MnTile<CC_BF16, COLS, KROW>;
   int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
   int clog = (col0 + 4 * pp) >> 3;
   bf16x8 out;
@@ -157,16 +167,18 @@ CC_DEV bf16x8 frag_mn_bf16(const char* tile, int col0, int kk, int lane) {
   }
   return out;
 }
-// ---- fragment reads, fp32 (16x16x4: lane holds X[l&15][k = l>>4]); a 32-k step is 8 MFMAs
-// (kk = 0..1, e = 0..3), lane group g = l>>4 supplies k = 4*(g + 4*kk) + e on both operands.
+// ---- fragment reads, fp32 (16x16x4: lane holds X[l&15][k = l>>4]); a 16-k slice kk is 4 MFMAs
+// (e = 0..3), lane group g = l>>4 supplies k = 4*(g + 4*kk) + e on both operands.
+template <int KROW>
 CC_DEV f32x4 frag_kc_f32(const char* tile, int row0, int kk, int lane) {
+  using T = KcTile<KROW>;
   int row = row0 + (lane & 15);
   int c = (lane >> 4) + 4 * kk;
-  return *(const f32x4*)(tile + row * 128 + ((c ^ (row & 7)) << 4));
+  return *(const f32x4*)(tile + row * KROW + ((c ^ T::swz(row)) << 4));
 }
-template <int COLS>
+template <int COLS, int KROW>
 CC_DEV f32x4 frag_mn_f32(const char* tile, int col0, int kk, int lane) {
-  using G = MnTile<CC_F32, COLS>;
+  using G = MnTile<CC_F32, COLS, KROW>;
   int g = lane >> 4;
   int col = col0 + (lane & 15);
   f32x4 out;
@@ -228,17 +240,38 @@ template <int DT> CC_DEV void st4(void* p, int64_t idx, const float v[4]) {
   }
 }
 
-template <int DT, bool AKC, bool BKC, int EPI, int BNT>
+// PIPE selects the K pipeline: KROW bytes per KC row per K-step and NST LDS stages.
+//   PIPE 0: KROW 128, NST 2 (prefetch 1 step)   PIPE 1: KROW 64, NST 4 (prefetch 3 steps)
+template <int PIPE> struct Pipe;
+template <> struct Pipe<0> { static constexpr int KROW = 128, NST = 2; };
+template <> struct Pipe<1> { static constexpr int KROW = 64, NST = 4; };
+#ifndef CC_GEMM_PIPE
+#define CC_GEMM_PIPE 0
+#endif
+
+template <int N> CC_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  // gfx9 s_waitcnt encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+template <int DT, bool AKC, bool BKC, int EPI, int BNT, int PIPE = CC_GEMM_PIPE>
 __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
   using E = Elem<DT>;
   using WG = WaveGeom<BNT>;
-  constexpr int BK = DT == CC_BF16 ? 64 : 32;
+  constexpr int KROW = Pipe<PIPE>::KROW, NST = Pipe<PIPE>::NST;
   constexpr int ES = DT == CC_BF16 ? 2 : 4;
-  constexpr int A_BYTES = AKC ? BM * 128 : MnTile<DT, BM>::BYTES;
-  constexpr int B_BYTES = BKC ? BNT * 128 : MnTile<DT, BNT>::BYTES;
+  constexpr int BK = KROW / ES;
+  constexpr int KK = KROW / 64;  // 32-element (bf16) / 16-element (fp32) slices per K-step
+  constexpr int A_BYTES = AKC ? BM * KROW : MnTile<DT, BM, KROW>::BYTES;
+  constexpr int B_BYTES = BKC ? BNT * KROW : MnTile<DT, BNT, KROW>::BYTES;
   constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int DA = (A_BYTES / 1024 + 7) / 8, DB = (B_BYTES / 1024 + 7) / 8;  // DMAs per wave per step
+  constexpr int D = DA + DB;
+  constexpr bool SPREAD = AKC;
   static_assert(!BKC || BNT == 256, "BN=288 tiles are built for MN-contiguous B only");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE + 1024];  // + junk DMA target
+  char* const junk = smem + NST * STAGE;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -268,14 +301,19 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
     }
   }
 
-  auto stage = [&](int kt, int s) {
+  // q-th DMA (0..D-1) of this wave for K-step kt into stage s
+  // q-th DMA (0..D-1) of this wave for K-step kt into stage s; steps >= nk go to the junk slot
+  auto dma = [&](int q, int kt, int s, bool live) {
     char* la = smem + s * STAGE;
     char* lb = la + A_BYTES;
-    int k0 = kt * BK;
-    if constexpr (AKC) stage_kc<DT, BM>(ra, la, M - m0, k0, K, args.lda, wave, lane);
-    else stage_mn<DT, BM>(ra, la, M - m0, k0, K, args.lda, wave, lane);
-    if constexpr (BKC) stage_kc<DT, BNT>(rb, lb, N - n0, k0, K, args.ldb, wave, lane);
-    else stage_mn<DT, BNT>(rb, lb, N - n0, k0, K, args.ldb, wave, lane);
+    const int k0 = kt * BK;
+    if (q < DA) {
+      if constexpr (AKC) dma_kc<DT, BM, KROW>(ra, la, junk, q, live, M - m0, k0, K, args.lda, wave, lane);
+      else dma_mn<DT, BM, KROW>(ra, la, junk, q, live, M - m0, k0, K, args.lda, wave, lane);
+    } else {
+      if constexpr (BKC) dma_kc<DT, BNT, KROW>(rb, lb, junk, q - DA, live, N - n0, k0, K, args.ldb, wave, lane);
+      else dma_mn<DT, BNT, KROW>(rb, lb, junk, q - DA, live, N - n0, k0, K, args.ldb, wave, lane);
+    }
   };
 
   // acc[i][j][e] = C[row = m0 + wr*WTM + 16i + (lane&15)][col = n0 + wc*WTN + 16j + 4*(lane>>4) + e]
@@ -286,54 +324,78 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
     for (int j = 0; j < WG::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (K + BK - 1) / BK;
-  stage(0, 0);
+  // prologue: steps 0 .. NST-2 in flight
+#pragma unroll
+  for (int p = 0; p < NST - 1; ++p)
+#pragma unroll
+    for (int q = 0; q < D; ++q) dma(q, p, p, p < nk);
+
   for (int kt = 0; kt < nk; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (kt + 1 < nk) stage(kt + 1, (kt + 1) & 1);
-    const char* la = smem + (kt & 1) * STAGE;
+    // step kt landed (this wave's DMAs): every step issues exactly D DMAs per wave, so the
+    // NST-2 younger steps may stay in flight
+#ifndef CC_EXP_NOWAIT  // timing-only experiment builds (never shipped): skip the DMA wait
+    wait_vmcnt<(NST - 2) * D>();
+#endif
+    __builtin_amdgcn_s_barrier();  // ... for every wave; stage (kt-1)%NST is free again
+    const int nxt = kt + NST - 1;
+    const bool pf = nxt < nk;
+    const int snx = nxt % NST;
+    const char* la = smem + (kt % NST) * STAGE;
     const char* lb = la + A_BYTES;
+    // KC-A kernels spread the next step's D DMAs over the TM A-fragment groups of the first
+    // slice; MN-A kernels (transposed reads) issue them all here (measured faster for each).
+    if constexpr (!SPREAD) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+      for (int q = 0; q < D; ++q) dma(q, nxt, snx, pf);
+    }
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
       if constexpr (DT == CC_BF16) {
-        bf16x8 a[WG::TM], b[WG::TN];
-#pragma unroll
-        for (int i = 0; i < WG::TM; ++i) {
-          const int r0 = wr * WG::WTM + i * 16;
-          a[i] = AKC ? frag_kc_bf16(la, r0, kk, lane) : frag_mn_bf16<BM>(la, r0, kk, lane);
-        }
+        bf16x8 b[WG::TN];
 #pragma unroll
         for (int j = 0; j < WG::TN; ++j) {
           const int c0 = wc * WG::WTN + j * 16;
-          b[j] = BKC ? frag_kc_bf16(lb, c0, kk, lane) : frag_mn_bf16<BNT>(lb, c0, kk, lane);
+          b[j] = BKC ? frag_kc_bf16<KROW>(lb, c0, kk, lane) : frag_mn_bf16<BNT, KROW>(lb, c0, kk, lane);
         }
 #pragma unroll
-        for (int i = 0; i < WG::TM; ++i)
+        for (int i = 0; i < WG::TM; ++i) {
+          if (SPREAD && kk == 0) {
+#pragma unroll
+            for (int q = 0; q < D; ++q)
+              if (q * WG::TM / D == i) dma(q, nxt, snx, pf);
+          }
+          const int r0 = wr * WG::WTM + i * 16;
+          bf16x8 a = AKC ? frag_kc_bf16<KROW>(la, r0, kk, lane) : frag_mn_bf16<BM, KROW>(la, r0, kk, lane);
 #pragma unroll
           for (int j = 0; j < WG::TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
-      } else {
-        f32x4 a[WG::TM], b[WG::TN];
-#pragma unroll
-        for (int i = 0; i < WG::TM; ++i) {
-          const int r0 = wr * WG::WTM + i * 16;
-          a[i] = AKC ? frag_kc_f32(la, r0, kk, lane) : frag_mn_f32<BM>(la, r0, kk, lane);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a, acc[i][j], 0, 0, 0);
         }
+      } else {
+        f32x4 b[WG::TN];
 #pragma unroll
         for (int j = 0; j < WG::TN; ++j) {
           const int c0 = wc * WG::WTN + j * 16;
-          b[j] = BKC ? frag_kc_f32(lb, c0, kk, lane) : frag_mn_f32<BNT>(lb, c0, kk, lane);
+          b[j] = BKC ? frag_kc_f32<KROW>(lb, c0, kk, lane) : frag_mn_f32<BNT, KROW>(lb, c0, kk, lane);
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int i = 0; i < WG::TM; ++i) {
+          if (SPREAD && kk == 0) {
 #pragma unroll
-          for (int i = 0; i < WG::TM; ++i)
+            for (int q = 0; q < D; ++q)
+              if (q * WG::TM / D == i) dma(q, nxt, snx, pf);
+          }
+          const int r0 = wr * WG::WTM + i * 16;
+          f32x4 a = AKC ? frag_kc_f32<KROW>(la, r0, kk, lane) : frag_mn_f32<BM, KROW>(la, r0, kk, lane);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
 #pragma unroll
             for (int j = 0; j < WG::TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[j][e], a[i][e], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[j][e], a[e], acc[i][j], 0, 0, 0);
+        }
       }
     }
   }
+  wait_vmcnt<0>();  // drain the junk-slot DMAs of the last NST-1 steps
 
   // ------------------------------- epilogue (transposed C fragments) -------------------------
   const int rbase = m0 + wr * WG::WTM + (lane & 15);
@@ -435,22 +497,28 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
   } else if constexpr (EPI == EPI_WGDEC || EPI == EPI_WGENC) {
     float sq = 0.f;
     const bool l1term = EPI == EPI_WGDEC && args.scale0 != 0.f;
+    // per-row factor scale * sum_b acts[b, row] and, per (row, model), 1/||W_dec[row, model]||
+    float cs[WG::TM];
 #pragma unroll
     for (int i = 0; i < WG::TM; ++i) {
       const int row = rbase + i * 16;
-      if (row >= M) continue;
-      const float cs = l1term ? args.scale0 * args.colsum[row] : 0.f;
+      cs[i] = (l1term && row < M) ? args.scale0 * args.colsum[row] : 0.f;
+    }
 #pragma unroll
-      for (int j = 0; j < WG::TN; ++j) {
-        const int col = cbase + j * 16;
-        if (col >= N) continue;
+    for (int j = 0; j < WG::TN; ++j) {
+      const int col = cbase + j * 16;
+      if (col >= N) continue;
+      const int model = l1term ? col / args.d_model : 0;
+#pragma unroll
+      for (int i = 0; i < WG::TM; ++i) {
+        const int row = rbase + i * 16;
+        if (row >= M) continue;
         const int64_t o = (int64_t)row * args.ldo + col;
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e];
         if (l1term) {
-          const float nrm = args.norms[(int64_t)row * args.n_models + col / args.d_model];
-          const float c = nrm > 0.f ? cs / nrm : 0.f;
+          const float c = cs[i] * args.norms[(int64_t)row * args.n_models + model];  // norms = inverse norms
           float w[4];
           ld4<DT>(args.w_src, o, w);
 #pragma unroll
@@ -588,9 +656,10 @@ int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const
   return launch_dt<EPI_DACTS, true, true>(dtype, a, (hipStream_t)stream);
 }
 
-int cc_wgrad_dec(const void* acts, const void* g_recon, const void* W_dec, const float* norms, const float* colsum_acts,
-                 float l1_scale, void* grad_W_dec, float* sq_part, int64_t B, int64_t h, int64_t n, int64_t d, int dtype,
-                 void* stream) {
+int cc_wgrad_dec(const void* acts, const void* g_recon, const void* W_dec, const float* inv_norms,
+                 const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_part, int64_t B, int64_t h,
+                 int64_t n, int64_t d, int dtype, void* stream) {
+  const float* norms = inv_norms;
   if (!grad_W_dec) return CC_ERR_NULL;
   if (l1_scale != 0.f && (!W_dec || !norms || !colsum_acts)) return CC_ERR_NULL;
   GemmArgs a = {};

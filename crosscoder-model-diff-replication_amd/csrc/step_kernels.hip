@@ -49,17 +49,33 @@ __global__ __launch_bounds__(256) void prep_kernel(const void* __restrict__ x_in
 
 // ---------------------------------------------------------------------------------------
 // out[j] = scale * sum_i part[i*ld + j]; optional dtype copy and squared-sum partial per block.
+// Block = 64 columns x 4 waves; wave w sums rows w, w+4, ... (independent loads in flight),
+// then a fixed-order combine of the 4 wave partials.  One sq partial per block.
+constexpr int RED_COLS = 64;
 template <int DT>
 __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ part, int R, int C, int64_t ld,
                                                           float scale, float* __restrict__ out_f32,
                                                           void* __restrict__ out_t, float* __restrict__ sq_part) {
-  __shared__ float red[4];
-  const int j = blockIdx.x * 256 + threadIdx.x;
+  __shared__ float red[4][RED_COLS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = blockIdx.x * RED_COLS + lane;
+  float s = 0.f;
+  if (j < C) {
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int i = wave;
+    for (; i + 12 < R; i += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += part[(int64_t)(i + 4 * u) * ld + j];
+    }
+    for (; i < R; i += 4) a[0] += part[(int64_t)i * ld + j];
+    s = (a[0] + a[1]) + (a[2] + a[3]);
+  }
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave != 0) return;
   float sq = 0.f;
   if (j < C) {
-    float s = 0.f;
-    for (int i = 0; i < R; ++i) s += part[(int64_t)i * ld + j];
-    s *= scale;
+    s = (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]) * scale;
     if (out_f32) out_f32[j] = s;
     if (out_t) {
       typename Elem<DT>::T q = Elem<DT>::from_f(s);
@@ -70,32 +86,42 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
   }
   if (!sq_part) return;
   sq = wave_sum(sq);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
-  __syncthreads();
-  if (threadIdx.x == 0) sq_part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+  if (lane == 0) sq_part[blockIdx.x] = sq;
 }
 
 // ---------------------------------------------------------------------------------------
 // norms[h][m] = ||W_dec[h,m,:]||, total[h] = sum_m.  One wave per (h) row, all models.
 template <int DT>
 __global__ __launch_bounds__(256) void dec_norms_kernel(const void* __restrict__ W, float* __restrict__ norms,
-                                                        float* __restrict__ total, int h, int n, int d) {
+                                                        float* __restrict__ total, float* __restrict__ inv_norms, int h,
+                                                        int n, int d) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= h) return;
   float tot = 0.f;
   for (int m = 0; m < n; ++m) {
     const int64_t base = ((int64_t)row * n + m) * d;
-    float s = 0.f;
-    for (int c = lane * 8; c < d; c += 512) {
+    float s0 = 0.f, s1 = 0.f;
+    int c = lane * 8;
+    for (; c + 512 < d; c += 1024) {  // two 16-B loads in flight per lane
+      float v[8], u[8];
+      load8<DT>(W, base + c, v);
+      load8<DT>(W, base + c + 512, u);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s0 += v[j] * v[j]; s1 += u[j] * u[j]; }
+    }
+    if (c < d) {
       float v[8];
       load8<DT>(W, base + c, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += v[j] * v[j];
+      for (int j = 0; j < 8; ++j) s0 += v[j] * v[j];
     }
-    s = wave_sum(s);
-    float nr = sqrtf(s);
-    if (lane == 0) norms[(int64_t)row * n + m] = nr;
+    const float s = wave_sum(s0 + s1);
+    const float nr = sqrtf(s);
+    if (lane == 0) {
+      norms[(int64_t)row * n + m] = nr;
+      if (inv_norms) inv_norms[(int64_t)row * n + m] = nr > 0.f ? 1.f / nr : 0.f;
+    }
     tot += nr;
   }
   if (lane == 0) total[row] = tot;
@@ -207,19 +233,21 @@ __global__ __launch_bounds__(256) void ev_kernel(const float* __restrict__ row_p
 }
 
 // Single block: scalars = {l2, l1, l0, mean ev, mean ev_a, mean ev_b}.
-__global__ __launch_bounds__(256) void loss_scalars_kernel(const float* __restrict__ ev_part, int nblk,
-                                                           const float* __restrict__ l1_part,
-                                                           const float* __restrict__ l0_part, int64_t n_wave, int B,
-                                                           float* __restrict__ scalars) {
-  __shared__ double red[4][6];
+constexpr int SCAL_THREADS = 1024;
+__global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const float* __restrict__ ev_part, int nblk,
+                                                                    const float* __restrict__ l1_part,
+                                                                    const float* __restrict__ l0_part, int64_t n_wave,
+                                                                    int B, float* __restrict__ scalars) {
+  constexpr int NW = SCAL_THREADS / 64;
+  __shared__ double red[NW][6];
   double acc[6] = {0, 0, 0, 0, 0, 0};
-  for (int i = threadIdx.x; i < nblk; i += 256) {
+  for (int i = threadIdx.x; i < nblk; i += SCAL_THREADS) {
     acc[0] += ev_part[i * 4 + 0];
     acc[3] += ev_part[i * 4 + 1];
     acc[4] += ev_part[i * 4 + 2];
     acc[5] += ev_part[i * 4 + 3];
   }
-  for (int64_t i = threadIdx.x; i < n_wave; i += 256) {
+  for (int64_t i = threadIdx.x; i < n_wave; i += SCAL_THREADS) {
     if (l1_part) acc[1] += l1_part[i];
     if (l0_part) acc[2] += l0_part[i];
   }
@@ -231,7 +259,8 @@ __global__ __launch_bounds__(256) void loss_scalars_kernel(const float* __restri
   __syncthreads();
   if (threadIdx.x < 6) {
     int q = threadIdx.x;
-    double s = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
+    double s = 0.0;
+    for (int w = 0; w < NW; ++w) s += red[w][q];
     scalars[q] = (float)(s / (double)B);
   }
   if (threadIdx.x == 6) scalars[6] = 0.f;
@@ -249,22 +278,32 @@ struct ClipArgs {
   int emulate_bf16;
   float* out;
 };
-__global__ __launch_bounds__(256) void clip_kernel(const ClipArgs a) {
-  __shared__ double red[4];
+__global__ __launch_bounds__(SCAL_THREADS) void clip_kernel(const ClipArgs a) {
+  constexpr int NW = SCAL_THREADS / 64;
+  __shared__ double red[8][NW];
   __shared__ float norms[8];
-  for (int p = 0; p < a.nparams; ++p) {
-    double s = 0.0;
-    for (int64_t i = a.off[p] + threadIdx.x; i < a.off[p + 1]; i += 256) s += (double)a.sq[i];
-    s = wave_sum_d(s);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float nr = (float)sqrt(((red[0] + red[1]) + red[2]) + red[3]);
-      if (a.emulate_bf16) nr = bf16r(nr);  // torch._foreach_norm on bf16 returns bf16
-      norms[p] = nr;
-    }
-    __syncthreads();
+  // all parameters in one pass: each thread keeps one running sum per parameter
+  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    if (p < a.nparams)
+      for (int64_t i = a.off[p] + threadIdx.x; i < a.off[p + 1]; i += SCAL_THREADS) s[p] += (double)a.sq[i];
   }
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    double t = wave_sum_d(s[p]);
+    if ((threadIdx.x & 63) == 0) red[p][threadIdx.x >> 6] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < a.nparams) {
+    const int p = threadIdx.x;
+    double t = 0.0;
+    for (int w = 0; w < NW; ++w) t += red[p][w];
+    float nr = (float)sqrt(t);
+    if (a.emulate_bf16) nr = bf16r(nr);  // torch._foreach_norm on bf16 returns bf16
+    norms[p] = nr;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int p = 0; p < a.nparams; ++p) s += norms[p] * norms[p];
@@ -310,7 +349,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
     float p[8], g[8], m[8], v[8];
     const bool full = i + 8 <= a.numel;
     if (full) {
-      load8<DT>(a.p, i, p); load8<DT>(a.g, i, g); load8<DT>(a.m, i, m); load8<DT>(a.v, i, v);
+      load8_nt<DT>(a.p, i, p); load8_nt<DT>(a.g, i, g); load8_nt<DT>(a.m, i, m); load8_nt<DT>(a.v, i, v);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -339,7 +378,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
       p[j] = pj; m[j] = mj; v[j] = vj;
     }
     if (full) {
-      store8<DT>(a.p, i, p); store8<DT>(a.m, i, m); store8<DT>(a.v, i, v);
+      store8_nt<DT>(a.p, i, p); store8_nt<DT>(a.m, i, m); store8_nt<DT>(a.v, i, v);
     } else {
       for (int j = 0; j < 8 && i + j < a.numel; ++j) {
         ((typename E::T*)a.p)[i + j] = E::from_f(p[j]);
@@ -385,6 +424,7 @@ int64_t cc_prep_part_rows(int64_t B) { return (B + PREP_ROWS - 1) / PREP_ROWS; }
 int64_t cc_loss_part_rows(int64_t B) { return (B + LOSS_ROWS - 1) / LOSS_ROWS; }
 int64_t cc_loss_col_blocks(int64_t d) { return (d + LOSS_COLS - 1) / LOSS_COLS; }
 int64_t cc_loss_scalars_len(int64_t B) { return 8 + 4 * ((B + 255) / 256); }
+int64_t cc_reduce_parts(int64_t C) { return (C + RED_COLS - 1) / RED_COLS; }
 
 int cc_prep_input(const void* x_in, int in_dtype, const void* factor, int factor_dtype, void* x_out,
                   float* colsum_part, int64_t B, int64_t n, int64_t d, int dtype, void* stream) {
@@ -416,7 +456,7 @@ int cc_reduce_rows(const float* part, int64_t R, int64_t C, int64_t ld, float sc
   if (!part) return CC_ERR_NULL;
   if (R <= 0 || C <= 0) return CC_ERR_SHAPE;
   if (sq_part && !out_t) return CC_ERR_NULL;
-  dim3 grid((unsigned)((C + 255) / 256));
+  dim3 grid((unsigned)((C + RED_COLS - 1) / RED_COLS));
   hipStream_t st = (hipStream_t)stream;
   if (out_t) {
     DISPATCH_DT(dtype, hipLaunchKernelGGL((reduce_rows_kernel<DT_>), grid, dim3(256), 0, st, part, (int)R, (int)C, ld,
@@ -429,15 +469,15 @@ int cc_reduce_rows(const float* part, int64_t R, int64_t C, int64_t ld, float sc
   return CC_OK;
 }
 
-int cc_dec_norms(const void* W_dec, float* norms, float* total, int64_t h, int64_t n, int64_t d, int dtype,
-                 void* stream) {
+int cc_dec_norms(const void* W_dec, float* norms, float* total, float* inv_norms, int64_t h, int64_t n, int64_t d,
+                 int dtype, void* stream) {
   if (!W_dec || !norms || !total) return CC_ERR_NULL;
   if (h <= 0 || n <= 0 || d <= 0 || d % 8) return CC_ERR_SHAPE;
   if (!al16(W_dec)) return CC_ERR_ALIGN;
   dim3 grid((unsigned)((h + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
-  DISPATCH_DT(dtype, hipLaunchKernelGGL((dec_norms_kernel<DT_>), grid, dim3(256), 0, st, W_dec, norms, total, (int)h,
-                                        (int)n, (int)d));
+  DISPATCH_DT(dtype, hipLaunchKernelGGL((dec_norms_kernel<DT_>), grid, dim3(256), 0, st, W_dec, norms, total,
+                                        inv_norms, (int)h, (int)n, (int)d));
   CC_LAUNCH_CHECK();
   return CC_OK;
 }
@@ -468,7 +508,7 @@ int cc_loss_finalize(const float* row_part, const float* l1_part, const float* l
   float* ev_part = scalars + 8;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(ev_kernel, dim3(nblk), dim3(256), 0, st, row_part, (int)B, (int)n, ncb, ev, ev_a, ev_b, ev_part);
-  hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(256), 0, st, ev_part, nblk, l1_part, l0_part, n_wave, (int)B,
+  hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(SCAL_THREADS), 0, st, ev_part, nblk, l1_part, l0_part, n_wave, (int)B,
                      scalars);
   CC_LAUNCH_CHECK();
   return CC_OK;
@@ -485,7 +525,7 @@ int cc_clip_finalize(const float* sq, const int64_t* off, int nparams, float max
   a.max_norm = max_norm;
   a.emulate_bf16 = emulate_bf16;
   a.out = out;
-  hipLaunchKernelGGL(clip_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(clip_kernel, dim3(1), dim3(SCAL_THREADS), 0, (hipStream_t)stream, a);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }

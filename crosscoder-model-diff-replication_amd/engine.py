@@ -105,7 +105,8 @@ class StepWorkspace:
         self.g_pre = E(B, h, dt=dtype)
         self.gpre_colpart = E(ops.col_part_rows(B), h)
         nw_w = ops.wgrad_parts(h, K, dtype)
-        sizes = [nw_w, nw_w, (h + 255) // 256, (K + 255) // 256]
+        self.inv_norms = E(h, n)
+        sizes = [nw_w, nw_w, ops.reduce_parts(h), ops.reduce_parts(K)]
         self.sq_off = [0]
         for s in sizes:
             self.sq_off.append(self.sq_off[-1] + s)
@@ -122,7 +123,7 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True):
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
     ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart)
     ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
-    ops.dec_norms(P.W_dec_hk, h, n, d, norms=ws.norms, total=ws.tn)
+    ops.dec_norms(P.W_dec_hk, h, n, d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
     with _span("G1_encode"):
         ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, tn=ws.tn, colsum_part=ws.acts_colpart,
                        l1_part=ws.l1_part, l0_part=ws.l0_part)
@@ -147,7 +148,7 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0):
     if l1_scale != 0.0:
         ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts)
     with _span("G4_wgrad_dec"):
-        ops.wgrad_dec(ws.acts, ws.g_recon, P.W_dec_hk, ws.norms, ws.colsum_acts, l1_scale, G.W_dec_hk,
+        ops.wgrad_dec(ws.acts, ws.g_recon, P.W_dec_hk, ws.inv_norms, ws.colsum_acts, l1_scale, G.W_dec_hk,
                       ws.sq_slice(1), n, d)
     with _span("G5_wgrad_enc"):
         ops.wgrad_enc(ws.g_pre, ws.x, G.W_enc_hk, ws.sq_slice(0))

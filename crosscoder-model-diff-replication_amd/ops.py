@@ -107,13 +107,17 @@ def reduce_rows(part, R, C, scale=1.0, out_f32=None, out_t=None, sq_part=None, l
                                dt, _ptr(sq_part), _stream(part)))
 
 
-def dec_norms(W_dec_hk, h, n, d, norms=None, total=None):
+def reduce_parts(C):
+    return int(lib().cc_reduce_parts(C))
+
+
+def dec_norms(W_dec_hk, h, n, d, norms=None, total=None, inv_norms=None):
     if norms is None:
         norms = torch.empty(h, n, device=W_dec_hk.device, dtype=torch.float32)
     if total is None:
         total = torch.empty(h, device=W_dec_hk.device, dtype=torch.float32)
-    check(lib().cc_dec_norms(_ptr(W_dec_hk), _ptr(norms), _ptr(total), h, n, d, dtype_code(W_dec_hk.dtype),
-                             _stream(W_dec_hk)))
+    check(lib().cc_dec_norms(_ptr(W_dec_hk), _ptr(norms), _ptr(total), _ptr(inv_norms), h, n, d,
+                             dtype_code(W_dec_hk.dtype), _stream(W_dec_hk)))
     return norms, total
 
 

@@ -76,14 +76,16 @@ int cc_prep_input(const void* x_in, int in_dtype, const void* factor, int factor
                   float* colsum_part, int64_t B, int64_t n, int64_t d, int dtype, void* stream);
 
 /* out[j] = scale * sum_{i<R} part[i*ld + j] (fixed order).  Optional: out_f32, out_t (dtype),
- * sq_part (per 256-column block: sum of dtype-rounded out^2, for clip_grad_norm_). */
+ * sq_part [cc_reduce_parts(C)] (per column block: sum of dtype-rounded out^2, for clip_grad_norm_). */
 int cc_reduce_rows(const float* part, int64_t R, int64_t C, int64_t ld, float scale, float* out_f32,
                    void* out_t, int dtype, float* sq_part, void* stream);
+int64_t cc_reduce_parts(int64_t C);
 
 /* W_dec.norm(dim=-1) and its sum over models (crosscoder.py:123-125):
- * norms[h*n + m] = ||W_dec[h,m,:]||_2, total[h] = sum_m norms.  fp32 results. */
-int cc_dec_norms(const void* W_dec, float* norms, float* total, int64_t h, int64_t n, int64_t d, int dtype,
-                 void* stream);
+ * norms[h*n + m] = ||W_dec[h,m,:]||_2, total[h] = sum_m norms, inv_norms (optional) = 1/norms
+ * (0 where a norm is 0: the norm backward's masked value).  fp32 results. */
+int cc_dec_norms(const void* W_dec, float* norms, float* total, float* inv_norms, int64_t h, int64_t n,
+                 int64_t d, int dtype, void* stream);
 
 /* CrossCoder.encode (crosscoder.py:69-80): acts[B,h] = act(x[B,K] . W_enc + b_enc), W_enc stored
  * h-major [h][K] (its physical layout, crosscoder.py:55-58).  act = ReLU if apply_relu.
@@ -125,8 +127,9 @@ int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const
                  void* g_pre, float* colsum_part, int64_t B, int64_t K, int64_t h, int dtype, void* stream);
 
 /* W_dec.grad [h][K] = acts^T . g_recon + l1_scale * sum_b(acts[:,h]) * W_dec[h,m,:]/||W_dec[h,m,:]||
- * (norm backward is 0 where the norm is 0).  sq_part [cc_wgrad_parts(h,K,dtype)]: sum of grad^2. */
-int cc_wgrad_dec(const void* acts, const void* g_recon, const void* W_dec, const float* norms,
+ * (norm backward is 0 where the norm is 0; inv_norms from cc_dec_norms).
+ * sq_part [cc_wgrad_parts(h,K,dtype)]: sum of grad^2. */
+int cc_wgrad_dec(const void* acts, const void* g_recon, const void* W_dec, const float* inv_norms,
                  const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_part, int64_t B,
                  int64_t h, int64_t n, int64_t d, int dtype, void* stream);
 

@@ -45,7 +45,7 @@ def test_argument_validation_without_gpu():
     fake = ctypes.c_void_p(1 << 20)
     assert lib.cc_gemm_f32out(fake, 0, 8, fake, 0, 8, fake, 8, 8, 8, 8, 7, null) == 2        # dtype
     assert lib.cc_gemm_f32out(fake, 0, 12, fake, 0, 12, fake, 12, 8, 8, 12, 1, null) == 3    # K % 8
-    assert lib.cc_dec_norms(fake, fake, fake, 8, 2, 12, 1, null) == 3                          # d % 8
+    assert lib.cc_dec_norms(fake, fake, fake, null, 8, 2, 12, 1, null) == 3                         # d % 8
     assert lib.cc_clip_finalize(fake, (ctypes.c_int64 * 2)(0, 1), 9, 1.0, 0, fake, null) == 3
     assert b"NULL" in lib.cc_strerror(1)
     assert lib.cc_col_part_rows(4096) == 32 and lib.cc_wave_parts(4096, 16384) == 8 * 16 * 64

@@ -1,0 +1,82 @@
+"""A/B timing of the five step GEMMs (config-2 shapes) across library builds, interleaved in
+ONE process (cdna guide rule 24).  Usage: python tools/gemm_bench.py lib1.so [lib2.so ...]"""
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import crosscoder_amd  # noqa: F401,E402
+from crosscoder_amd._lib import SIGNATURES  # noqa: E402
+
+B, n, d, h = 4096, 2, 2304, 16384
+K = n * d
+PEAK = 256 * 2.4e9 * 4096 / 1e12
+
+
+def load(path):
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.restype, f.argtypes = res, args
+    return lib
+
+
+def main():
+    libs = [(p, load(p)) for p in sys.argv[1:]]
+    dev = torch.device("cuda:0")
+    bf = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(B, K, device=dev, generator=g).to(bf)
+    W = (torch.randn(h, K, device=dev, generator=g) * 0.02).to(bf)
+    W2 = (torch.randn(h, K, device=dev, generator=g) * 0.02).to(bf)
+    b_enc = torch.zeros(h, device=dev, dtype=bf)
+    acts = torch.empty(B, h, device=dev, dtype=bf)
+    recon = torch.empty(B, K, device=dev)
+    g_recon = (torch.randn(B, K, device=dev, generator=g) * 1e-3).to(bf)
+    g_pre = torch.empty(B, h, device=dev, dtype=bf)
+    tn = torch.ones(h, device=dev)
+    norms = torch.ones(h, n, device=dev)
+    colsum = torch.ones(h, device=dev)
+    gW = torch.empty(h, K, device=dev, dtype=bf)
+    parts = torch.empty(1 << 20, device=dev)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    N0 = ctypes.c_void_p(0)
+
+    def calls(L):
+        return {
+            "G1_encode": lambda: L.cc_encode_fwd(P(x), P(W), P(b_enc), P(tn), P(acts), 1, P(parts), P(parts), P(parts),
+                                                 B, K, h, 1, st),
+            "G2_decode": lambda: L.cc_decode_fwd(P(acts), P(W2), N0, P(recon), N0, B, h, K, 1, st),
+            "G3_dacts": lambda: L.cc_dacts_bwd(P(g_recon), P(W2), P(acts), P(tn), 1e-4, P(g_pre), P(parts), B, K, h, 1,
+                                               st),
+            "G4_wgrad_dec": lambda: L.cc_wgrad_dec(P(acts), P(g_recon), P(W2), P(norms), P(colsum), 1e-4, P(gW),
+                                                   P(parts), B, h, n, d, 1, st),
+            "G5_wgrad_enc": lambda: L.cc_wgrad_enc(P(g_pre), P(x), P(gW), P(parts), B, h, K, 1, st),
+        }
+
+    flop = 2.0 * B * K * h
+    res = {}
+    for rnd in range(5):
+        for path, L in libs:
+            for name, fn in calls(L).items():
+                for _ in range(2):
+                    assert fn() == 0
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(10):
+                    fn()
+                e.record()
+                torch.cuda.synchronize()
+                res.setdefault((os.path.basename(path), name), []).append(s.elapsed_time(e) / 10)
+    for (p, name), ts in sorted(res.items(), key=lambda kv: (kv[0][1], kv[0][0])):
+        ts.sort()
+        med = ts[len(ts) // 2]
+        print(f"{name:14s} {p:34s} median {med*1e3:7.1f} us  min {ts[0]*1e3:7.1f} us  {flop/med/1e9:7.1f} TF/s "
+              f"({flop/med/1e9/PEAK*100:4.1f}% peak)")
+
+
+if __name__ == "__main__":
+    main()
