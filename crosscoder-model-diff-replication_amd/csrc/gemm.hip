@@ -55,6 +55,7 @@ struct GemmArgs {
   float scale0;
   int flag;             // apply_relu
   int d_model, n_models;
+  void* dbg;            // diagnostic stamp buffer (CC_STAMPS builds only)
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -139,6 +140,84 @@ CC_DEV void dma_mn(__amdgpu_buffer_rsrc_t r, char* lds, char* junk, int q, bool 
   const bool ok = use && (k0 + k) < K && col < cols_left;
   const uint32_t voff = ok ? (uint32_t)(((int64_t)(k0 + k) * ld + col) * G::ES) : OOB;
   dma16(r, use ? lds + ci * 1024 : junk, voff);
+}
+
+// Step-invariant part of the q-th DMA's per-lane source offset (bytes from the panel origin at
+// k0 = 0), or OOB; the step adds k0 through the scalar soffset (k0*ES for KC, k0*ld*ES for MN),
+// so the steady-state K loop spends no VALU on DMA addressing.  Valid when the whole K step is
+// in range (k0 + BK <= K); the K-tail step uses dma_kc / dma_mn.
+template <int DT, int ROWS, int KROW>
+CC_DEV uint32_t dma_kc_base(int q, int rows_left, int64_t ld, int wave, int lane) {
+  using T = KcTile<KROW>;
+  constexpr int EPC = DT == CC_BF16 ? 8 : 4;
+  constexpr int ES = DT == CC_BF16 ? 2 : 4;
+  constexpr int NDMA = ROWS * KROW / 1024;
+  const int ci = q * 8 + wave;
+  const int row = ci * T::RPD + lane / T::CPR;
+  const int c = (lane % T::CPR) ^ T::swz(row);
+  const bool ok = (NDMA % 8 == 0 || ci < NDMA) && row < rows_left;
+  return ok ? (uint32_t)(((int64_t)row * ld + c * EPC) * ES) : OOB;
+}
+template <int DT, int COLS, int KROW>
+CC_DEV uint32_t dma_mn_base(int q, int cols_left, int64_t ld, int wave, int lane) {
+  using G = MnTile<DT, COLS, KROW>;
+  const int ci = q * 8 + wave;
+  const int b = ci * 1024 + lane * 16;
+  const int k = b / G::RB;
+  const int cph = (b - k * G::RB) >> 4;
+  int clog = cph - G::rot(k);
+  clog += clog < 0 ? G::CH : 0;
+  const int col = clog * G::EPC;
+  const bool ok = (G::NDMA % 8 == 0 || ci < G::NDMA) && col < cols_left;
+  return ok ? (uint32_t)(((int64_t)k * ld + col) * G::ES) : OOB;
+}
+CC_DEV void dma16s(__amdgpu_buffer_rsrc_t r, char* lds_base, uint32_t voff, uint32_t soff) {
+#ifdef CC_EXP_NOLOAD
+  voff = OOB;
+#endif
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_base, 16, (int)voff, (int)soff, 0, 0);
+}
+
+// Step-invariant LDS byte offset of a lane's MN fragment read for the 16-column group at col0
+// (the k rows 8*(l>>4) + (l&3)... of the slice go to immediates): rot(k) depends only on the
+// lane's row-within-slice bits, so the whole address is lane part + compile-time constant.
+template <int DT, int COLS, int KROW>
+CC_DEV int mn_frag_off(int col0, int lane) {
+  using G = MnTile<DT, COLS, KROW>;
+  if constexpr (DT == CC_BF16) {
+    const int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
+    const int k = 8 * g + qq;  // + 32*kk + 4*t (immediates; rot() is invariant under them)
+    int cph = ((col0 + 4 * pp) >> 3) + G::rot(k);
+    cph -= cph >= G::CH ? G::CH : 0;
+    return k * G::RB + cph * 16 + 8 * (pp & 1);
+  } else {
+    const int g = lane >> 4;
+    const int col = col0 + (lane & 15);
+    const int k = 4 * g;  // + 16*kk + e
+    int cph = (col >> 2) + G::rot(k);
+    cph -= cph >= G::CH ? G::CH : 0;
+    return k * G::RB + cph * 16 + 4 * (col & 3);
+  }
+}
+template <int COLS, int KROW>
+CC_DEV bf16x8 frag_mn_bf16_at(const char* tile, int off, int kk) {
+  using G = MnTile<CC_BF16, COLS, KROW>;
+  bf16x8 out;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(tile + off + (32 * kk + 4 * t) * G::RB));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[4 * t + e] = v[e];
+  }
+  return out;
+}
+template <int COLS, int KROW>
+CC_DEV f32x4 frag_mn_f32_at(const char* tile, int off, int kk) {
+  using G = MnTile<CC_F32, COLS, KROW>;
+  f32x4 out;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) out[e] = *(const float*)(tile + off + (16 * kk + e) * G::RB);
+  return out;
 }
 
 // ---- fragment reads, bf16 (16x16x32 operand map: lane l holds X[r = l&15][k = 8*(l>>4) + j]);
@@ -249,6 +328,10 @@ template <> struct Pipe<1> { static constexpr int KROW = 64, NST = 4; };
 #define CC_GEMM_PIPE 0
 #endif
 
+#ifndef CC_FRAG_MODE
+#define CC_FRAG_MODE 1
+#endif
+
 template <int N> CC_DEV void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   // gfx9 s_waitcnt encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]
@@ -303,10 +386,34 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 
   // q-th DMA (0..D-1) of this wave for K-step kt into stage s
   // q-th DMA (0..D-1) of this wave for K-step kt into stage s; steps >= nk go to the junk slot
+  uint32_t vo[D];  // step-invariant per-lane DMA source offsets (see dma_kc_base / dma_mn_base)
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+    if (q < DA)
+      vo[q] = AKC ? dma_kc_base<DT, BM, KROW>(q, M - m0, args.lda, wave, lane)
+                  : dma_mn_base<DT, BM, KROW>(q, M - m0, args.lda, wave, lane);
+    else
+      vo[q] = BKC ? dma_kc_base<DT, BNT, KROW>(q - DA, N - n0, args.ldb, wave, lane)
+                  : dma_mn_base<DT, BNT, KROW>(q - DA, N - n0, args.ldb, wave, lane);
+  }
   auto dma = [&](int q, int kt, int s, bool live) {
     char* la = smem + s * STAGE;
     char* lb = la + A_BYTES;
     const int k0 = kt * BK;
+    // MN operands, whole step in range: precomputed offsets + scalar k0 offset (measured slower
+    // than the per-step address math for KC operands, which keep it)
+    if (!(q < DA ? AKC : BKC) && k0 + BK <= K) {
+      const bool isA = q < DA;
+      const int ci = (isA ? q : q - DA) * 8 + wave;
+      const int ndma = (isA ? A_BYTES : B_BYTES) / 1024;
+      const bool use = live && ((isA ? A_BYTES : B_BYTES) / 1024 % 8 == 0 || ci < ndma);
+      char* dst = use ? (isA ? la : lb) + ci * 1024 : junk;
+      const bool kc = isA ? AKC : BKC;
+      const int64_t ld = isA ? args.lda : args.ldb;
+      const uint32_t soff = live ? (uint32_t)(kc ? (int64_t)k0 * ES : (int64_t)k0 * ld * ES) : 0u;
+      dma16s(isA ? ra : rb, dst, live ? vo[q] : OOB, soff);
+      return;
+    }
     if (q < DA) {
       if constexpr (AKC) dma_kc<DT, BM, KROW>(ra, la, junk, q, live, M - m0, k0, K, args.lda, wave, lane);
       else dma_mn<DT, BM, KROW>(ra, la, junk, q, live, M - m0, k0, K, args.lda, wave, lane);
@@ -323,6 +430,13 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 #pragma unroll
     for (int j = 0; j < WG::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // step-invariant per-lane LDS offsets of the MN fragment reads (transposed-read operands)
+  int offA[WG::TM], offB[WG::TN];
+#pragma unroll
+  for (int i = 0; i < WG::TM; ++i) offA[i] = AKC ? 0 : mn_frag_off<DT, BM, KROW>(wr * WG::WTM + i * 16, lane);
+#pragma unroll
+  for (int j = 0; j < WG::TN; ++j) offB[j] = BKC ? 0 : mn_frag_off<DT, BNT, KROW>(wc * WG::WTN + j * 16, lane);
+
   const int nk = (K + BK - 1) / BK;
   // prologue: steps 0 .. NST-2 in flight
 #pragma unroll
@@ -330,13 +444,46 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 #pragma unroll
     for (int q = 0; q < D; ++q) dma(q, p, p, p < nk);
 
+#ifdef CC_STAMPS  // diagnostic build only: per-wave cycle sums of {DMA wait, barrier, compute}
+  uint64_t st_wait = 0, st_bar = 0, st_comp = 0, st_t0 = 0, st_pro = 0;
+  auto stamp = [&]() -> uint64_t {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+  };
+  st_t0 = stamp();
+  uint64_t st_prev = st_t0;
+#endif
   for (int kt = 0; kt < nk; ++kt) {
     // step kt landed (this wave's DMAs): every step issues exactly D DMAs per wave, so the
     // NST-2 younger steps may stay in flight
+#ifdef CC_STAMPS
+    {
+      uint64_t t = stamp();
+      if (kt) st_comp += t - st_prev; else st_pro += t - st_prev;
+      st_prev = t;
+    }
+#endif
 #ifndef CC_EXP_NOWAIT  // timing-only experiment builds (never shipped): skip the DMA wait
     wait_vmcnt<(NST - 2) * D>();
 #endif
+#ifdef CC_STAMPS
+    {
+      uint64_t t = stamp();
+      st_wait += t - st_prev;
+      st_prev = t;
+    }
+#endif
     __builtin_amdgcn_s_barrier();  // ... for every wave; stage (kt-1)%NST is free again
+#ifdef CC_STAMPS
+    {
+      uint64_t t = stamp();
+      st_bar += t - st_prev;
+      st_prev = t;
+    }
+#endif
     const int nxt = kt + NST - 1;
     const bool pf = nxt < nk;
     const int snx = nxt % NST;
@@ -348,6 +495,44 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 #pragma unroll
       for (int q = 0; q < D; ++q) dma(q, nxt, snx, pf);
     }
+#if CC_FRAG_MODE > 0
+    if constexpr (DT == CC_BF16) {
+      // all fragments of the step (mode 2) or of each 32-k slice (mode 1) are read first, so a
+      // wave waits for LDS once per slice and then issues its MFMAs back to back
+      constexpr int KB = CC_FRAG_MODE == 2 ? KK : 1;
+#pragma unroll
+      for (int k0 = 0; k0 < KK; k0 += KB) {
+        bf16x8 a[KB][WG::TM], b[KB][WG::TN];
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+#pragma unroll
+          for (int j = 0; j < WG::TN; ++j) {
+            const int c0 = wc * WG::WTN + j * 16;
+            b[u][j] = BKC ? frag_kc_bf16<KROW>(lb, c0, k0 + u, lane) : frag_mn_bf16_at<BNT, KROW>(lb, offB[j], k0 + u);
+          }
+#pragma unroll
+          for (int i = 0; i < WG::TM; ++i) {
+            const int r0 = wr * WG::WTM + i * 16;
+            a[u][i] = AKC ? frag_kc_bf16<KROW>(la, r0, k0 + u, lane) : frag_mn_bf16_at<BM, KROW>(la, offA[i], k0 + u);
+          }
+        }
+        if (SPREAD && k0 == 0) {
+#pragma unroll
+          for (int q = 0; q < D; ++q) dma(q, nxt, snx, pf);
+        }
+#pragma unroll
+        for (int u = 0; u < KB; ++u)
+#pragma unroll
+          for (int i = 0; i < WG::TM; ++i)
+#pragma unroll
+            for (int j = 0; j < WG::TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[u][j], a[u][i], acc[i][j], 0, 0, 0);
+        // keep the reads ahead of the MFMAs (the scheduler otherwise sinks them for pressure)
+        __builtin_amdgcn_sched_group_barrier(0x100, KB * (WG::TM * (AKC ? 1 : 2) + WG::TN * (BKC ? 1 : 2)), 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, KB * WG::TM * WG::TN, 0);
+      }
+    } else
+#endif
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
       if constexpr (DT == CC_BF16) {
@@ -355,7 +540,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 #pragma unroll
         for (int j = 0; j < WG::TN; ++j) {
           const int c0 = wc * WG::WTN + j * 16;
-          b[j] = BKC ? frag_kc_bf16<KROW>(lb, c0, kk, lane) : frag_mn_bf16<BNT, KROW>(lb, c0, kk, lane);
+          b[j] = BKC ? frag_kc_bf16<KROW>(lb, c0, kk, lane) : frag_mn_bf16_at<BNT, KROW>(lb, offB[j], kk);
         }
 #pragma unroll
         for (int i = 0; i < WG::TM; ++i) {
@@ -365,7 +550,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
               if (q * WG::TM / D == i) dma(q, nxt, snx, pf);
           }
           const int r0 = wr * WG::WTM + i * 16;
-          bf16x8 a = AKC ? frag_kc_bf16<KROW>(la, r0, kk, lane) : frag_mn_bf16<BM, KROW>(la, r0, kk, lane);
+          bf16x8 a = AKC ? frag_kc_bf16<KROW>(la, r0, kk, lane) : frag_mn_bf16_at<BM, KROW>(la, offA[i], kk);
 #pragma unroll
           for (int j = 0; j < WG::TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a, acc[i][j], 0, 0, 0);
@@ -375,7 +560,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 #pragma unroll
         for (int j = 0; j < WG::TN; ++j) {
           const int c0 = wc * WG::WTN + j * 16;
-          b[j] = BKC ? frag_kc_f32<KROW>(lb, c0, kk, lane) : frag_mn_f32<BNT, KROW>(lb, c0, kk, lane);
+          b[j] = BKC ? frag_kc_f32<KROW>(lb, c0, kk, lane) : frag_mn_f32_at<BNT, KROW>(lb, offB[j], kk);
         }
 #pragma unroll
         for (int i = 0; i < WG::TM; ++i) {
@@ -385,7 +570,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
               if (q * WG::TM / D == i) dma(q, nxt, snx, pf);
           }
           const int r0 = wr * WG::WTM + i * 16;
-          f32x4 a = AKC ? frag_kc_f32<KROW>(la, r0, kk, lane) : frag_mn_f32<BM, KROW>(la, r0, kk, lane);
+          f32x4 a = AKC ? frag_kc_f32<KROW>(la, r0, kk, lane) : frag_mn_f32_at<BM, KROW>(la, offA[i], kk);
 #pragma unroll
           for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -396,6 +581,17 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
     }
   }
   wait_vmcnt<0>();  // drain the junk-slot DMAs of the last NST-1 steps
+#ifdef CC_STAMPS
+  {
+    uint64_t t = stamp();
+    st_comp += t - st_prev;
+    uint64_t* dbg = (uint64_t*)args.dbg;
+    if (dbg && lane == 0) {
+      uint64_t* o = dbg + ((uint64_t)blockIdx.x * 8 + wave) * 6;
+      o[0] = st_pro; o[1] = st_wait; o[2] = st_bar; o[3] = st_comp; o[4] = t - st_t0; o[5] = nk;
+    }
+  }
+#endif
 
   // ------------------------------- epilogue (transposed C fragments) -------------------------
   const int rbase = m0 + wr * WG::WTM + (lane & 15);
@@ -546,8 +742,16 @@ static int pick_bn(int64_t N, bool bkc, int dtype) {
 }
 static int64_t n_blocks(int64_t M, int64_t N, int bn) { return ((M + BM - 1) / BM) * ((N + bn - 1) / bn); }
 
+#ifdef CC_STAMPS
+static void* g_stamp_buf = nullptr;
+extern "C" void cc_debug_set_stamp_buffer(void* p) { g_stamp_buf = p; }
+#endif
+
 template <int DT, bool AKC, bool BKC, int EPI, int BNT>
 static int launch(GemmArgs a, hipStream_t st) {
+#ifdef CC_STAMPS
+  a.dbg = g_stamp_buf;
+#endif
   a.nbm = (a.M + BM - 1) / BM;
   a.nbn = (a.N + BNT - 1) / BNT;
   dim3 grid(a.nbm * a.nbn), block(NTHR);
