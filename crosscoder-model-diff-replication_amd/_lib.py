@@ -9,6 +9,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcrosscoder_hip.so")
+DEFAULT_PP_MASK = 5  # CC_PP_MASK the library is built with (csrc/gemm.hip)
 
 CC_BF16 = 1
 CC_F32 = 2
@@ -69,6 +70,9 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # tuning hook outside the public ABI: which bf16 layouts run the ping-pong GEMM loop
+    lib.cc_debug_set_pp_mask.restype = None
+    lib.cc_debug_set_pp_mask.argtypes = [ctypes.c_int]
     _lib = lib
     return lib
 

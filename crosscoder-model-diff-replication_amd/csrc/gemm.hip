@@ -319,6 +319,31 @@ template <int DT> CC_DEV void st4(void* p, int64_t idx, const float v[4]) {
   }
 }
 
+// raw 4-element vectors held across an epilogue batch (8 B bf16 / 16 B fp32 per lane)
+template <int DT> struct V4;
+template <> struct V4<CC_BF16> {
+  typedef bf16x4 T;
+  static CC_DEV T load(const void* p, int64_t idx) { return *(const bf16x4*)((const bf16_t*)p + idx); }
+  static CC_DEV T zero() { return bf16x4{0, 0, 0, 0}; }
+  static CC_DEV float get(T v, int e) { return bf2f((bf16_t)v[e]); }
+};
+template <> struct V4<CC_F32> {
+  typedef f32x4 T;
+  static CC_DEV T load(const void* p, int64_t idx) { return *(const f32x4*)((const float*)p + idx); }
+  static CC_DEV T zero() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+  static CC_DEV float get(T v, int e) { return v[e]; }
+};
+// epilogue load batch: JB column groups x TM row groups of vectors in flight per batch
+template <int DT, int BNT>
+struct EPB {
+  static constexpr int JB = DT == CC_F32 ? 1 : (WaveGeom<BNT>::TM * WaveGeom<BNT>::TN <= 32 ? WaveGeom<BNT>::TN : 3);
+  // W_dec term (vector + per-row factor each): half the batch within 256 VGPRs
+  static constexpr int JB_W = DT == CC_F32 ? 1 : (WaveGeom<BNT>::TN == 4 ? 2 : 3);
+  // activation mask of d_acts (kept beside the per-fragment output offsets)
+  static constexpr int JB_M = DT == CC_F32 ? 1 : (WaveGeom<BNT>::TN == 4 ? 1 : 3);
+  static_assert(WaveGeom<BNT>::TN % JB == 0 && WaveGeom<BNT>::TN % JB_W == 0, "batch must divide the column groups");
+};
+
 // PIPE selects the K pipeline: KROW bytes per KC row per K-step and NST LDS stages.
 //   PIPE 0: KROW 128, NST 2 (prefetch 1 step)   PIPE 1: KROW 64, NST 4 (prefetch 3 steps)
 template <int PIPE> struct Pipe;
@@ -338,9 +363,10 @@ template <int N> CC_DEV void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
+#include "gemm_epilogue.h"
+
 template <int DT, bool AKC, bool BKC, int EPI, int BNT, int PIPE = CC_GEMM_PIPE>
 __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
-  using E = Elem<DT>;
   using WG = WaveGeom<BNT>;
   constexpr int KROW = Pipe<PIPE>::KROW, NST = Pipe<PIPE>::NST;
   constexpr int ES = DT == CC_BF16 ? 2 : 4;
@@ -593,151 +619,27 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
   }
 #endif
 
-  // ------------------------------- epilogue (transposed C fragments) -------------------------
-  const int rbase = m0 + wr * WG::WTM + (lane & 15);
-  const int cbase = n0 + wc * WG::WTN + 4 * (lane >> 4);
-  const int wave_slot = blockIdx.x * 8 + wave;
-  // N % 4 == 0 (checked on the host), so a lane's 4 columns are all valid or all invalid.
-
-  if constexpr (EPI == EPI_F32 || EPI == EPI_DEC) {
-    const typename E::T* bias = (const typename E::T*)args.bias;
-#pragma unroll
-    for (int j = 0; j < WG::TN; ++j) {
-      const int col = cbase + j * 16;
-      if (col >= N) continue;
-      float bc[4] = {0.f, 0.f, 0.f, 0.f};
-      if (EPI == EPI_DEC && bias) ld4<DT>(bias, col, bc);
-#pragma unroll
-      for (int i = 0; i < WG::TM; ++i) {
-        const int row = rbase + i * 16;
-        if (row >= M) continue;
-        const int64_t o = (int64_t)row * args.ldo + col;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bc[e];
-        if constexpr (EPI == EPI_F32) {
-          st4<CC_F32>(args.out, o, v);
-        } else {
-          if (args.out_f32) st4<CC_F32>(args.out_f32, o, v);
-          if (args.out) st4<DT>(args.out, o, v);
-        }
-      }
-    }
-  } else if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
-    float s_l1 = 0.f, s_l0 = 0.f;
-#pragma unroll
-    for (int j = 0; j < WG::TN; ++j) {
-      const int col = cbase + j * 16;
-      const bool cv = col < N;
-      float add[4] = {0.f, 0.f, 0.f, 0.f}, tnc[4] = {0.f, 0.f, 0.f, 0.f}, csum[4] = {0.f, 0.f, 0.f, 0.f};
-      if (cv) {
-        if constexpr (EPI == EPI_ENC) {
-          if (args.bias) ld4<DT>(args.bias, col, add);
-          if (args.tn) ld4<CC_F32>(args.tn, col, tnc);
-        } else {
-          if (args.tn) {
-            ld4<CC_F32>(args.tn, col, add);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) add[e] *= args.scale0;
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < WG::TM; ++i) {
-        const int row = rbase + i * 16;
-        if (!cv || row >= M) continue;
-        const int64_t o = (int64_t)row * args.ldo + col;
-        float v[4], mk[4];
-        if constexpr (EPI == EPI_DACTS) ld4<DT>(args.mask_src, o, mk);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float t = acc[i][j][e] + add[e];
-          if constexpr (EPI == EPI_ENC) {
-            if (args.flag) t = fmaxf(t, 0.f);
-          } else {
-            t = mk[e] > 0.f ? t : 0.f;
-          }
-          v[e] = E::round(t);
-          csum[e] += v[e];
-          if constexpr (EPI == EPI_ENC) {
-            s_l1 += v[e] * tnc[e];
-            s_l0 += v[e] > 0.f ? 1.f : 0.f;
-          }
-        }
-        st4<DT>(args.out, o, v);
-      }
-      if (args.col_part) {  // reduce over the 16 lanes (rows) that share these 4 columns
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float s = csum[e];
-          s += __shfl_xor(s, 1, 64);
-          s += __shfl_xor(s, 2, 64);
-          s += __shfl_xor(s, 4, 64);
-          s += __shfl_xor(s, 8, 64);
-          csum[e] = s;
-        }
-        if ((lane & 15) == 0 && cv)
-          st4<CC_F32>(args.col_part, (int64_t)(tm * WG::WARPS_M + wr) * N + col, csum);
-      }
-    }
-    if constexpr (EPI == EPI_ENC) {
-      if (args.wave_part0) {
-        float t = wave_sum(s_l1);
-        if (lane == 0) args.wave_part0[wave_slot] = t;
-      }
-      if (args.wave_part1) {
-        float t = wave_sum(s_l0);
-        if (lane == 0) args.wave_part1[wave_slot] = t;
-      }
-    }
-  } else if constexpr (EPI == EPI_WGDEC || EPI == EPI_WGENC) {
-    float sq = 0.f;
-    const bool l1term = EPI == EPI_WGDEC && args.scale0 != 0.f;
-    // per-row factor scale * sum_b acts[b, row] and, per (row, model), 1/||W_dec[row, model]||
-    float cs[WG::TM];
-#pragma unroll
-    for (int i = 0; i < WG::TM; ++i) {
-      const int row = rbase + i * 16;
-      cs[i] = (l1term && row < M) ? args.scale0 * args.colsum[row] : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < WG::TN; ++j) {
-      const int col = cbase + j * 16;
-      if (col >= N) continue;
-      const int model = l1term ? col / args.d_model : 0;
-#pragma unroll
-      for (int i = 0; i < WG::TM; ++i) {
-        const int row = rbase + i * 16;
-        if (row >= M) continue;
-        const int64_t o = (int64_t)row * args.ldo + col;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e];
-        if (l1term) {
-          const float c = cs[i] * args.norms[(int64_t)row * args.n_models + model];  // norms = inverse norms
-          float w[4];
-          ld4<DT>(args.w_src, o, w);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += c * w[e];
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = E::round(v[e]);
-          sq += v[e] * v[e];
-        }
-        st4<DT>(args.out, o, v);
-      }
-    }
-    if (args.wave_part0) {
-      float t = wave_sum(sq);
-      if (lane == 0) args.wave_part0[wave_slot] = t;
-    }
-  }
+  gemm_epilogue<DT, EPI, BNT>(args, acc, tm, m0, n0, wr, wc, lane, blockIdx.x * 8 + wave);
 }
+
+#include "gemm_pp.h"
 
 // N = n*d multiple of 288 (and an MN-contiguous bf16 B operand): 256 x 288 tiles.  (The fp32
 // parity mode keeps 256 x 256: its 288-wide variant exceeds 256 VGPRs.)
-static int pick_bn(int64_t N, bool bkc, int dtype) {
+// bf16 GEMMs whose layout bit is set in CC_PP_MASK run the ping-pong kernel (gemm_pp.h, 256 x 256
+// tiles): bit 0 KC/KC (G1, G3), bit 1 KC/MN (G2), bit 2 MN/MN (G4, G5).
+#ifndef CC_PP_MASK
+#define CC_PP_MASK 5
+#endif
+static int g_pp_mask = CC_PP_MASK;  // cc_debug_set_pp_mask: in-process A/B of the two loops
+static bool use_pp(bool akc, bool bkc, int dtype) {
+  if (dtype != CC_BF16 || (!akc && bkc)) return false;
+  const int bit = akc && bkc ? 0 : (akc ? 1 : 2);
+  return (g_pp_mask >> bit) & 1;
+}
+extern "C" void cc_debug_set_pp_mask(int mask) { g_pp_mask = mask; }
+static int pick_bn(int64_t N, bool akc, bool bkc, int dtype) {
+  if (use_pp(akc, bkc, dtype)) return 256;
   return (!bkc && dtype == CC_BF16 && N % 288 == 0) ? 288 : 256;
 }
 static int64_t n_blocks(int64_t M, int64_t N, int bn) { return ((M + BM - 1) / BM) * ((N + bn - 1) / bn); }
@@ -760,10 +662,22 @@ static int launch(GemmArgs a, hipStream_t st) {
   return CC_OK;
 }
 
+template <bool AKC, bool BKC, int EPI>
+static int launch_pp(GemmArgs a, hipStream_t st) {
+  a.nbm = (a.M + BM - 1) / BM;
+  a.nbn = (a.N + 255) / 256;
+  hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI>), dim3(a.nbm * a.nbn), dim3(NTHR), 0, st, a);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
 template <int EPI, bool AKC, bool BKC>
 static int launch_dt(int dtype, GemmArgs a, hipStream_t st) {
+  if constexpr (!(!AKC && BKC)) {
+    if (use_pp(AKC, BKC, dtype)) return launch_pp<AKC, BKC, EPI>(a, st);
+  }
   if constexpr (!BKC) {
-    if (pick_bn(a.N, BKC, dtype) == 288) return launch<CC_BF16, AKC, BKC, EPI, 288>(a, st);
+    if (pick_bn(a.N, AKC, BKC, dtype) == 288) return launch<CC_BF16, AKC, BKC, EPI, 288>(a, st);
   }
   if (dtype == CC_BF16) return launch<CC_BF16, AKC, BKC, EPI, 256>(a, st);
   if (dtype == CC_F32) return launch<CC_F32, AKC, BKC, EPI, 256>(a, st);
@@ -801,7 +715,8 @@ extern "C" {
 
 int64_t cc_col_part_rows(int64_t M) { return 2 * ((M + BM - 1) / BM); }
 int64_t cc_wave_parts(int64_t M, int64_t N) { return 8 * n_blocks(M, N, 256); }
-int64_t cc_wgrad_parts(int64_t h, int64_t K, int dtype) { return 8 * n_blocks(h, K, pick_bn(K, false, dtype)); }
+// exactly the partials the weight-gradient GEMMs write (the clip sums all of them)
+int64_t cc_wgrad_parts(int64_t h, int64_t K, int dtype) { return 8 * n_blocks(h, K, pick_bn(K, false, false, dtype)); }
 
 int cc_gemm_f32out(const void* A, int a_layout, int64_t lda, const void* Bm, int b_layout, int64_t ldb, float* C,
                    int64_t ldc, int64_t M, int64_t N, int64_t K, int dtype, void* stream) {

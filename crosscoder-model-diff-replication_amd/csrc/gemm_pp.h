@@ -1,0 +1,218 @@
+// Ping-pong bf16 main loop (included by gemm.hip inside namespace cc).
+//
+// Tile 256 x 256, BK 64, 8 waves 2(M) x 4(N), 128 x 64 outputs per wave (the same accumulator
+// map as gemm_kernel<.., 256>, so the epilogues are shared).  The two wave rows form two groups
+// (waves 0-3 and 4-7: one wave of each per SIMD) that run half a phase apart: while one group
+// issues its MFMAs the other reads its next fragments from LDS and issues its share of the
+// LDS-DMA traffic, so each SIMD's matrix pipe alternates between its two waves.
+//
+// Per K-step each wave runs 4 phases p; phase p = 16 MFMAs (A tiles i = 2p, 2p+1 x the 4 B
+// tiles x 2 k-slices).  Fragment reads: all B fragments in phase 0 (kept for the step), the two
+// A fragments of the phase in each phase.  Each phase is
+//     [ds_read fragments][issue 2 LDS-DMAs][vmcnt(6)] barrier [16 MFMA] barrier
+// and group 1 starts one barrier late (group 0 ends with one extra barrier).
+//
+// LDS: 2 buffers x (A tile 32 KB | B tile 32 KB).  The DMA traffic of one K-step (64 x 1 KB)
+// is split over the 4 phases by LDS region, in the order the regions free up:
+//   phase 0: A rows {0..63, 128..191} of step t+1     (freed: last read in phase 1 of step t-1)
+//   phase 1: A rows {64..127, 192..255} of step t+1   (freed: last read in phase 3 of step t-1)
+//   phase 2: B cols/rows 0..127 of step t+2            (freed: last read in phase 0 of step t)
+//   phase 3: B cols/rows 128..255 of step t+2
+// Every region is read >= 4 phases after its DMA was issued and >= 1 phase after its last
+// reader's lgkmcnt-wait + barrier, so a per-phase vmcnt(6) (the DMAs of the last three phases
+// may stay in flight) before the phase's barrier orders every read after the data landed.
+// Steps past the end load zeros (range-checked offsets), so the loop needs no tail case.
+//
+// MN operands use 64-column blocks, [4 blocks][64 k][128 B], phys 16-B chunk =
+// chunk ^ 2*h(k), h(k) = bit1(k) | bit3(k) << 1: conflict-free for ds_read_b64_tr_b16 (each
+// 32-lane group reads 8 k rows x 32 B = all 64 banks once) and full 128-B lines per DMA row.
+// KC operands keep [256 rows][128 B] with chunk ^ (row & 7).
+
+CC_DEV int pp_h(int k) { return ((k >> 1) & 1) | ((k >> 2) & 2); }
+
+// Per-lane source offset (bytes, step k0 = 0) of DMA ci (0..31) of a 256 x 64 operand tile, or
+// OOB for rows / columns past the matrix edge.
+template <bool KC>
+CC_DEV uint32_t pp_dma_off(int ci, int lim, int64_t ld, int lane) {
+  if constexpr (KC) {
+    const int row = ci * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (lane >> 3);
+    return row < lim ? (uint32_t)((int64_t)row * ld * 2 + c * 16) : OOB;
+  } else {
+    const int k = 8 * (ci & 7) + (lane >> 3);
+    const int c = (lane & 7) ^ (2 * pp_h(k));
+    const int col = (ci >> 3) * 64 + 8 * c;
+    return col < lim ? (uint32_t)(((int64_t)k * ld + col) * 2) : OOB;
+  }
+}
+// Per-lane k (elements, within the step) of this lane's 16 B in every DMA of the operand (the
+// K-tail mask): the same for all of a wave's DMAs by construction of the ci schedule.
+template <bool KC>
+CC_DEV int pp_dma_k(int wave, int lane) {
+  return KC ? 8 * ((lane & 7) ^ (lane >> 3)) : 8 * wave + (lane >> 3);
+}
+
+// ci of DMA q (0/1) of phase p for this wave (see the schedule above)
+CC_DEV int pp_ci(int p, int q, int wave) {
+  switch (p) {
+    case 0: return (q ? 16 : 0) + wave;
+    case 1: return (q ? 24 : 8) + wave;
+    case 2: return (q ? 8 : 0) + wave;
+    default: return (q ? 24 : 16) + wave;
+  }
+}
+
+// 16x16x32 operand fragment for the 16 rows/cols starting at r0 (multiple of 16), slice kk.
+// KC: lane l holds X[r0 + (l&15)][32kk + 8(l>>4) .. +7]; kc_off[kk] = the lane part.
+CC_DEV bf16x8 pp_frag_kc(const char* tile, int r0, int off) {
+  return *(const bf16x8*)(tile + r0 * 128 + off);
+}
+// MN: two transposed 8-byte reads (k rows 32kk + 8g + qq and +4); mn_off[m] = the lane part for
+// column groups with (r0 >> 4) & 3 == m.
+CC_DEV bf16x8 pp_frag_mn(const char* tile, int r0, int kk, int off) {
+  const char* p = tile + (r0 >> 6) * 8192 + kk * 32 * 128 + off;
+  bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)p);
+  bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(p + 4 * 128));
+  return bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+}
+
+template <bool AKC, bool BKC, int EPI>
+__global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
+  using WG = WaveGeom<256>;
+  static_assert(WG::TM == 8 && WG::TN == 4, "ping-pong geometry");
+  constexpr int TILE = 256 * 128;  // one operand's K-step image
+  constexpr int BUF = 2 * TILE;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  int tm, tn;
+  tile_of_block(blockIdx.x, args.nbm, args.nbn, tm, tn);
+  const int m0 = tm * BM, n0 = tn * 256;
+  const int M = args.M, N = args.N, K = args.K;
+
+  __amdgpu_buffer_rsrc_t ra, rb;
+  {
+    const char* a = (const char*)args.A;
+    const char* b = (const char*)args.B;
+    if constexpr (AKC) {
+      a += (int64_t)m0 * args.lda * 2;
+      ra = make_rsrc(a, (uint64_t)(M - m0) * args.lda * 2);
+    } else {
+      a += (int64_t)m0 * 2;
+      ra = make_rsrc(a, ((uint64_t)(K - 1) * args.lda + (M - m0)) * 2);
+    }
+    if constexpr (BKC) {
+      b += (int64_t)n0 * args.ldb * 2;
+      rb = make_rsrc(b, (uint64_t)(N - n0) * args.ldb * 2);
+    } else {
+      b += (int64_t)n0 * 2;
+      rb = make_rsrc(b, ((uint64_t)(K - 1) * args.ldb + (N - n0)) * 2);
+    }
+  }
+
+  // DMA offsets: vo[p][q] for the 4 phases x 2 DMAs (p 0,1: A; p 2,3: B)
+  uint32_t vo[4][2];
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      vo[p][q] = p < 2 ? pp_dma_off<AKC>(pp_ci(p, q, wave), M - m0, args.lda, lane)
+                       : pp_dma_off<BKC>(pp_ci(p, q, wave), N - n0, args.ldb, lane);
+  const int kA = pp_dma_k<AKC>(wave, lane), kB = pp_dma_k<BKC>(wave, lane);
+  const int nk = (K + 63) / 64;
+
+  // issue phase p's DMAs for step T (target buffer T & 1)
+  auto issue = [&](int p, int T) {
+    const bool isA = p < 2;
+    const int k0 = T * 64;
+    char* dst = smem + (T & 1) * BUF + (isA ? 0 : TILE);
+    const int64_t ld = isA ? args.lda : args.ldb;
+    const bool kc = isA ? AKC : BKC;
+    const uint32_t kadd = (uint32_t)(kc ? (int64_t)k0 * 2 : (int64_t)k0 * ld * 2);
+    const bool kin = k0 + (isA ? kA : kB) < K;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const uint32_t v = vo[p][q];
+      const uint32_t off = (kin && v != OOB) ? v + kadd : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? ra : rb, (lds_void*)(dst + pp_ci(p, q, wave) * 1024), 16,
+                                               (int)off, 0, 0, 0);
+    }
+  };
+
+  // fragment lane offsets
+  int kc_off[2], mn_off[4];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) kc_off[kk] = (lane & 15) * 128 + ((((lane >> 4) + 4 * kk) ^ (lane & 7)) << 4);
+  {
+    const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+    const int kq = 8 * g + qq;
+    const int h = pp_h(kq);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) mn_off[m] = kq * 128 + (((2 * (m ^ h)) | (pp >> 1)) << 4) + 8 * (pp & 1);
+  }
+
+  f32x4 acc[WG::TM][WG::TN];
+#pragma unroll
+  for (int i = 0; i < WG::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < WG::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: the DMAs steady state would have issued in steps -2 and -1
+  issue(2, 0);
+  issue(3, 0);
+  issue(0, 0);
+  issue(1, 0);
+  issue(2, 1);
+  issue(3, 1);
+  wait_vmcnt<6>();
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs half a phase behind
+
+  bf16x8 bfr[WG::TN][2];
+  for (int t = 0; t < nk; ++t) {
+    const char* la = smem + (t & 1) * BUF;
+    const char* lb = la + TILE;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (p == 0) {
+#pragma unroll
+        for (int j = 0; j < WG::TN; ++j) {
+          const int c0 = wc * WG::WTN + 16 * j;
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+            bfr[j][kk] = BKC ? pp_frag_kc(lb, c0, kc_off[kk]) : pp_frag_mn(lb, c0, kk, mn_off[(c0 >> 4) & 3]);
+        }
+      }
+      bf16x8 afr[2][2];
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int r0 = wr * WG::WTM + 16 * (2 * p + ii);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          afr[ii][kk] = AKC ? pp_frag_kc(la, r0, kc_off[kk]) : pp_frag_mn(la, r0, kk, mn_off[(r0 >> 4) & 3]);
+      }
+      issue(p, p < 2 ? t + 1 : t + 2);
+      wait_vmcnt<6>();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int j = 0; j < WG::TN; ++j)
+            acc[2 * p + ii][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii][kk], acc[2 * p + ii][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();
+  wait_vmcnt<0>();
+
+  gemm_epilogue<CC_BF16, EPI, 256>(args, acc, tm, m0, n0, wr, wc, lane, blockIdx.x * 8 + wave);
+}

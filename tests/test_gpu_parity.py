@@ -71,6 +71,68 @@ def test_gemm_layouts(gpu, dtype, shape, layouts):
     assert rel(C, ref) < 1e-5
 
 
+@pytest.fixture
+def pp_mask():
+    """Selects which layouts run the ping-pong main loop; restored afterwards."""
+    from crosscoder_amd import _lib
+    lib = _lib.load()
+    yield lib.cc_debug_set_pp_mask
+    lib.cc_debug_set_pp_mask(_lib.DEFAULT_PP_MASK)
+
+
+@pytest.mark.parametrize("shape", [(256, 256, 64), (296, 520, 72), (96, 200, 80), (512, 768, 1000),
+                                   (1024, 4608, 4096), (4096, 2304, 640)])
+@pytest.mark.parametrize("layouts", [(0, 0), (0, 1), (1, 1)])
+def test_gemm_pingpong_matches_two_stage(gpu, pp_mask, shape, layouts):
+    """Both bf16 main loops accumulate each output in the same k order, so they agree bitwise;
+    and both match fp64 (ragged M/N/K tails included)."""
+    M, N, K = shape
+    al, bl = layouts
+    g = torch.Generator().manual_seed(M + 3 * N + 7 * K)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    Bm = torch.randn(K, N, generator=g).to(torch.bfloat16)
+    A_st = (A.contiguous() if al == 0 else A.t().contiguous()).to(gpu)
+    B_st = (Bm.t().contiguous() if bl == 0 else Bm.contiguous()).to(gpu)
+    outs = []
+    for mask in (0, 7):
+        pp_mask(mask)
+        outs.append(ops.gemm_f32out(A_st, al, B_st, bl, M, N, K))
+    torch.cuda.synchronize()
+    ref = A.double() @ Bm.double()
+    assert rel(outs[1], ref) < 1e-5
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("mask", [0, 7])
+def test_step_gemm_paths(gpu, pp_mask, mask):
+    """One fused fwd+bwd at a mid size through each main loop vs the fp32 oracle."""
+    pp_mask(mask)
+    n, d, h, B = 2, 576, 2048, 1024
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16", seed=11,
+               device=str(gpu))
+    cc = ca.CrossCoder(cfg, n_models=n)
+    g = torch.Generator().manual_seed(5)
+    buf = torch.randn(B, n, d, generator=g) * 3
+    factor = torch.tensor([0.7, 1.3]).to(torch.bfloat16)
+    ws = cc._workspace(B)
+    a = cc.arena()
+    G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+    engine.forward(ws, a, buf.to(gpu), factor.to(gpu))
+    engine.backward(ws, a, G, l1_coeff=2.0)
+    torch.cuda.synchronize()
+    P32 = {k: v.detach().float().cpu().clone().requires_grad_(True) for k, v in cc.state_dict().items()}
+    x32 = ws.x.cpu().float().view(B, n, d)
+    lo = O.get_losses(x32, P32, torch.float32)
+    (lo["l2_loss"] + 2.0 * lo["l1_loss"]).backward()
+    s = ws.scalars[:6].cpu()
+    assert math.isclose(s[0].item(), lo["l2_loss"].item(), rel_tol=1e-2)
+    Gv = G.views()
+    bounds = {"W_enc": 1e-1, "W_dec": 1e-2, "b_enc": 1e-2, "b_dec": 1e-2}
+    for k in O.PARAM_ORDER:
+        e = rel(Gv[k].cpu(), P32[k].grad)
+        assert e <= bounds[k], (k, e)
+
+
 # ----------------------------------------------------------------------------- forward
 @pytest.mark.parametrize("name", STEP_FIXTURES)
 def test_forward_parity(gpu, name):

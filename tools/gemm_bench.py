@@ -24,7 +24,11 @@ def load(path):
 
 
 def main():
-    libs = [(p, load(p)) for p in sys.argv[1:]]
+    # each argument: path/to/lib.so[@pp_mask]  (the mask selects the ping-pong loop per layout)
+    libs = []
+    for arg in sys.argv[1:]:
+        path, _, mask = arg.partition("@")
+        libs.append((os.path.basename(path) + (f"@{mask}" if mask else ""), load(path), int(mask) if mask else None))
     dev = torch.device("cuda:0")
     bf = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
@@ -54,13 +58,18 @@ def main():
                                                st),
             "G4_wgrad_dec": lambda: L.cc_wgrad_dec(P(acts), P(g_recon), P(W2), P(norms), P(colsum), 1e-4, P(gW),
                                                    P(parts), B, h, n, d, 1, st),
+            "G4_no_l1term": lambda: L.cc_wgrad_dec(P(acts), P(g_recon), P(W2), P(norms), P(colsum), 0.0, P(gW),
+                                                   P(parts), B, h, n, d, 1, st),
             "G5_wgrad_enc": lambda: L.cc_wgrad_enc(P(g_pre), P(x), P(gW), P(parts), B, h, K, 1, st),
+            "G5_on_G4_data": lambda: L.cc_wgrad_enc(P(acts), P(g_recon), P(gW), P(parts), B, h, K, 1, st),
         }
 
     flop = 2.0 * B * K * h
     res = {}
     for rnd in range(5):
-        for path, L in libs:
+        for path, L, mask in libs:
+            if mask is not None:
+                L.cc_debug_set_pp_mask(mask)
             for name, fn in calls(L).items():
                 for _ in range(2):
                     assert fn() == 0
@@ -70,7 +79,7 @@ def main():
                     fn()
                 e.record()
                 torch.cuda.synchronize()
-                res.setdefault((os.path.basename(path), name), []).append(s.elapsed_time(e) / 10)
+                res.setdefault((path, name), []).append(s.elapsed_time(e) / 10)
     for (p, name), ts in sorted(res.items(), key=lambda kv: (kv[0][1], kv[0][0])):
         ts.sort()
         med = ts[len(ts) // 2]
