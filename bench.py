@@ -35,23 +35,29 @@ PEAK_BF16_TFLOPS = 256 * 2.4e9 * 4096 / 1e12  # 256 CU x 2.4 GHz x 4096 bf16 FLO
 
 
 class EventTimer:
-    """HIP events on torch's current stream (the stream every launch uses) around named spans."""
+    """HIP events on torch's current stream (the stream every launch uses) around named spans.
+
+    `only` restricts recording to one span name: inside the timed region only the roofline kernel
+    is bracketed (each timing event costs the stream a few microseconds); the per-kernel breakdown
+    comes from an attribution pass of its own."""
 
     def __init__(self):
         self.rec = {}
         self.enabled = False
+        self.only = None
 
     class _Span:
         def __init__(self, t, name):
             self.t, self.name = t, name
+            self.on = t.enabled and (t.only is None or t.only == name)
 
         def __enter__(self):
-            if self.t.enabled:
+            if self.on:
                 self.s = torch.cuda.Event(enable_timing=True)
                 self.s.record()
 
         def __exit__(self, *a):
-            if self.t.enabled:
+            if self.on:
                 e = torch.cuda.Event(enable_timing=True)
                 e.record()
                 self.t.rec.setdefault(self.name, []).append((self.s, e))
@@ -130,7 +136,18 @@ def main():
     engine.TIMER = timer
     for _ in range(args.warmup):
         tr.step()
+    # attribution pass (not timed): every kernel bracketed by events
+    attrib = EventTimer()
+    engine.TIMER = attrib
+    attrib.enabled = True
+    for _ in range(max(3, min(args.steps, 10))):
+        tr.step()
     torch.cuda.synchronize()
+    kern = attrib.averages_ms()
+    gemms = {k: v for k, v in kern.items() if k.startswith("G")}
+    dom = max(gemms, key=gemms.get)
+    engine.TIMER = timer
+    timer.only = dom  # the roofline kernel, measured live inside the timed region
     if world > 1:
         dist.barrier()
     timer.enabled = True
@@ -150,11 +167,9 @@ def main():
     ms = elapsed / args.steps * 1e3
     acts_equiv = B * (h_total / H_LOCAL)
     value = acts_equiv / (elapsed / args.steps)
-    kern = timer.averages_ms()
+    dom_ms = timer.averages_ms()[dom]
     gemm_flop = 2.0 * B * N_MODELS * D_MODEL * H_LOCAL  # per GEMM launch (per rank)
-    gemms = {k: v for k, v in kern.items() if k.startswith("G")}
-    dom = max(gemms, key=gemms.get)
-    achieved = gemm_flop / (gemms[dom] * 1e-3) / 1e12
+    achieved = gemm_flop / (dom_ms * 1e-3) / 1e12
     step_flop = 5 * gemm_flop
     result = {
         "metric": "activations/sec per train step (fwd+bwd+Adam), 2x2304->16384; % bf16 MFMA peak",
@@ -175,7 +190,7 @@ def main():
                    "parallelism": f"latent{world}"},
         "step_mfma_frac": round(step_flop / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
         "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items())},
-        "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 1), "peak": round(PEAK_BF16_TFLOPS, 1),
+        "roofline": {"bound": "mfma", "kernel": dom, "kernel_ms": round(dom_ms, 4), "achieved": round(achieved, 1), "peak": round(PEAK_BF16_TFLOPS, 1),
                      "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None},
         "last_loss": {k: round(v, 6) for k, v in last.items()},
     }

@@ -632,14 +632,15 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 #define CC_PP_MASK 5
 #endif
 static int g_pp_mask = CC_PP_MASK;  // cc_debug_set_pp_mask: in-process A/B of the two loops
-static bool use_pp(bool akc, bool bkc, int dtype) {
-  if (dtype != CC_BF16 || (!akc && bkc)) return false;
+static bool use_pp(int64_t N, bool akc, bool bkc, int dtype) {
+  // (N % 8: the ping-pong epilogue moves whole 16-byte column chunks through LDS)
+  if (dtype != CC_BF16 || (!akc && bkc) || N % 8) return false;
   const int bit = akc && bkc ? 0 : (akc ? 1 : 2);
   return (g_pp_mask >> bit) & 1;
 }
 extern "C" void cc_debug_set_pp_mask(int mask) { g_pp_mask = mask; }
 static int pick_bn(int64_t N, bool akc, bool bkc, int dtype) {
-  if (use_pp(akc, bkc, dtype)) return 256;
+  if (use_pp(N, akc, bkc, dtype)) return 256;
   return (!bkc && dtype == CC_BF16 && N % 288 == 0) ? 288 : 256;
 }
 static int64_t n_blocks(int64_t M, int64_t N, int bn) { return ((M + BM - 1) / BM) * ((N + bn - 1) / bn); }
@@ -674,7 +675,7 @@ static int launch_pp(GemmArgs a, hipStream_t st) {
 template <int EPI, bool AKC, bool BKC>
 static int launch_dt(int dtype, GemmArgs a, hipStream_t st) {
   if constexpr (!(!AKC && BKC)) {
-    if (use_pp(AKC, BKC, dtype)) return launch_pp<AKC, BKC, EPI>(a, st);
+    if (use_pp(a.N, AKC, BKC, dtype)) return launch_pp<AKC, BKC, EPI>(a, st);
   }
   if constexpr (!BKC) {
     if (pick_bn(a.N, AKC, BKC, dtype) == 288) return launch<CC_BF16, AKC, BKC, EPI, 288>(a, st);

@@ -3,12 +3,16 @@
 // Accumulator map (transposed C fragments): acc[i][j][e] = C[m0 + r0 + 16i][n0 + c0 + 16j + e]
 // with r0 = wr*WTM + (lane & 15), c0 = wc*WTN + 4*(lane >> 4).
 //
-// Every element-wise load and store goes through a buffer descriptor anchored at the tile origin
-// (m0, n0): a row or column past the matrix edge gets an out-of-range offset, so its load returns
-// 0 and its store is dropped.  There is no branch per fragment -- a branch around each load makes
-// the compiler wait for that load by itself (one memory latency per fragment), which is what made
-// the W_dec term of dW_dec cost a quarter of that GEMM.  N % 4 == 0 (host check): a lane's 4
-// columns are all in range or all out.
+// The element-wise work of each epilogue is written once (epilogue_core) against an IO policy
+// that supplies the tile-shaped input operand of the epilogue (the activation mask of d_acts,
+// W_dec for dW_dec) and takes the dtype output, fragment by fragment:
+//   RegIO -- straight from/to HBM through buffer descriptors anchored at the tile origin: a row
+//            or column past the matrix edge gets an out-of-range offset (load 0, store dropped),
+//            so there is no branch per fragment (a branch around each load makes the compiler
+//            wait for that load by itself: one memory latency per fragment).
+//   LdsIO  -- (gemm_pp.h) a swizzled LDS image of the tile, staged in and out with full-line
+//            transfers.
+// N % 4 == 0 (host check): a lane's 4 columns are all in range or all out.
 
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
@@ -27,73 +31,73 @@ template <int DT> CC_DEV typename V4<DT>::T bld4(__amdgpu_buffer_rsrc_t r, uint3
   if constexpr (DT == CC_BF16) return __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
   else return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
 }
-template <int DT> CC_DEV void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, const float v[4]) {
+template <int DT> CC_DEV typename V4<DT>::T pack4(const float v[4]) {
   if constexpr (DT == CC_BF16) {
     bf16x4 p;
 #pragma unroll
     for (int e = 0; e < 4; ++e) p[e] = (short)f2bf(v[e]);
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, p), r, (int)off, 0, 0);
+    return p;
   } else {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{v[0], v[1], v[2], v[3]}), r, (int)off,
-                                           0, 0);
+    return f32x4{v[0], v[1], v[2], v[3]};
   }
+}
+template <int DT> CC_DEV void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, const float v[4]) {
+  if constexpr (DT == CC_BF16)
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pack4<DT>(v)), r, (int)off, 0, 0);
+  else
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack4<DT>(v)), r, (int)off, 0, 0);
 }
 CC_DEV float bldf(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
 
-template <int DT, int EPI, int BNT>
-CC_DEV void gemm_epilogue(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN], int tm,
-                          int m0, int n0, int wr, int wc, int lane, int wave_slot) {
+// Fragment geometry of one wave's sub-tile: range flags and tile-relative element offsets.
+template <int BNT>
+struct FragGeom {
+  using WG = WaveGeom<BNT>;
+  int r0, c0, ldo;
+  bool rv[WG::TM], cv[WG::TN];
+  CC_DEV FragGeom(const GemmArgs& args, int m0, int n0, int wr, int wc, int lane) {
+    r0 = wr * WG::WTM + (lane & 15);
+    c0 = wc * WG::WTN + 4 * (lane >> 4);
+    ldo = (int)args.ldo;
+#pragma unroll
+    for (int i = 0; i < WG::TM; ++i) rv[i] = m0 + r0 + 16 * i < args.M;
+#pragma unroll
+    for (int j = 0; j < WG::TN; ++j) cv[j] = n0 + c0 + 16 * j < args.N;
+  }
+  CC_DEV bool ok(int i, int j) const { return rv[i] && cv[j]; }
+  // byte offset of fragment (i, j) in a tile-anchored [.][ldo] matrix of element size es, or OOB
+  CC_DEV uint32_t boff(int i, int j, int es) const {
+    return ok(i, j) ? (uint32_t)(((r0 + 16 * i) * ldo + c0 + 16 * j) * es) : OOB;
+  }
+};
+
+// HBM IO policy: input = mask_src (DACTS) / w_src (WGDEC), output = out, both indexed like out.
+template <int DT, int BNT>
+struct RegIO {
+  const FragGeom<BNT>& fg;
+  __amdgpu_buffer_rsrc_t rin, rout;
+  static constexpr int ES = DT == CC_BF16 ? 2 : 4;
+  CC_DEV RegIO(const GemmArgs& args, const FragGeom<BNT>& g, const void* in, int m0, int n0) : fg(g) {
+    rout = tile_rsrc(args.out, args.ldo, m0, n0, args.M, args.N, ES);
+    rin = tile_rsrc(in ? in : args.out, args.ldo, m0, n0, args.M, args.N, ES);
+  }
+  CC_DEV typename V4<DT>::T in4(int i, int j) const { return bld4<DT>(rin, fg.boff(i, j, ES)); }
+  CC_DEV void out4(int i, int j, const float v[4]) const { bst4<DT>(rout, fg.boff(i, j, ES), v); }
+};
+
+// The element-wise part of EPI_ENC / EPI_DACTS / EPI_WGDEC / EPI_WGENC over one wave's fragments.
+template <int DT, int EPI, int BNT, class IO>
+CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN],
+                          const FragGeom<BNT>& fg, const IO& io, int tm, int m0, int n0, int wr, int lane,
+                          int wave_slot) {
   using E = Elem<DT>;
   using WG = WaveGeom<BNT>;
   constexpr int ES = DT == CC_BF16 ? 2 : 4;
   const int M = args.M, N = args.N;
-  const int r0 = wr * WG::WTM + (lane & 15);
-  const int c0 = wc * WG::WTN + 4 * (lane >> 4);
-  bool rv[WG::TM], cv[WG::TN];
-#pragma unroll
-  for (int i = 0; i < WG::TM; ++i) rv[i] = m0 + r0 + 16 * i < M;
-#pragma unroll
-  for (int j = 0; j < WG::TN; ++j) cv[j] = n0 + c0 + 16 * j < N;
-  const int ldo = (int)args.ldo;
-  // element offset of fragment (i, j) from the tile origin, or -1 (-> OOB) when out of range
-  auto eoff = [&](int i, int j) -> int { return (rv[i] && cv[j]) ? (r0 + 16 * i) * ldo + c0 + 16 * j : -1; };
-  auto boff = [&](int e, int es) -> uint32_t { return e < 0 ? OOB : (uint32_t)(e * es); };
-
-  if constexpr (EPI == EPI_F32 || EPI == EPI_DEC) {
-    const __amdgpu_buffer_rsrc_t ro32 = tile_rsrc(EPI == EPI_F32 ? args.out : (const void*)args.out_f32, args.ldo,
-                                                  m0, n0, M, N, 4);
-    const __amdgpu_buffer_rsrc_t rot = tile_rsrc(args.out, args.ldo, m0, n0, M, N, ES);
-    const bool has_bias = EPI == EPI_DEC && args.bias;
-    const __amdgpu_buffer_rsrc_t rbias = vec_rsrc(has_bias ? args.bias : args.A, n0, N, ES);
-#pragma unroll
-    for (int j = 0; j < WG::TN; ++j) {
-      float bc[4] = {0.f, 0.f, 0.f, 0.f};
-      if (has_bias) {
-        const auto b = bld4<DT>(rbias, (uint32_t)((c0 + 16 * j) * ES));
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bc[e] = V4<DT>::get(b, e);
-      }
-#pragma unroll
-      for (int i = 0; i < WG::TM; ++i) {
-        const int eo = eoff(i, j);
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bc[e];
-        if constexpr (EPI == EPI_F32) {
-          bst4<CC_F32>(ro32, boff(eo, 4), v);
-        } else {
-          if (args.out_f32) bst4<CC_F32>(ro32, boff(eo, 4), v);
-          if (args.out) bst4<DT>(rot, boff(eo, ES), v);
-        }
-      }
-    }
-  } else if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
+  if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
     constexpr int JB = EPB<DT, BNT>::JB_M;
-    const __amdgpu_buffer_rsrc_t rot = tile_rsrc(args.out, args.ldo, m0, n0, M, N, ES);
-    const __amdgpu_buffer_rsrc_t rmask =
-        tile_rsrc(EPI == EPI_DACTS ? args.mask_src : args.out, args.ldo, m0, n0, M, N, ES);
     const bool has_bias = EPI == EPI_ENC && args.bias;
     const __amdgpu_buffer_rsrc_t rbias = vec_rsrc(has_bias ? args.bias : args.A, n0, N, ES);
     const __amdgpu_buffer_rsrc_t rtn = vec_rsrc(args.tn ? (const void*)args.tn : args.A, n0, N, 4);
@@ -106,11 +110,11 @@ CC_DEV void gemm_epilogue(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
 #pragma unroll
           for (int jj = 0; jj < JB; ++jj)
 #pragma unroll
-            for (int i = 0; i < WG::TM; ++i) mraw[i][jj] = bld4<DT>(rmask, boff(eoff(i, j + jj), ES));
+            for (int i = 0; i < WG::TM; ++i) mraw[i][jj] = io.in4(i, j + jj);
         }
       }
       float add[4] = {0.f, 0.f, 0.f, 0.f}, tnc[4] = {0.f, 0.f, 0.f, 0.f}, csum[4] = {0.f, 0.f, 0.f, 0.f};
-      const uint32_t cvo = (uint32_t)(c0 + 16 * j);
+      const uint32_t cvo = (uint32_t)(fg.c0 + 16 * j);
       if constexpr (EPI == EPI_ENC) {
         if (has_bias) {
           const auto b = bld4<DT>(rbias, cvo * ES);
@@ -129,8 +133,7 @@ CC_DEV void gemm_epilogue(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
       }
 #pragma unroll
       for (int i = 0; i < WG::TM; ++i) {
-        const int eo = eoff(i, j);
-        const bool ok = eo >= 0;
+        const bool ok = fg.ok(i, j);
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -147,7 +150,7 @@ CC_DEV void gemm_epilogue(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
             s_l0 += v[e] > 0.f ? 1.f : 0.f;
           }
         }
-        bst4<DT>(rot, boff(eo, ES), v);
+        io.out4(i, j, v);
       }
       if (args.col_part) {  // reduce over the 16 lanes (rows) that share these 4 columns
 #pragma unroll
@@ -159,8 +162,8 @@ CC_DEV void gemm_epilogue(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
           s += __shfl_xor(s, 8, 64);
           csum[e] = s;
         }
-        if ((lane & 15) == 0 && cv[j])
-          st4<CC_F32>(args.col_part, (int64_t)(tm * WG::WARPS_M + wr) * N + n0 + c0 + 16 * j, csum);
+        if ((lane & 15) == 0 && fg.cv[j])
+          st4<CC_F32>(args.col_part, (int64_t)(tm * WG::WARPS_M + wr) * N + n0 + fg.c0 + 16 * j, csum);
       }
     }
     if constexpr (EPI == EPI_ENC) {
@@ -175,22 +178,20 @@ CC_DEV void gemm_epilogue(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
     }
   } else if constexpr (EPI == EPI_WGDEC || EPI == EPI_WGENC) {
     constexpr int JB = EPB<DT, BNT>::JB_W;
-    const __amdgpu_buffer_rsrc_t rot = tile_rsrc(args.out, args.ldo, m0, n0, M, N, ES);
     const bool l1term = EPI == EPI_WGDEC && args.scale0 != 0.f;
     float sq = 0.f;
     // per-row factor scale * sum_b acts[b, row]; per (row, model) the inverse decoder norm
     float cs[WG::TM];
     typename V4<DT>::T wraw[EPI == EPI_WGDEC ? WG::TM : 1][JB];
     float cw[EPI == EPI_WGDEC ? WG::TM : 1][JB];
-    __amdgpu_buffer_rsrc_t rw = rot, rnorm = rot;
+    __amdgpu_buffer_rsrc_t rnorm = make_rsrc(args.A, 0);
     if constexpr (EPI == EPI_WGDEC) {
       if (l1term) {
-        rw = tile_rsrc(args.w_src, args.ldo, m0, n0, M, N, ES);
         rnorm = vec_rsrc(args.norms, m0 * args.n_models, (int64_t)M * args.n_models, 4);
         const __amdgpu_buffer_rsrc_t rcol = vec_rsrc(args.colsum, m0, M, 4);
 #pragma unroll
         for (int i = 0; i < WG::TM; ++i)
-          cs[i] = args.scale0 * bldf(rcol, rv[i] ? (uint32_t)((r0 + 16 * i) * 4) : OOB);
+          cs[i] = args.scale0 * bldf(rcol, fg.rv[i] ? (uint32_t)((fg.r0 + 16 * i) * 4) : OOB);
       }
     }
 #pragma unroll
@@ -199,19 +200,19 @@ CC_DEV void gemm_epilogue(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
         if (l1term && j % JB == 0) {
 #pragma unroll
           for (int jj = 0; jj < JB; ++jj) {
-            const int model = (n0 + c0 + 16 * (j + jj)) / args.d_model;
+            const int model = (n0 + fg.c0 + 16 * (j + jj)) / args.d_model;
 #pragma unroll
             for (int i = 0; i < WG::TM; ++i) {
-              const int eo = eoff(i, j + jj);
-              wraw[i][jj] = bld4<DT>(rw, boff(eo, ES));
-              cw[i][jj] = cs[i] * bldf(rnorm, eo < 0 ? OOB : (uint32_t)(((r0 + 16 * i) * args.n_models + model) * 4));
+              wraw[i][jj] = io.in4(i, j + jj);
+              cw[i][jj] = cs[i] * bldf(rnorm, fg.ok(i, j + jj)
+                                                  ? (uint32_t)(((fg.r0 + 16 * i) * args.n_models + model) * 4)
+                                                  : OOB);  // inverse norms
             }
           }
         }
       }
 #pragma unroll
       for (int i = 0; i < WG::TM; ++i) {
-        const int eo = eoff(i, j);
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e];
@@ -224,14 +225,54 @@ CC_DEV void gemm_epilogue(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           v[e] = E::round(v[e]);
-          sq += v[e] * v[e];  // out-of-range fragments are exactly 0 (zero-filled operands, OOB loads)
+          sq += v[e] * v[e];  // out-of-range fragments are exactly 0 (zero-filled operands and inputs)
         }
-        bst4<DT>(rot, boff(eo, ES), v);
+        io.out4(i, j, v);
       }
     }
     if (args.wave_part0) {
       float t = wave_sum(sq);
       if (lane == 0) args.wave_part0[wave_slot] = t;
     }
+  }
+}
+
+template <int DT, int EPI, int BNT>
+CC_DEV void gemm_epilogue(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN], int tm,
+                          int m0, int n0, int wr, int wc, int lane, int wave_slot) {
+  using WG = WaveGeom<BNT>;
+  constexpr int ES = DT == CC_BF16 ? 2 : 4;
+  const FragGeom<BNT> fg(args, m0, n0, wr, wc, lane);
+  if constexpr (EPI == EPI_F32 || EPI == EPI_DEC) {
+    const __amdgpu_buffer_rsrc_t ro32 = tile_rsrc(EPI == EPI_F32 ? args.out : (const void*)args.out_f32, args.ldo,
+                                                  m0, n0, args.M, args.N, 4);
+    const __amdgpu_buffer_rsrc_t rot = tile_rsrc(args.out, args.ldo, m0, n0, args.M, args.N, ES);
+    const bool has_bias = EPI == EPI_DEC && args.bias;
+    const __amdgpu_buffer_rsrc_t rbias = vec_rsrc(has_bias ? args.bias : args.A, n0, args.N, ES);
+#pragma unroll
+    for (int j = 0; j < WG::TN; ++j) {
+      float bc[4] = {0.f, 0.f, 0.f, 0.f};
+      if (has_bias) {
+        const auto b = bld4<DT>(rbias, (uint32_t)((fg.c0 + 16 * j) * ES));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bc[e] = V4<DT>::get(b, e);
+      }
+#pragma unroll
+      for (int i = 0; i < WG::TM; ++i) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bc[e];
+        if constexpr (EPI == EPI_F32) {
+          bst4<CC_F32>(ro32, fg.boff(i, j, 4), v);
+        } else {
+          if (args.out_f32) bst4<CC_F32>(ro32, fg.boff(i, j, 4), v);
+          if (args.out) bst4<DT>(rot, fg.boff(i, j, ES), v);
+        }
+      }
+    }
+  } else {
+    const void* in = EPI == EPI_DACTS ? args.mask_src : (EPI == EPI_WGDEC ? args.w_src : nullptr);
+    const RegIO<DT, BNT> io(args, fg, in, m0, n0);
+    epilogue_core<DT, EPI, BNT>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot);
   }
 }

@@ -76,6 +76,64 @@ CC_DEV bf16x8 pp_frag_mn(const char* tile, int r0, int kk, int off) {
   return bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
 }
 
+// ---- LDS-staged epilogue (bf16 output tiles, N % 8 == 0) ----
+// Tile image [256 rows][512 B] (all 128 KB of LDS once the main loop has drained), phys 16-B
+// chunk = chunk ^ (row & 15): a fragment access (per 32-lane group 16 rows x one chunk) hits 16
+// distinct bank groups.  The image moves between HBM and LDS in whole 512-B rows (1 KB = 2 rows
+// per wave instruction, 16 B per lane), so every HBM line of the epilogue's input (activation
+// mask / W_dec) and output is transferred once and whole -- the fragment-shaped 8-byte accesses
+// of the register path fetch up to 4x the bytes (PMC FETCH_SIZE).
+struct LdsIO {
+  char* smem;
+  int off[4];  // lane byte offset of fragment (0, j); fragment i adds 16 rows
+  CC_DEV LdsIO(char* s, int wr, int wc, int lane) : smem(s) {
+    const int r = wr * 128 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = wc * 64 + 4 * (lane >> 4) + 16 * j;
+      off[j] = r * 512 + (((col >> 3) ^ (lane & 15)) << 4) + (col & 4) * 2;
+    }
+  }
+  CC_DEV bf16x4 in4(int i, int j) const { return *(const bf16x4*)(smem + off[j] + i * 16 * 512); }
+  CC_DEV void out4(int i, int j, const float v[4]) const {
+    *(bf16x4*)(smem + off[j] + i * 16 * 512) = pack4<CC_BF16>(v);
+  }
+};
+
+template <int EPI>
+CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char* smem, int tm, int m0, int n0,
+                            int wr, int wc, int lane, int wave, int wave_slot) {
+  const FragGeom<256> fg(args, m0, n0, wr, wc, lane);
+  const int rows = args.M - m0, cols = args.N - n0, ldo = (int)args.ldo;
+  // source/destination offset of this lane's 16 B of 1-KB piece ci (tile rows 2ci, 2ci+1)
+  auto xoff = [&](int ci) -> uint32_t {
+    const int row = 2 * ci + (lane >> 5);
+    const int c = (lane & 31) ^ (row & 15);
+    return (row < rows && 8 * c < cols) ? (uint32_t)((row * ldo + 8 * c) * 2) : OOB;
+  };
+  const void* in = EPI == EPI_DACTS ? args.mask_src : (EPI == EPI_WGDEC && args.scale0 != 0.f ? args.w_src : nullptr);
+  if (in) {
+    const __amdgpu_buffer_rsrc_t rin = tile_rsrc(in, args.ldo, m0, n0, args.M, args.N, 2);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int ci = q * 8 + wave;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_void*)(smem + ci * 1024), 16, (int)xoff(ci), 0, 0, 0);
+    }
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+  }
+  const LdsIO io(smem, wr, wc, lane);
+  epilogue_core<CC_BF16, EPI, 256>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot);
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rout = tile_rsrc(args.out, args.ldo, m0, n0, args.M, args.N, 2);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int ci = q * 8 + wave;
+    const bf16x8 v = *(const bf16x8*)(smem + ci * 1024 + lane * 16);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, (int)xoff(ci), 0, 0);
+  }
+}
+
 template <bool AKC, bool BKC, int EPI>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
   using WG = WaveGeom<256>;
@@ -214,5 +272,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
   if (wr == 0) __builtin_amdgcn_s_barrier();
   wait_vmcnt<0>();
 
-  gemm_epilogue<CC_BF16, EPI, 256>(args, acc, tm, m0, n0, wr, wc, lane, blockIdx.x * 8 + wave);
+  if constexpr (EPI == EPI_F32 || EPI == EPI_DEC) {
+    gemm_epilogue<CC_BF16, EPI, 256>(args, acc, tm, m0, n0, wr, wc, lane, blockIdx.x * 8 + wave);
+  } else {  // (the host routes N % 8 != 0 to gemm_kernel)
+    __builtin_amdgcn_s_barrier();  // every wave's zero-fill DMAs landed: the LDS is free
+    pp_epilogue_lds<EPI>(args, acc, smem, tm, m0, n0, wr, wc, lane, wave, blockIdx.x * 8 + wave);
+  }
 }

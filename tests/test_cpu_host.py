@@ -49,7 +49,8 @@ def test_argument_validation_without_gpu():
     assert lib.cc_clip_finalize(fake, (ctypes.c_int64 * 2)(0, 1), 9, 1.0, 0, fake, null) == 3
     assert b"NULL" in lib.cc_strerror(1)
     assert lib.cc_col_part_rows(4096) == 32 and lib.cc_wave_parts(4096, 16384) == 8 * 16 * 64
-    assert lib.cc_wgrad_parts(16384, 4608, 1) == 8 * 64 * 16  # 256 x 288 tiles
+    assert lib.cc_wgrad_parts(16384, 4608, 1) == 8 * 64 * 18  # bf16: ping-pong 256 x 256 tiles
+    assert lib.cc_wgrad_parts(16384, 4608, 2) == 8 * 64 * 18  # fp32: 256 x 256 tiles
     assert lib.cc_wgrad_parts(16384, 4608, 2) == 8 * 64 * 18  # fp32: 256 x 256
     assert lib.cc_loss_col_blocks(2304) == 5
 
