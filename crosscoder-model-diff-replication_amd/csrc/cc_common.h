@@ -14,14 +14,11 @@ typedef __attribute__((ext_vector_type(4))) short bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef uint16_t bf16_t;  // raw bits
 
-// ---- bf16 <-> f32 (round-to-nearest-even, NaN preserving like torch) ----
+// ---- bf16 <-> f32.  f32 -> bf16 is gfx950's v_cvt_pk_bf16_f32: round-to-nearest-even like
+// torch's c10::BFloat16 (NaN stays NaN, quieted); one instruction instead of the integer
+// rounding sequence and its NaN branch.
 CC_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
-CC_DEV bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);  // quiet NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
-}
+CC_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 
 // Storage element type of params / activations: bf16 (CC_BF16) or fp32 (CC_F32).
 template <int DT> struct Elem;

@@ -193,7 +193,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const uint32_t v = vo[p][q];
+#ifdef CC_EXP_NOLOAD  // timing-only experiment build (never shipped): every lane out of range
+      const uint32_t off = OOB + 0 * (kin && v != OOB ? v + kadd : 0);
+#else
       const uint32_t off = (kin && v != OOB) ? v + kadd : OOB;
+#endif
       __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? ra : rb, (lds_void*)(dst + pp_ci(p, q, wave) * 1024), 16,
                                                (int)off, 0, 0, 0);
     }
@@ -253,10 +257,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
           afr[ii][kk] = AKC ? pp_frag_kc(la, r0, kc_off[kk]) : pp_frag_mn(la, r0, kk, mn_off[(r0 >> 4) & 3]);
       }
       issue(p, p < 2 ? t + 1 : t + 2);
+#ifndef CC_PP_EXP_NOWAIT  // timing-only experiment builds (never shipped): skip the DMA wait
       wait_vmcnt<6>();
+#endif
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
+#if CC_PP_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -265,6 +274,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
           for (int j = 0; j < WG::TN; ++j)
             acc[2 * p + ii][j] =
                 __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii][kk], acc[2 * p + ii][j], 0, 0, 0);
+#if CC_PP_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
     }

@@ -340,6 +340,54 @@ struct AdamArgs {
   float bc2s;       // sqrt(1 - beta2^t)
   float neg_step;   // -lr / (1 - beta1^t)
 };
+// One Adam element update with torch's rounding points (see adam_kernel).
+template <int DT>
+CC_DEV void adam_elem(const AdamArgs& a, float coef, float& p, float g, float& m, float& v) {
+#pragma clang fp contract(off)
+  using E = Elem<DT>;
+  float gj = E::round(g * coef);
+  float w = a.w1;
+  float mj = w < 0.5f ? __builtin_fmaf(w, gj - m, m) : __builtin_fmaf(-(gj - m), 1.f - w, gj);
+  mj = E::round(mj);
+  float vj = E::round(v * a.beta2);
+  vj = E::round(vj + a.omb2 * gj * gj);
+  float den = E::round(sqrtf(vj));
+  den = E::round(den / a.bc2s);
+  den = E::round(den + a.eps);
+  p = E::round(p + a.neg_step * (mj / den));
+  m = mj;
+  v = vj;
+}
+
+#ifndef CC_ADAM_U
+#define CC_ADAM_U 1
+#endif
+// Bulk of the arena: U 8-element chunks per thread, all 4*U loads issued before any math, one
+// pass over the grid (no grid-stride loop).  U = 1 measured fastest (390 us for the 151 M-element
+// config-2 arena = 5.4 TB/s; U = 2: 398 us; the grid-stride loop: 431 us).
+template <int DT, int U>
+__global__ __launch_bounds__(256) void adam_bulk_kernel(const AdamArgs a, int64_t nchunks) {
+  const float coef = a.coef ? *a.coef : 1.f;
+  const int64_t c0 = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
+  float p[U][8], g[U][8], m[U][8], v[U][8];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t c = c0 + u * 256;
+    if (c < nchunks) {
+      load8<DT>(a.p, c * 8, p[u]); load8<DT>(a.g, c * 8, g[u]); load8<DT>(a.m, c * 8, m[u]); load8<DT>(a.v, c * 8, v[u]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t c = c0 + u * 256;
+    if (c < nchunks) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) adam_elem<DT>(a, coef, p[u][j], g[u][j], m[u][j], v[u][j]);
+      store8<DT>(a.p, c * 8, p[u]); store8<DT>(a.m, c * 8, m[u]); store8<DT>(a.v, c * 8, v[u]);
+    }
+  }
+}
+
 template <int DT>
 __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   using E = Elem<DT>;
@@ -546,12 +594,31 @@ int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const 
   double bc1 = 1.0 - pow(b1, (double)step), bc2 = 1.0 - pow(b2, (double)step);
   a.bc2s = (float)sqrt(bc2);
   a.neg_step = (float)(-((double)lr / bc1));
+  hipStream_t st = (hipStream_t)stream;
+#if CC_ADAM_U > 0
+  const int64_t nchunks = numel / 8;
+  if (nchunks > 0) {
+    const int64_t blocks = (nchunks + 256 * CC_ADAM_U - 1) / (256 * CC_ADAM_U);
+    DISPATCH_DT(dtype, hipLaunchKernelGGL((adam_bulk_kernel<DT_, CC_ADAM_U>), dim3((unsigned)blocks), dim3(256), 0,
+                                          st, a, nchunks));
+    CC_LAUNCH_CHECK();
+  }
+  if (numel % 8) {  // the last < 8 elements
+    const int es = dtype == CC_BF16 ? 2 : 4;
+    const int64_t off = nchunks * 8 * es;
+    AdamArgs t = a;
+    t.p = (char*)p + off; t.g = (const char*)g + off; t.m = (char*)m + off; t.v = (char*)v + off;
+    t.numel = numel % 8;
+    DISPATCH_DT(dtype, hipLaunchKernelGGL((adam_kernel<DT_>), dim3(1), dim3(256), 0, st, t));
+    CC_LAUNCH_CHECK();
+  }
+#else
   int64_t work = (numel + 7) / 8;
   int64_t blocks = (work + 255) / 256;
   if (blocks > 256 * 16) blocks = 256 * 16;
-  hipStream_t st = (hipStream_t)stream;
   DISPATCH_DT(dtype, hipLaunchKernelGGL((adam_kernel<DT_>), dim3((unsigned)blocks), dim3(256), 0, st, a));
   CC_LAUNCH_CHECK();
+#endif
   return CC_OK;
 }
 
