@@ -776,33 +776,73 @@ int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const
   return launch_dt<EPI_DACTS, true, true>(dtype, a, (hipStream_t)stream);
 }
 
-int cc_wgrad_dec(const void* acts, const void* g_recon, const void* W_dec, const float* inv_norms,
-                 const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_part, int64_t B, int64_t h,
-                 int64_t n, int64_t d, int dtype, void* stream) {
-  const float* norms = inv_norms;
+}  // extern "C"
+
+static int wgrad_dec_args(GemmArgs& a, const void* acts, const void* g_recon, const void* W_dec, const float* inv_norms,
+                          const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_part, int64_t B,
+                          int64_t h, int64_t n, int64_t d, int dtype) {
   if (!grad_W_dec) return CC_ERR_NULL;
-  if (l1_scale != 0.f && (!W_dec || !norms || !colsum_acts)) return CC_ERR_NULL;
-  GemmArgs a = {};
+  if (l1_scale != 0.f && (!W_dec || !inv_norms || !colsum_acts)) return CC_ERR_NULL;
+  a = GemmArgs{};
   int64_t K = n * d;
   a.A = acts; a.lda = h; a.B = g_recon; a.ldb = K;
   a.M = (int)h; a.N = (int)K; a.K = (int)B;
-  a.out = grad_W_dec; a.ldo = K; a.w_src = W_dec; a.norms = norms; a.colsum = colsum_acts;
+  a.out = grad_W_dec; a.ldo = K; a.w_src = W_dec; a.norms = inv_norms; a.colsum = colsum_acts;
   a.scale0 = l1_scale; a.wave_part0 = sq_part; a.d_model = (int)d; a.n_models = (int)n;
-  int rc = check_gemm(a, dtype, false, false);
+  return check_gemm(a, dtype, false, false);
+}
+
+static int wgrad_enc_args(GemmArgs& a, const void* g_pre, const void* x, void* grad_W_enc, float* sq_part, int64_t B,
+                          int64_t h, int64_t K, int dtype) {
+  if (!grad_W_enc) return CC_ERR_NULL;
+  a = GemmArgs{};
+  a.A = g_pre; a.lda = h; a.B = x; a.ldb = K;
+  a.M = (int)h; a.N = (int)K; a.K = (int)B;
+  a.out = grad_W_enc; a.ldo = K; a.wave_part0 = sq_part;
+  return check_gemm(a, dtype, false, false);
+}
+
+extern "C" {
+
+int cc_wgrad_dec(const void* acts, const void* g_recon, const void* W_dec, const float* inv_norms,
+                 const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_part, int64_t B, int64_t h,
+                 int64_t n, int64_t d, int dtype, void* stream) {
+  GemmArgs a;
+  int rc = wgrad_dec_args(a, acts, g_recon, W_dec, inv_norms, colsum_acts, l1_scale, grad_W_dec, sq_part, B, h, n, d,
+                          dtype);
   if (rc) return rc;
   return launch_dt<EPI_WGDEC, false, false>(dtype, a, (hipStream_t)stream);
 }
 
 int cc_wgrad_enc(const void* g_pre, const void* x, void* grad_W_enc, float* sq_part, int64_t B, int64_t h, int64_t K,
                  int dtype, void* stream) {
-  if (!grad_W_enc) return CC_ERR_NULL;
-  GemmArgs a = {};
-  a.A = g_pre; a.lda = h; a.B = x; a.ldb = K;
-  a.M = (int)h; a.N = (int)K; a.K = (int)B;
-  a.out = grad_W_enc; a.ldo = K; a.wave_part0 = sq_part;
-  int rc = check_gemm(a, dtype, false, false);
+  GemmArgs a;
+  int rc = wgrad_enc_args(a, g_pre, x, grad_W_enc, sq_part, B, h, K, dtype);
   if (rc) return rc;
   return launch_dt<EPI_WGENC, false, false>(dtype, a, (hipStream_t)stream);
+}
+
+int cc_wgrad_both(const void* acts, const void* g_recon, const void* W_dec, const float* inv_norms,
+                  const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_pre,
+                  const void* x, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
+                  int dtype, void* stream) {
+  GemmArgs a0, a1;
+  int rc = wgrad_dec_args(a0, acts, g_recon, W_dec, inv_norms, colsum_acts, l1_scale, grad_W_dec, sq_dec, B, h, n, d,
+                          dtype);
+  if (rc) return rc;
+  rc = wgrad_enc_args(a1, g_pre, x, grad_W_enc, sq_enc, B, h, n * d, dtype);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (!use_pp(a0.N, false, false, dtype)) {
+    rc = launch_dt<EPI_WGDEC, false, false>(dtype, a0, st);
+    return rc ? rc : launch_dt<EPI_WGENC, false, false>(dtype, a1, st);
+  }
+  a0.nbm = a1.nbm = (a0.M + BM - 1) / BM;
+  a0.nbn = a1.nbn = (a0.N + 255) / 256;
+  hipLaunchKernelGGL((gemm_pp_dual_kernel<false, false, EPI_WGDEC, EPI_WGENC>), dim3(2 * a0.nbm * a0.nbn), dim3(NTHR),
+                     0, st, a0, a1);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
 }
 
 }  // extern "C"

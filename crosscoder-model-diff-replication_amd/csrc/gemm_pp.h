@@ -134,19 +134,21 @@ CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char
   }
 }
 
+constexpr int PP_LDS = 4 * 256 * 128;  // 2 buffers x (A | B) K-step images
+
+// One output tile of one GEMM; bid = the tile's block index within that GEMM's grid.
 template <bool AKC, bool BKC, int EPI>
-__global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
+CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
   using WG = WaveGeom<256>;
   static_assert(WG::TM == 8 && WG::TN == 4, "ping-pong geometry");
   constexpr int TILE = 256 * 128;  // one operand's K-step image
   constexpr int BUF = 2 * TILE;
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   int tm, tn;
-  tile_of_block(blockIdx.x, args.nbm, args.nbn, tm, tn);
+  tile_of_block(bid, args.nbm, args.nbn, tm, tn);
   const int m0 = tm * BM, n0 = tn * 256;
   const int M = args.M, N = args.N, K = args.K;
 
@@ -285,9 +287,26 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
   wait_vmcnt<0>();
 
   if constexpr (EPI == EPI_F32 || EPI == EPI_DEC) {
-    gemm_epilogue<CC_BF16, EPI, 256>(args, acc, tm, m0, n0, wr, wc, lane, blockIdx.x * 8 + wave);
+    gemm_epilogue<CC_BF16, EPI, 256>(args, acc, tm, m0, n0, wr, wc, lane, bid * 8 + wave);
   } else {  // (the host routes N % 8 != 0 to gemm_kernel)
     __builtin_amdgcn_s_barrier();  // every wave's zero-fill DMAs landed: the LDS is free
-    pp_epilogue_lds<EPI>(args, acc, smem, tm, m0, n0, wr, wc, lane, wave, blockIdx.x * 8 + wave);
+    pp_epilogue_lds<EPI>(args, acc, smem, tm, m0, n0, wr, wc, lane, wave, bid * 8 + wave);
   }
+}
+
+template <bool AKC, bool BKC, int EPI>
+__global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
+  __shared__ __attribute__((aligned(16))) char smem[PP_LDS];
+  pp_tile<AKC, BKC, EPI>(args, smem, blockIdx.x);
+}
+
+// Two independent GEMMs of one layout in one launch: blocks [0, nb0) are a0's tiles, the rest
+// a1's.  dW_dec and dW_enc (1152 tiles each at config 2: 4.5 waves of 256 CUs apiece) become
+// 2304 tiles = 9 full waves, and one kernel boundary disappears.
+template <bool AKC, bool BKC, int EPI0, int EPI1>
+__global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_kernel(const GemmArgs a0, const GemmArgs a1) {
+  __shared__ __attribute__((aligned(16))) char smem[PP_LDS];
+  const int nb0 = a0.nbm * a0.nbn;
+  if ((int)blockIdx.x < nb0) pp_tile<AKC, BKC, EPI0>(a0, smem, blockIdx.x);
+  else pp_tile<AKC, BKC, EPI1>(a1, smem, blockIdx.x - nb0);
 }

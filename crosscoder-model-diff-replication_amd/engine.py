@@ -147,11 +147,9 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0):
         ops.dacts_bwd(ws.g_recon, P.W_dec_hk, ws.acts, ws.tn, l1_scale, ws.g_pre, colsum_part=ws.gpre_colpart)
     if l1_scale != 0.0:
         ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts)
-    with _span("G4_wgrad_dec"):
-        ops.wgrad_dec(ws.acts, ws.g_recon, P.W_dec_hk, ws.inv_norms, ws.colsum_acts, l1_scale, G.W_dec_hk,
-                      ws.sq_slice(1), n, d)
-    with _span("G5_wgrad_enc"):
-        ops.wgrad_enc(ws.g_pre, ws.x, G.W_enc_hk, ws.sq_slice(0))
+    with _span("G4G5_wgrad"):
+        ops.wgrad_both(ws.acts, ws.g_recon, P.W_dec_hk, ws.inv_norms, ws.colsum_acts, l1_scale, G.W_dec_hk,
+                       ws.sq_slice(1), ws.g_pre, ws.x, G.W_enc_hk, ws.sq_slice(0), n, d)
     ops.reduce_rows(ws.gpre_colpart, ws.gpre_colpart.shape[0], h, out_t=G.b_enc, sq_part=ws.sq_slice(2))
     ops.reduce_rows(ws.loss_colpart, ws.loss_colpart.shape[0], K, out_t=G.b_dec_flat, sq_part=ws.sq_slice(3))
 

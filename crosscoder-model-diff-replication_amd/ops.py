@@ -168,6 +168,15 @@ def wgrad_enc(g_pre, x, grad, sq_part):
                              _stream(g_pre)))
 
 
+def wgrad_both(acts, g_recon, W_dec_hk, norms, colsum_acts, l1_scale, grad_dec, sq_dec, g_pre, x, grad_enc, sq_enc,
+               n, d):
+    """wgrad_dec + wgrad_enc (same results), one launch where the ping-pong GEMM serves both."""
+    B, h = acts.shape
+    check(lib().cc_wgrad_both(_ptr(acts), _ptr(g_recon), _ptr(W_dec_hk), _ptr(norms), _ptr(colsum_acts), l1_scale,
+                              _ptr(grad_dec), _ptr(sq_dec), _ptr(g_pre), _ptr(x), _ptr(grad_enc), _ptr(sq_enc), B, h,
+                              n, d, dtype_code(acts.dtype), _stream(acts)))
+
+
 def clip_finalize(sq, offsets, max_norm, emulate_bf16, out):
     arr = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
     check(lib().cc_clip_finalize(_ptr(sq), arr, len(offsets) - 1, max_norm, int(emulate_bf16), _ptr(out),

@@ -137,6 +137,14 @@ int cc_wgrad_dec(const void* acts, const void* g_recon, const void* W_dec, const
 int cc_wgrad_enc(const void* g_pre, const void* x, void* grad_W_enc, float* sq_part, int64_t B, int64_t h,
                  int64_t K, int dtype, void* stream);
 
+/* cc_wgrad_dec and cc_wgrad_enc with the same arguments and results, as ONE launch when the
+ * ping-pong GEMM serves them (bf16, K % 8 == 0): the two tile sets fill whole waves together
+ * (2 x 1152 tiles = 9 x 256 CUs at config 2); otherwise two launches. */
+int cc_wgrad_both(const void* acts, const void* g_recon, const void* W_dec, const float* inv_norms,
+                  const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_pre,
+                  const void* x, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
+                  int dtype, void* stream);
+
 /* clip_grad_norm_(params, max_norm) (trainer.py:46; torch/nn/utils/clip_grad.py): per-param
  * norms from the squared-sum partials sq[off[i] .. off[i+1]) (nparams <= 8, off on the HOST),
  * total = ||(norm_i)||, coef = min(1, max_norm / (total + 1e-6)).  emulate_bf16 rounds the

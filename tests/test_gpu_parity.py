@@ -103,6 +103,38 @@ def test_gemm_pingpong_matches_two_stage(gpu, pp_mask, shape, layouts):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("shape", [(512, 768, 2, 200), (1024, 1000, 2, 96)])
+def test_wgrad_both_matches_separate(gpu, shape):
+    """The single-launch dW_dec + dW_enc (cc_wgrad_both) equals the two separate launches bitwise."""
+    B, h, n, d = shape
+    K = n * d
+    g = torch.Generator().manual_seed(B + h)
+    bf = torch.bfloat16
+    mk = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).to(bf).to(gpu)  # noqa: E731
+    acts = torch.relu(mk(B, h)).contiguous()
+    g_recon, g_pre, x = mk(B, K, sc=1e-2), mk(B, h, sc=1e-2), mk(B, K)
+    W = mk(h, K, sc=0.05)
+    inv = torch.rand(h, n, generator=g).to(gpu) + 0.5
+    colsum = acts.float().sum(0)
+    parts = ops.wgrad_parts(h, K, bf)
+    outs = []
+    for both in (False, True):
+        gd, ge = torch.empty(h, K, dtype=bf, device=gpu), torch.empty(h, K, dtype=bf, device=gpu)
+        sd, se = torch.zeros(parts, device=gpu), torch.zeros(parts, device=gpu)
+        if both:
+            ops.wgrad_both(acts, g_recon, W, inv, colsum, 3e-4, gd, sd, g_pre, x, ge, se, n, d)
+        else:
+            ops.wgrad_dec(acts, g_recon, W, inv, colsum, 3e-4, gd, sd, n, d)
+            ops.wgrad_enc(g_pre, x, ge, se)
+        outs.append((gd, ge, sd, se))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    ref = (acts.double().t() @ g_recon.double())
+    assert rel(outs[1][0].double() - 3e-4 * colsum.double()[:, None] * (W.double().view(h, n, d) *
+               inv.double()[:, :, None]).view(h, K), ref) < 1e-2
+
+
 @pytest.mark.parametrize("mask", [0, 7])
 def test_step_gemm_paths(gpu, pp_mask, mask):
     """One fused fwd+bwd at a mid size through each main loop vs the fp32 oracle."""

@@ -44,6 +44,8 @@ def main():
     norms = torch.ones(h, n, device=dev)
     colsum = torch.ones(h, device=dev)
     gW = torch.empty(h, K, device=dev, dtype=bf)
+    gW2 = torch.empty(h, K, device=dev, dtype=bf)
+    parts2 = torch.empty(1 << 20, device=dev)
     parts = torch.empty(1 << 20, device=dev)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -61,6 +63,8 @@ def main():
             "G4_no_l1term": lambda: L.cc_wgrad_dec(P(acts), P(g_recon), P(W2), P(norms), P(colsum), 0.0, P(gW),
                                                    P(parts), B, h, n, d, 1, st),
             "G5_wgrad_enc": lambda: L.cc_wgrad_enc(P(g_pre), P(x), P(gW), P(parts), B, h, K, 1, st),
+            "G4G5_both_x0.5": lambda: L.cc_wgrad_both(P(acts), P(g_recon), P(W2), P(norms), P(colsum), 1e-4, P(gW),
+                                                      P(parts), P(g_pre), P(x), P(gW2), P(parts2), B, h, n, d, 1, st),
             "G5_on_G4_data": lambda: L.cc_wgrad_enc(P(acts), P(g_recon), P(gW), P(parts), B, h, K, 1, st),
         }
 
@@ -79,7 +83,7 @@ def main():
                     fn()
                 e.record()
                 torch.cuda.synchronize()
-                res.setdefault((path, name), []).append(s.elapsed_time(e) / 10)
+                res.setdefault((path, name), []).append(s.elapsed_time(e) / 10 / (2 if name.startswith("G4G5") else 1))
     for (p, name), ts in sorted(res.items(), key=lambda kv: (kv[0][1], kv[0][0])):
         ts.sort()
         med = ts[len(ts) // 2]
