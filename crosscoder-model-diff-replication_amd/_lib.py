@@ -41,6 +41,7 @@ SIGNATURES = {
     "cc_encode_fwd": (_i, [_p, _p, _p, _p, _p, _i, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_decode_fwd": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_loss_fwd_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i, _p]),
+    "cc_loss_fwd_bwd_rows": (_i, [_p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_loss_finalize": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
     "cc_dacts_bwd": (_i, [_p, _p, _p, _p, _f, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_dec": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),

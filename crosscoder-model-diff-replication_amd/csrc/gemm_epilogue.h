@@ -87,15 +87,44 @@ struct RegIO {
   CC_DEV void out4(int i, int j, const float v[4]) const { bst4<DT>(rout, fg.boff(i, j, ES), v); }
 };
 
+// Per-fragment factor of dW_dec's L1 term: (l1_scale * sum_b acts[b, row]) * (1 / ||W_dec[row, model]||),
+// 0 outside the matrix.  All 8 + 32 loads are issued before any is used (one memory latency for
+// the lot; the LDS-staged epilogue issues them beside its W_dec tile DMA).
+template <int BNT>
+CC_DEV void wgdec_factors(const GemmArgs& args, const FragGeom<BNT>& fg, int m0, int n0,
+                          float (&cw)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN]) {
+  using WG = WaveGeom<BNT>;
+  const __amdgpu_buffer_rsrc_t rnorm = vec_rsrc(args.norms, m0 * args.n_models, (int64_t)args.M * args.n_models, 4);
+  const __amdgpu_buffer_rsrc_t rcol = vec_rsrc(args.colsum, m0, args.M, 4);
+  float cs[WG::TM];
+#pragma unroll
+  for (int i = 0; i < WG::TM; ++i) cs[i] = bldf(rcol, fg.rv[i] ? (uint32_t)((fg.r0 + 16 * i) * 4) : OOB);
+#pragma unroll
+  for (int j = 0; j < WG::TN; ++j) {
+    const int model = (n0 + fg.c0 + 16 * j) / args.d_model;
+#pragma unroll
+    for (int i = 0; i < WG::TM; ++i)
+      cw[i][j] = bldf(rnorm, fg.ok(i, j) ? (uint32_t)(((fg.r0 + 16 * i) * args.n_models + model) * 4) : OOB);
+  }
+#pragma unroll
+  for (int i = 0; i < WG::TM; ++i) {
+    const float c = args.scale0 * cs[i];
+#pragma unroll
+    for (int j = 0; j < WG::TN; ++j) cw[i][j] = c * cw[i][j];
+  }
+}
+
 // The element-wise part of EPI_ENC / EPI_DACTS / EPI_WGDEC / EPI_WGENC over one wave's fragments.
+// cw: dW_dec L1-term factors loaded by the caller (wgdec_factors; EPI_WGDEC with l1_scale != 0
+// only, otherwise unread).  Passed by reference so they stay in registers.
 template <int DT, int EPI, int BNT, class IO>
 CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN],
                           const FragGeom<BNT>& fg, const IO& io, int tm, int m0, int n0, int wr, int lane,
-                          int wave_slot) {
+                          int wave_slot, const float (&cw)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN]) {
   using E = Elem<DT>;
   using WG = WaveGeom<BNT>;
   constexpr int ES = DT == CC_BF16 ? 2 : 4;
-  const int M = args.M, N = args.N;
+  const int N = args.N;
   if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
     constexpr int JB = EPB<DT, BNT>::JB_M;
     const bool has_bias = EPI == EPI_ENC && args.bias;
@@ -180,35 +209,15 @@ CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
     constexpr int JB = EPB<DT, BNT>::JB_W;
     const bool l1term = EPI == EPI_WGDEC && args.scale0 != 0.f;
     float sq = 0.f;
-    // per-row factor scale * sum_b acts[b, row]; per (row, model) the inverse decoder norm
-    float cs[WG::TM];
     typename V4<DT>::T wraw[EPI == EPI_WGDEC ? WG::TM : 1][JB];
-    float cw[EPI == EPI_WGDEC ? WG::TM : 1][JB];
-    __amdgpu_buffer_rsrc_t rnorm = make_rsrc(args.A, 0);
-    if constexpr (EPI == EPI_WGDEC) {
-      if (l1term) {
-        rnorm = vec_rsrc(args.norms, m0 * args.n_models, (int64_t)M * args.n_models, 4);
-        const __amdgpu_buffer_rsrc_t rcol = vec_rsrc(args.colsum, m0, M, 4);
-#pragma unroll
-        for (int i = 0; i < WG::TM; ++i)
-          cs[i] = args.scale0 * bldf(rcol, fg.rv[i] ? (uint32_t)((fg.r0 + 16 * i) * 4) : OOB);
-      }
-    }
 #pragma unroll
     for (int j = 0; j < WG::TN; ++j) {
       if constexpr (EPI == EPI_WGDEC) {
         if (l1term && j % JB == 0) {
 #pragma unroll
-          for (int jj = 0; jj < JB; ++jj) {
-            const int model = (n0 + fg.c0 + 16 * (j + jj)) / args.d_model;
+          for (int jj = 0; jj < JB; ++jj)
 #pragma unroll
-            for (int i = 0; i < WG::TM; ++i) {
-              wraw[i][jj] = io.in4(i, j + jj);
-              cw[i][jj] = cs[i] * bldf(rnorm, fg.ok(i, j + jj)
-                                                  ? (uint32_t)(((fg.r0 + 16 * i) * args.n_models + model) * 4)
-                                                  : OOB);  // inverse norms
-            }
-          }
+            for (int i = 0; i < WG::TM; ++i) wraw[i][jj] = io.in4(i, j + jj);
         }
       }
 #pragma unroll
@@ -219,7 +228,7 @@ CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
         if constexpr (EPI == EPI_WGDEC) {
           if (l1term) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += cw[i][j % JB] * V4<DT>::get(wraw[i][j % JB], e);
+            for (int e = 0; e < 4; ++e) v[e] += cw[i][j] * V4<DT>::get(wraw[i][j % JB], e);
           }
         }
 #pragma unroll
@@ -273,6 +282,10 @@ CC_DEV void gemm_epilogue(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
   } else {
     const void* in = EPI == EPI_DACTS ? args.mask_src : (EPI == EPI_WGDEC ? args.w_src : nullptr);
     const RegIO<DT, BNT> io(args, fg, in, m0, n0);
-    epilogue_core<DT, EPI, BNT>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot);
+    float cw[WG::TM][WG::TN];
+    if constexpr (EPI == EPI_WGDEC) {
+      if (args.scale0 != 0.f) wgdec_factors<BNT>(args, fg, m0, n0, cw);
+    }
+    epilogue_core<DT, EPI, BNT>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, cw);
   }
 }

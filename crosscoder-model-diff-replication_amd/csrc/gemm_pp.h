@@ -112,6 +112,7 @@ CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char
     return (row < rows && 8 * c < cols) ? (uint32_t)((row * ldo + 8 * c) * 2) : OOB;
   };
   const void* in = EPI == EPI_DACTS ? args.mask_src : (EPI == EPI_WGDEC && args.scale0 != 0.f ? args.w_src : nullptr);
+  float cw[8][4];  // dW_dec L1-term factors (EPI_WGDEC only)
   if (in) {
     const __amdgpu_buffer_rsrc_t rin = tile_rsrc(in, args.ldo, m0, n0, args.M, args.N, 2);
 #pragma unroll
@@ -119,11 +120,13 @@ CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char
       const int ci = q * 8 + wave;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_void*)(smem + ci * 1024), 16, (int)xoff(ci), 0, 0, 0);
     }
+    // the L1-term factors' loads fly with the tile DMA (one latency for both)
+    if constexpr (EPI == EPI_WGDEC) wgdec_factors<256>(args, fg, m0, n0, cw);
     wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
   }
   const LdsIO io(smem, wr, wc, lane);
-  epilogue_core<CC_BF16, EPI, 256>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot);
+  epilogue_core<CC_BF16, EPI, 256>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, cw);
   __syncthreads();
   const __amdgpu_buffer_rsrc_t rout = tile_rsrc(args.out, args.ldo, m0, n0, args.M, args.N, 2);
 #pragma unroll

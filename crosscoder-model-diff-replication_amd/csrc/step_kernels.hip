@@ -128,15 +128,17 @@ __global__ __launch_bounds__(256) void dec_norms_kernel(const void* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------
-// Reconstruction loss + gradient.  grid: (n * ncb, ceil(B/32)); block 256 = 4 waves.
-// Block covers model m = blockIdx.x / ncb, columns [m*d + cb*512, +512) ∩ model, 32 rows.
-// lane -> 8 columns; wave w -> rows r0 + w + 4i.
+// Reconstruction loss + gradient.  grid: (n * ncb, ceil(rows/32)); block 256 = 4 waves.
+// Block covers model m = blockIdx.x / ncb, columns [m*d + cb*512, +512) ∩ model, 32 rows of the
+// row range [row0, row_end) (row0 % 32 == 0).  The slabs keep the whole-batch layout, so disjoint
+// row ranges can be separate launches: the latent-sharded step runs each batch slice as soon as
+// its all-reduce has landed.  lane -> 8 columns; wave w -> rows r0 + w + 4i.
 template <int DT>
 __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ recon, const void* __restrict__ b_dec,
                                                    const void* __restrict__ x, const float* __restrict__ x_mean,
                                                    void* __restrict__ g_recon, float* __restrict__ row_part,
                                                    float* __restrict__ col_part, float grad_scale, int B, int n,
-                                                   int d, int ncb) {
+                                                   int d, int ncb, int row0, int row_end) {
   __shared__ float red[4][512];
   using E = Elem<DT>;
   const int K = n * d;
@@ -145,7 +147,7 @@ __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ rec
   const int jc = cb * LOSS_COLS + lane * 8;  // column within model
   const bool cv = jc < d;
   const int col = m * d + jc;
-  const int r0 = blockIdx.y * LOSS_ROWS;
+  const int r0 = row0 + blockIdx.y * LOSS_ROWS;
   float bd[8], mu[8], cs[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bd[j] = mu[j] = cs[j] = 0.f;
@@ -156,7 +158,7 @@ __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ rec
   const int64_t plane = (int64_t)n * ncb * B;  // row_part [2][n*ncb][B]
   for (int i = 0; i < LOSS_ROWS / 4; ++i) {
     const int r = r0 + wave + 4 * i;
-    if (r >= B) break;  // wave-uniform
+    if (r >= row_end) break;  // wave-uniform
     float l2 = 0.f, tv = 0.f;
     if (cv) {
       float rv[8], xv[8], g[8];
@@ -186,7 +188,9 @@ __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ rec
   __syncthreads();
   for (int i = threadIdx.x; i < LOSS_COLS; i += 256) {
     int jj = cb * LOSS_COLS + i;
-    if (jj < d) col_part[(int64_t)blockIdx.y * K + m * d + jj] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+    if (jj < d)
+      col_part[(int64_t)(row0 / LOSS_ROWS + blockIdx.y) * K + m * d + jj] =
+          ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
   }
 }
 
@@ -530,20 +534,29 @@ int cc_dec_norms(const void* W_dec, float* norms, float* total, float* inv_norms
   return CC_OK;
 }
 
-int cc_loss_fwd_bwd(const float* recon_f32, const void* b_dec, const void* x, const float* x_mean, void* g_recon,
-                    float* row_part, float* col_part, float grad_scale, int64_t B, int64_t n, int64_t d, int dtype,
-                    void* stream) {
+int cc_loss_fwd_bwd_rows(const float* recon_f32, const void* b_dec, const void* x, const float* x_mean,
+                         void* g_recon, float* row_part, float* col_part, float grad_scale, int64_t row0,
+                         int64_t rows, int64_t B, int64_t n, int64_t d, int dtype, void* stream) {
   if (!recon_f32 || !x || !g_recon || !row_part) return CC_ERR_NULL;
   if (B <= 0 || n <= 0 || d <= 0 || d % 8) return CC_ERR_SHAPE;
+  if (row0 < 0 || rows <= 0 || row0 + rows > B || row0 % LOSS_ROWS) return CC_ERR_SHAPE;
   if (!al16(recon_f32) || !al16(x) || !al16(g_recon) || (b_dec && !al16(b_dec)) || (x_mean && !al16(x_mean)))
     return CC_ERR_ALIGN;
   int ncb = (int)cc_loss_col_blocks(d);
-  dim3 grid((unsigned)(n * ncb), (unsigned)cc_loss_part_rows(B));
+  dim3 grid((unsigned)(n * ncb), (unsigned)cc_loss_part_rows(rows));
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_DT(dtype, hipLaunchKernelGGL((loss_kernel<DT_>), grid, dim3(256), 0, st, recon_f32, b_dec, x, x_mean,
-                                        g_recon, row_part, col_part, grad_scale, (int)B, (int)n, (int)d, ncb));
+                                        g_recon, row_part, col_part, grad_scale, (int)B, (int)n, (int)d, ncb,
+                                        (int)row0, (int)(row0 + rows)));
   CC_LAUNCH_CHECK();
   return CC_OK;
+}
+
+int cc_loss_fwd_bwd(const float* recon_f32, const void* b_dec, const void* x, const float* x_mean, void* g_recon,
+                    float* row_part, float* col_part, float grad_scale, int64_t B, int64_t n, int64_t d, int dtype,
+                    void* stream) {
+  return cc_loss_fwd_bwd_rows(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_scale, 0, B, B, n, d,
+                              dtype, stream);
 }
 
 int cc_loss_finalize(const float* row_part, const float* l1_part, const float* l0_part, int64_t n_wave, float* ev,

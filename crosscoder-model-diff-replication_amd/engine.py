@@ -117,9 +117,10 @@ class StepWorkspace:
         return self.sq[self.sq_off[i]:self.sq_off[i + 1]]
 
 
-def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True):
+def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True):
     """Forward + reconstruction-loss gradient.  P: params Arena.  x_in [B, n, d] any of
-    fp32/bf16, factor [n] or None.  Leaves losses in ws.scalars / ws.ev*, g_recon ready."""
+    fp32/bf16, factor [n] or None.  Leaves losses in ws.scalars / ws.ev*, g_recon ready
+    (loss=False: stops at the fp32 reconstruction, for loss_rows / loss_finalize by slices)."""
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
     ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart)
     ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
@@ -129,22 +130,51 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True):
                        l1_part=ws.l1_part, l0_part=ws.l0_part)
     with _span("G2_decode"):
         ops.decode_fwd(ws.acts, P.W_dec_hk, None, recon_f32=ws.recon)
-    return loss_from_recon(ws, P, grad_scale)
+    if loss:
+        loss_from_recon(ws, P, grad_scale)
+
+
+def loss_rows(ws, P, r0, r1, grad_scale=None):
+    """Loss row terms + g_recon for batch rows [r0, r1) (r0 % 32 == 0); slabs keep the batch layout."""
+    gs = 2.0 / ws.B if grad_scale is None else grad_scale
+    ops.loss_fwd_bwd(ws.recon, P.b_dec_flat, ws.x, ws.x_mean, ws.g_recon, ws.row_part, ws.loss_colpart, gs, ws.B,
+                     ws.n, ws.d, row0=r0, rows=r1 - r0)
+
+
+def loss_finalize(ws):
+    ops.loss_finalize(ws.row_part, ws.l1_part, ws.l0_part, ws.n_wave, ws.ev, ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n,
+                      ws.d)
 
 
 def loss_from_recon(ws, P, grad_scale=None):
-    B, n, d = ws.B, ws.n, ws.d
-    gs = 2.0 / B if grad_scale is None else grad_scale
-    ops.loss_fwd_bwd(ws.recon, P.b_dec_flat, ws.x, ws.x_mean, ws.g_recon, ws.row_part, ws.loss_colpart, gs, B, n, d)
-    ops.loss_finalize(ws.row_part, ws.l1_part, ws.l0_part, ws.n_wave, ws.ev, ws.ev_a, ws.ev_b, ws.scalars, B, n, d)
+    loss_rows(ws, P, 0, ws.B, grad_scale)
+    loss_finalize(ws)
 
 
-def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0):
-    """Gradients of l2 + l1_coeff * l1 into the grads Arena G (+ squared-sum partials)."""
+def row_chunks(B, n_chunks):
+    """Batch slices [r0, r1) for the chunked (comm-overlapped) step: boundaries on 256-row GEMM
+    tiles, so each slice's d_acts launch owns whole column-partial rows."""
+    step = -(-B // max(1, n_chunks))
+    step = -(-step // 256) * 256
+    return [(r0, min(B, r0 + step)) for r0 in range(0, B, step)]
+
+
+def dacts_rows(ws, P, l1_coeff, r0, r1, l1_grad_weight=1.0):
+    """G3 over batch rows [r0, r1) (r0 % 256 == 0): g_pre rows + their column-sum partial rows."""
+    l1_scale = float(l1_coeff) * l1_grad_weight / ws.B
+    c0, c1 = ops.col_part_rows(r0), ops.col_part_rows(r1)
+    with _span("G3_dacts"):
+        ops.dacts_bwd(ws.g_recon[r0:r1], P.W_dec_hk, ws.acts[r0:r1], ws.tn, l1_scale, ws.g_pre[r0:r1],
+                      colsum_part=ws.gpre_colpart[c0:c1])
+
+
+def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False):
+    """Gradients of l2 + l1_coeff * l1 into the grads Arena G (+ squared-sum partials).
+    dacts_done: G3 already ran per batch slice (dacts_rows)."""
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
     l1_scale = float(l1_coeff) * l1_grad_weight / B
-    with _span("G3_dacts"):
-        ops.dacts_bwd(ws.g_recon, P.W_dec_hk, ws.acts, ws.tn, l1_scale, ws.g_pre, colsum_part=ws.gpre_colpart)
+    if not dacts_done:
+        dacts_rows(ws, P, l1_coeff, 0, B, l1_grad_weight)
     if l1_scale != 0.0:
         ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts)
     with _span("G4G5_wgrad"):

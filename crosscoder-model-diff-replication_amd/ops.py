@@ -138,9 +138,12 @@ def decode_fwd(acts, W_dec_hk, b_dec=None, recon_f32=None, recon_t=None):
                               dtype_code(acts.dtype), _stream(acts)))
 
 
-def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_scale, B, n, d):
-    check(lib().cc_loss_fwd_bwd(_ptr(recon_f32), _ptr(b_dec), _ptr(x), _ptr(x_mean), _ptr(g_recon), _ptr(row_part),
-                                _ptr(col_part), grad_scale, B, n, d, dtype_code(x.dtype), _stream(x)))
+def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_scale, B, n, d, row0=0, rows=None):
+    """Loss terms + g_recon for batch rows [row0, row0 + rows) (default: all B rows)."""
+    rows = B - row0 if rows is None else rows
+    check(lib().cc_loss_fwd_bwd_rows(_ptr(recon_f32), _ptr(b_dec), _ptr(x), _ptr(x_mean), _ptr(g_recon),
+                                     _ptr(row_part), _ptr(col_part), grad_scale, row0, rows, B, n, d,
+                                     dtype_code(x.dtype), _stream(x)))
 
 
 def loss_finalize(row_part, l1_part, l0_part, n_wave, ev, ev_a, ev_b, scalars, B, n, d):

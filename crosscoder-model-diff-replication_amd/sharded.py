@@ -5,12 +5,18 @@ Rank r owns latents [r*h/G, (r+1)*h/G): its slice of W_enc / W_dec / b_enc and t
 moments; b_dec is replicated.  Per step (reference Trainer.step, trainer.py:41-63):
   1. every rank reads the SAME batch (replicated x), encodes its latents and decodes them into
      an fp32 partial reconstruction [B, n*d] (no bias)                     -> G1, G2 local
-  2. all_reduce(SUM) of the partial reconstructions (the only bulk exchange)   RCCL, 4*B*n*d bytes
+  2. all_reduce(SUM) of the partial reconstructions (the only bulk exchange: 4*B*n*d bytes),
+     issued per batch slice (`recon_chunks`, default 4) on RCCL's stream.  As soon as slice c
+     has landed, its loss rows / g_recon and its d_acts rows (G3) run on the compute stream
+     while the all-reduce of slice c+1 is still on the wire, so only the first slice's
+     all-reduce is exposed.  (Slicing the encode/decode instead would leave the 256-tile G2
+     launch a fraction of the 256 CUs per slice.)
   3. b_dec + loss + g_recon on the full reconstruction: identical on all ranks
-  4. all_reduce of the two latent-local loss sums (l1, l0)                 8 bytes
-  5. backward is local (g_recon is replicated): G3, G4, G5, db_enc local; db_dec replicated
-  6. clip_grad_norm_: per-parameter squared sums all-reduced (b_dec counted once)   16 bytes
-  7. Adam on the local arena (b_dec updates are identical on every rank).
+  4. the rest of the backward is local (g_recon is replicated): G4, G5, db_enc local; db_dec
+     replicated
+  5. ONE small all-reduce: the per-parameter squared-gradient sums for clip_grad_norm_ (b_dec
+     counted once) and the two latent-local loss sums (l1, l0)            24 bytes
+  6. Adam on the local arena (b_dec updates are identical on every rank).
 
 `ShardedStep` holds the orchestration (the collectives and how partial results combine) and
 drives a backend that does the local compute: `HipShardBackend` (the product, engine.py
@@ -53,26 +59,37 @@ class ShardedStep:
     def step(self, raw, factor, l1c, lr, betas, eps, t, max_norm=1.0):
         b = self.b
         recon = b.forward_partial(raw, factor)
-        dist.all_reduce(recon, op=dist.ReduceOp.SUM, group=self.group)
-        scalars = b.loss_from_full_recon()           # [l2, l1_local, l0_local, ev, ev_a, ev_b, ...]
-        dist.all_reduce(scalars[1:3], op=dist.ReduceOp.SUM, group=self.group)
+        chunks = b.row_chunks()
+        # every slice's all-reduce is queued at once on the collective stream; the compute stream
+        # waits for slice c only when it needs it
+        works = [dist.all_reduce(recon[r0:r1], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                 for r0, r1 in chunks]
+        for (r0, r1), w in zip(chunks, works):
+            w.wait()
+            b.rows_ready(r0, r1, l1c)                # loss rows + g_recon + d_acts rows of the slice
+        scalars = b.loss_finalize()                  # [l2, l1_local, l0_local, ev, ev_a, ev_b, ...]
         sums = b.backward(l1c)                       # [4] local squared sums
-        gs = clip_sums_for_allreduce(sums, self.rank)
-        dist.all_reduce(gs, op=dist.ReduceOp.SUM, group=self.group)
-        b.clip_and_adam_from_sums(gs, lr, betas, eps, t, max_norm)
+        red = b.reduce_buffer()                      # [6]: 4 clip sums + l1, l0
+        red[0:4] = clip_sums_for_allreduce(sums, self.rank)
+        red[4:6] = scalars[1:3]
+        dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
+        scalars[1:3] = red[4:6]
+        b.clip_and_adam_from_sums(red[0:4], lr, betas, eps, t, max_norm)
         return scalars
 
 
 class HipShardBackend:
     """Local compute of one rank on its GPU (engine.py kernels)."""
 
-    def __init__(self, cc):
+    def __init__(self, cc, recon_chunks=4):
         self.cc = cc
         a = cc.arena()
         self.G = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
         self.M = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
         self.V = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
         self.sums = torch.zeros(4, dtype=torch.float32, device=a.data.device)
+        self.red = torch.zeros(6, dtype=torch.float32, device=a.data.device)
+        self.recon_chunks = recon_chunks
         self.ws = None
 
     def forward_partial(self, raw, factor):
@@ -90,16 +107,27 @@ class HipShardBackend:
             ops.decode_fwd(ws.acts, P.W_dec_hk, None, recon_f32=ws.recon)
         return ws.recon
 
-    def loss_from_full_recon(self):
-        engine.loss_from_recon(self.ws, self.cc.arena())
+    def row_chunks(self):
+        return engine.row_chunks(self.ws.B, self.recon_chunks)
+
+    def rows_ready(self, r0, r1, l1c):
+        P = self.cc.arena()
+        engine.loss_rows(self.ws, P, r0, r1)
+        engine.dacts_rows(self.ws, P, l1c, r0, r1)
+
+    def loss_finalize(self):
+        engine.loss_finalize(self.ws)
         return self.ws.scalars
 
     def backward(self, l1c):
         ws = self.ws
-        engine.backward(ws, self.cc.arena(), self.G, l1c)
+        engine.backward(ws, self.cc.arena(), self.G, l1c, dacts_done=True)
         for i in range(4):
             self.sums[i] = ws.sq_slice(i).sum()
         return self.sums
+
+    def reduce_buffer(self):
+        return self.red
 
     def clip_and_adam_from_sums(self, sums, lr, betas, eps, t, max_norm):
         ws = self.ws
@@ -113,7 +141,7 @@ class ShardedTrainer:
     """Trainer.step contract over latent shards (the whole job is one crosscoder with
     cfg["dict_size"] latents; this rank trains its slice)."""
 
-    def __init__(self, cfg, buffer, group=None, crosscoder=None):
+    def __init__(self, cfg, buffer, group=None, crosscoder=None, recon_chunks=None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -126,7 +154,8 @@ class ShardedTrainer:
             crosscoder = CrossCoder(local)
         self.crosscoder = crosscoder
         self.buffer = buffer
-        self.backend = HipShardBackend(crosscoder)
+        chunks = recon_chunks if recon_chunks is not None else cfg.get("recon_chunks", 4)
+        self.backend = HipShardBackend(crosscoder, recon_chunks=chunks)
         self.engine = ShardedStep(self.backend, group)
         self.total_steps = cfg["num_tokens"] // cfg["batch_size"]
         self.step_counter = 0
@@ -150,8 +179,13 @@ class ShardedTrainer:
         scalars = self.engine.step(raw, factor, l1c, self.lr, (self.cfg["beta1"], self.cfg["beta2"]), 1e-8, self.t)
         self.lr = self.cfg["lr"] * self.lr_lambda(self.t)
         s = scalars[:6].tolist()
-        d = {"loss": s[0] + l1c * s[1], "l2_loss": s[0], "l1_loss": s[1], "l0_loss": s[2], "l1_coeff": l1c,
-             "lr": self.lr, "explained_variance": s[3], "explained_variance_A": s[4], "explained_variance_B": s[5]}
+        # the reference's l1 / EV_A / EV_B are param-dtype tensors (crosscoder.py:115-126): same rounding as Trainer.step
+        dt = self.crosscoder.dtype
+        rd = (lambda v: float(torch.tensor(v, dtype=dt))) if dt != torch.float32 else float
+        l1 = rd(s[1])
+        d = {"loss": s[0] + l1c * l1, "l2_loss": s[0], "l1_loss": l1, "l0_loss": s[2], "l1_coeff": l1c,
+             "lr": self.lr, "explained_variance": s[3], "explained_variance_A": rd(s[4]),
+             "explained_variance_B": rd(s[5])}
         self.step_counter += 1
         return d
 

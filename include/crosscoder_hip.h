@@ -110,6 +110,12 @@ int cc_decode_fwd(const void* acts, const void* W_dec, const void* b_dec, float*
 int cc_loss_fwd_bwd(const float* recon_f32, const void* b_dec, const void* x, const float* x_mean,
                     void* g_recon, float* row_part, float* col_part, float grad_scale, int64_t B, int64_t n,
                     int64_t d, int dtype, void* stream);
+/* cc_loss_fwd_bwd over the batch rows [row0, row0 + rows) only (row0 % 32 == 0, row0 + rows <= B).
+ * The slabs keep the whole-batch layout, so disjoint row ranges may be separate calls: the
+ * latent-sharded step processes each batch slice as soon as its all-reduce has landed. */
+int cc_loss_fwd_bwd_rows(const float* recon_f32, const void* b_dec, const void* x, const float* x_mean,
+                         void* g_recon, float* row_part, float* col_part, float grad_scale, int64_t row0,
+                         int64_t rows, int64_t B, int64_t n, int64_t d, int dtype, void* stream);
 
 /* Loss reduction (crosscoder.py:106-128, trainer.py:51-61): per-row explained variances
  * ev/ev_a/ev_b [B] (fp32) and scalars[0:8] = {l2, l1, l0, mean ev, mean ev_a, mean ev_b, 0, 0};

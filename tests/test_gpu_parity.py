@@ -398,3 +398,77 @@ def test_full_size_step_deterministic(gpu, full_size_case):
     assert outs[0][0] == outs[1][0] and outs[0][1] == outs[1][1]
     assert torch.equal(outs[0][2], outs[1][2])
     assert outs[0][1]["l2_loss"] < outs[0][0]["l2_loss"]
+
+
+# ----------------------------------------------------------------------------- batch slices / sharded
+@pytest.mark.parametrize("B", [1024, 1000])
+def test_sliced_loss_and_dacts_match_whole_batch(gpu, B):
+    """The sharded step's per-slice loss rows + d_acts (run as each slice's all-reduce lands)
+    reproduce the whole-batch launches bit for bit (same per-row math, same slab layout)."""
+    n, d, h = 2, 256, 1024
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16", seed=3,
+               device=str(gpu))
+    cc = ca.CrossCoder(cfg, n_models=n)
+    g = torch.Generator().manual_seed(9)
+    raw = (torch.randn(B, n, d, generator=g) * 3).to(gpu)
+    factor = torch.tensor([0.7, 1.3]).to(torch.bfloat16).to(gpu)
+    ws = cc._workspace(B)
+    a = cc.arena()
+    outs = []
+    for sliced in (False, True):
+        G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+        if sliced:
+            engine.forward(ws, a, raw, factor, loss=False)
+            chunks = engine.row_chunks(B, 4)
+            assert len(chunks) == 4 and chunks[-1][1] == B
+            for r0, r1 in chunks:
+                engine.loss_rows(ws, a, r0, r1)
+                engine.dacts_rows(ws, a, 2.0, r0, r1)
+            engine.loss_finalize(ws)
+            engine.backward(ws, a, G, 2.0, dacts_done=True)
+        else:
+            engine.forward(ws, a, raw, factor)
+            engine.backward(ws, a, G, 2.0)
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in (ws.g_recon, ws.g_pre, ws.row_part, ws.loss_colpart, ws.scalars[:6],
+                                         G.data, ws.sq)])
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+
+
+def test_sharded_trainer_world1_matches_trainer(gpu):
+    """ShardedTrainer over a 1-rank RCCL group (the sliced async all-reduce path, 4 slices) takes
+    the same steps as the single-GPU Trainer."""
+    import os
+
+    import torch.distributed as dist
+    from crosscoder_amd import sharded
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(29600 + os.getpid() % 1000))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
+    try:
+        B, n, d, h = 1024, 2, 256, 2048
+        cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+                   num_tokens=B * 20, device=str(gpu))
+        dicts = []
+        for which in ("single", "sharded"):
+            buf = ca.SyntheticBuffer(cfg, rows=B * 3, seed=1)
+            if which == "single":
+                tr = ca.Trainer(cfg, buffer=buf, crosscoder=ca.CrossCoder(cfg))
+            else:
+                tr = sharded.ShardedTrainer(cfg, buffer=buf, recon_chunks=4)
+            dicts.append([tr.step() for _ in range(3)])
+            torch.cuda.synchronize()
+            if which == "single":
+                p_single = tr.crosscoder.arena().data.float().cpu()
+            else:
+                p_sharded = tr.crosscoder.arena().data.float().cpu()
+        for a, b in zip(*dicts):
+            for k in ("l2_loss", "l1_loss", "l0_loss", "explained_variance"):
+                assert math.isclose(a[k], b[k], rel_tol=1e-3, abs_tol=1e-3), (k, a[k], b[k])
+            assert a["lr"] == b["lr"] and a["l1_coeff"] == b["l1_coeff"]
+        # clip sums are combined in a different order (torch sums vs the clip kernel): <= 1 bf16 ulp of drift
+        assert (p_single - p_sharded).abs().max().item() <= 4 * 5e-5 + 1e-3 * p_single.abs().max().item()
+    finally:
+        dist.destroy_process_group()

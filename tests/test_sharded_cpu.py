@@ -30,6 +30,18 @@ class CpuShardBackend:
         self.recon = self.partial.detach().clone().contiguous()
         return self.recon
 
+    def row_chunks(self):
+        return [(0, B // 2), (B // 2, B)]  # two slices: exercises the sliced all-reduce path
+
+    def rows_ready(self, r0, r1, l1c):
+        pass  # the torch backend does all loss / backward work in loss_finalize / backward
+
+    def reduce_buffer(self):
+        return torch.zeros(6)
+
+    def loss_finalize(self):
+        return self.loss_from_full_recon()
+
     def loss_from_full_recon(self):
         self.R = self.recon.clone().requires_grad_(True)
         full = self.R + self.P["b_dec"]

@@ -15,8 +15,9 @@ NUMEL = 2 * 16384 * 4608 + 16384 + 4608
 def load(path):
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
-        f = getattr(lib, name)
-        f.restype, f.argtypes = res, args
+        f = getattr(lib, name, None)  # (an older build may lack newer entry points)
+        if f is not None:
+            f.restype, f.argtypes = res, args
     return lib
 
 

@@ -18,8 +18,9 @@ PEAK = 256 * 2.4e9 * 4096 / 1e12
 def load(path):
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
-        f = getattr(lib, name)
-        f.restype, f.argtypes = res, args
+        f = getattr(lib, name, None)  # (an older build may lack newer entry points)
+        if f is not None:
+            f.restype, f.argtypes = res, args
     return lib
 
 
