@@ -55,7 +55,8 @@ struct GemmArgs {
   float scale0;
   int flag;             // apply_relu
   int d_model, n_models;
-  void* dbg;            // diagnostic stamp buffer (CC_STAMPS builds only)
+  void* dbg;            // diagnostic stamp buffer (CC_STAMPS / CC_PP_STAMPS builds only)
+  int stamp_base;       // first record of this GEMM in dbg (CC_PP_STAMPS)
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -645,7 +646,7 @@ static int pick_bn(int64_t N, bool akc, bool bkc, int dtype) {
 }
 static int64_t n_blocks(int64_t M, int64_t N, int bn) { return ((M + BM - 1) / BM) * ((N + bn - 1) / bn); }
 
-#ifdef CC_STAMPS
+#if defined(CC_STAMPS) || defined(CC_PP_STAMPS)
 static void* g_stamp_buf = nullptr;
 extern "C" void cc_debug_set_stamp_buffer(void* p) { g_stamp_buf = p; }
 #endif
@@ -665,6 +666,9 @@ static int launch(GemmArgs a, hipStream_t st) {
 
 template <bool AKC, bool BKC, int EPI>
 static int launch_pp(GemmArgs a, hipStream_t st) {
+#ifdef CC_PP_STAMPS
+  a.dbg = g_stamp_buf;
+#endif
   a.nbm = (a.M + BM - 1) / BM;
   a.nbn = (a.N + 255) / 256;
   hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI>), dim3(a.nbm * a.nbn), dim3(NTHR), 0, st, a);
@@ -839,6 +843,10 @@ int cc_wgrad_both(const void* acts, const void* g_recon, const void* W_dec, cons
   }
   a0.nbm = a1.nbm = (a0.M + BM - 1) / BM;
   a0.nbn = a1.nbn = (a0.N + 255) / 256;
+#ifdef CC_PP_STAMPS
+  a0.dbg = a1.dbg = g_stamp_buf;
+  a1.stamp_base = 4 * a0.nbm * a0.nbn;
+#endif
   hipLaunchKernelGGL((gemm_pp_dual_kernel<false, false, EPI_WGDEC, EPI_WGENC>), dim3(2 * a0.nbm * a0.nbn), dim3(NTHR),
                      0, st, a0, a1);
   CC_LAUNCH_CHECK();

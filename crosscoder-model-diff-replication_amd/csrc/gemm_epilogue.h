@@ -115,21 +115,44 @@ CC_DEV void wgdec_factors(const GemmArgs& args, const FragGeom<BNT>& fg, int m0,
 }
 
 // The element-wise part of EPI_ENC / EPI_DACTS / EPI_WGDEC / EPI_WGENC over one wave's fragments.
+// Per-column epilogue vectors of a wave's TN column groups (b_enc for EPI_ENC, the total decoder
+// norm tn for EPI_ENC / EPI_DACTS), loaded by the caller ahead of the epilogue with no branch
+// around any load (absent vectors read as 0 through out-of-range offsets): one memory latency for
+// all of them, overlapped with whatever the caller waits on next.
+template <int DT, int BNT>
+struct EpiCols {
+  typename V4<DT>::T bias[WaveGeom<BNT>::TN];
+  f32x4 tn[WaveGeom<BNT>::TN];
+  CC_DEV void load(const GemmArgs& args, const FragGeom<BNT>& fg, int n0, bool want_bias) {
+    constexpr int ES = DT == CC_BF16 ? 2 : 4;
+    const __amdgpu_buffer_rsrc_t rbias = vec_rsrc(want_bias ? args.bias : args.A, n0, args.N, ES);
+    const __amdgpu_buffer_rsrc_t rtn = vec_rsrc(args.tn ? (const void*)args.tn : args.A, n0, args.N, 4);
+#pragma unroll
+    for (int j = 0; j < WaveGeom<BNT>::TN; ++j) {
+      const uint32_t cvo = (uint32_t)(fg.c0 + 16 * j);
+      bias[j] = bld4<DT>(rbias, want_bias ? cvo * ES : OOB);
+      tn[j] = bld4<CC_F32>(rtn, args.tn ? cvo * 4 : OOB);
+    }
+  }
+};
+template <int DT, int EPI, int BNT>
+CC_DEV void load_epi_cols(EpiCols<DT, BNT>& c, const GemmArgs& args, const FragGeom<BNT>& fg, int n0) {
+  if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) c.load(args, fg, n0, EPI == EPI_ENC && args.bias);
+}
+
+// cols: EpiCols loaded by the caller (EPI_ENC / EPI_DACTS; otherwise unread).
 // cw: dW_dec L1-term factors loaded by the caller (wgdec_factors; EPI_WGDEC with l1_scale != 0
 // only, otherwise unread).  Passed by reference so they stay in registers.
 template <int DT, int EPI, int BNT, class IO>
 CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN],
                           const FragGeom<BNT>& fg, const IO& io, int tm, int m0, int n0, int wr, int lane,
-                          int wave_slot, const float (&cw)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN]) {
+                          int wave_slot, const EpiCols<DT, BNT>& cols,
+                          const float (&cw)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN]) {
   using E = Elem<DT>;
   using WG = WaveGeom<BNT>;
-  constexpr int ES = DT == CC_BF16 ? 2 : 4;
   const int N = args.N;
   if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
     constexpr int JB = EPB<DT, BNT>::JB_M;
-    const bool has_bias = EPI == EPI_ENC && args.bias;
-    const __amdgpu_buffer_rsrc_t rbias = vec_rsrc(has_bias ? args.bias : args.A, n0, N, ES);
-    const __amdgpu_buffer_rsrc_t rtn = vec_rsrc(args.tn ? (const void*)args.tn : args.A, n0, N, 4);
     float s_l1 = 0.f, s_l0 = 0.f;
     typename V4<DT>::T mraw[EPI == EPI_DACTS ? WG::TM : 1][JB];
 #pragma unroll
@@ -142,23 +165,16 @@ CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
             for (int i = 0; i < WG::TM; ++i) mraw[i][jj] = io.in4(i, j + jj);
         }
       }
-      float add[4] = {0.f, 0.f, 0.f, 0.f}, tnc[4] = {0.f, 0.f, 0.f, 0.f}, csum[4] = {0.f, 0.f, 0.f, 0.f};
-      const uint32_t cvo = (uint32_t)(fg.c0 + 16 * j);
-      if constexpr (EPI == EPI_ENC) {
-        if (has_bias) {
-          const auto b = bld4<DT>(rbias, cvo * ES);
+      float add[4], tnc[4], csum[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) add[e] = V4<DT>::get(b, e);
+      for (int e = 0; e < 4; ++e) {
+        if constexpr (EPI == EPI_ENC) {
+          add[e] = V4<DT>::get(cols.bias[j], e);
+          tnc[e] = cols.tn[j][e];
+        } else {
+          add[e] = cols.tn[j][e] * args.scale0;
+          tnc[e] = 0.f;
         }
-        if (args.tn) {
-          const auto t = bld4<CC_F32>(rtn, cvo * 4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) tnc[e] = t[e];
-        }
-      } else if (args.tn) {
-        const auto t = bld4<CC_F32>(rtn, cvo * 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) add[e] = t[e] * args.scale0;
       }
 #pragma unroll
       for (int i = 0; i < WG::TM; ++i) {
@@ -226,7 +242,11 @@ CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e];
         if constexpr (EPI == EPI_WGDEC) {
+#ifndef CC_EXP_EPI_NOMATH  // timing-only experiment build (never shipped): input loaded, term not added
           if (l1term) {
+#else
+          if (l1term && lane > 64) {
+#endif
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] += cw[i][j] * V4<DT>::get(wraw[i][j % JB], e);
           }
@@ -286,6 +306,8 @@ CC_DEV void gemm_epilogue(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
     if constexpr (EPI == EPI_WGDEC) {
       if (args.scale0 != 0.f) wgdec_factors<BNT>(args, fg, m0, n0, cw);
     }
-    epilogue_core<DT, EPI, BNT>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, cw);
+    EpiCols<DT, BNT> cols;
+    load_epi_cols<DT, EPI, BNT>(cols, args, fg, n0);
+    epilogue_core<DT, EPI, BNT>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, cols, cw);
   }
 }

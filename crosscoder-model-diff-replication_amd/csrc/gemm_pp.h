@@ -28,6 +28,12 @@
 // 32-lane group reads 8 k rows x 32 B = all 64 banks once) and full 128-B lines per DMA row.
 // KC operands keep [256 rows][128 B] with chunk ^ (row & 7).
 
+#include <type_traits>
+
+#ifndef CC_PP_ORDER
+#define CC_PP_ORDER 1
+#endif
+
 CC_DEV int pp_h(int k) { return ((k >> 1) & 1) | ((k >> 2) & 2); }
 
 // Per-lane source offset (bytes, step k0 = 0) of DMA ci (0..31) of a 256 x 64 operand tile, or
@@ -77,67 +83,85 @@ CC_DEV bf16x8 pp_frag_mn(const char* tile, int r0, int kk, int off) {
 }
 
 // ---- LDS-staged epilogue (bf16 output tiles, N % 8 == 0) ----
-// Tile image [256 rows][512 B] (all 128 KB of LDS once the main loop has drained), phys 16-B
-// chunk = chunk ^ (row & 15): a fragment access (per 32-lane group 16 rows x one chunk) hits 16
-// distinct bank groups.  The image moves between HBM and LDS in whole 512-B rows (1 KB = 2 rows
-// per wave instruction, 16 B per lane), so every HBM line of the epilogue's input (activation
-// mask / W_dec) and output is transferred once and whole -- the fragment-shaped 8-byte accesses
-// of the register path fetch up to 4x the bytes (PMC FETCH_SIZE).
+// Tile image: 4 quarters of [64 rows][512 B] (32 KB each, quarter Q = tile rows 64Q..64Q+63 at LDS
+// offset qb[Q]), phys 16-B chunk = chunk ^ (row & 15): a fragment access (per 32-lane group 16
+// rows x one chunk) hits 16 distinct bank groups.  The image moves between HBM and LDS in whole
+// 512-B rows (1 KB piece ci = tile rows 2ci, 2ci+1 = 2 rows per wave instruction, 16 B per lane),
+// so every HBM line of the epilogue's input (activation mask / W_dec) and output is transferred
+// once and whole -- the fragment-shaped 8-byte accesses of the register path fetch up to 4x the
+// bytes (PMC FETCH_SIZE).  Normally qb = {0, 32K, 64K, 96K}; dW_dec's W_dec tile is instead
+// prefetched into LDS regions the K loop frees before it ends (pp_tile).
 struct LdsIO {
-  char* smem;
-  int off[4];  // lane byte offset of fragment (0, j); fragment i adds 16 rows
-  CC_DEV LdsIO(char* s, int wr, int wc, int lane) : smem(s) {
-    const int r = wr * 128 + (lane & 15);
+  char* lo;    // quarter of fragments i = 0..3 (rows wr*128 + 0..63)
+  char* hi;    // quarter of fragments i = 4..7
+  int off[4];  // lane byte offset of fragment (i & 3 = 0, j) within its quarter
+  CC_DEV LdsIO(char* s, const int (&qb)[4], int wr, int wc, int lane)
+      : lo(s + (wr ? qb[2] : qb[0])), hi(s + (wr ? qb[3] : qb[1])) {  // (no runtime array index: scratch)
+    const int r = lane & 15;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int col = wc * 64 + 4 * (lane >> 4) + 16 * j;
-      off[j] = r * 512 + (((col >> 3) ^ (lane & 15)) << 4) + (col & 4) * 2;
+      off[j] = r * 512 + (((col >> 3) ^ r) << 4) + (col & 4) * 2;
     }
   }
-  CC_DEV bf16x4 in4(int i, int j) const { return *(const bf16x4*)(smem + off[j] + i * 16 * 512); }
-  CC_DEV void out4(int i, int j, const float v[4]) const {
-    *(bf16x4*)(smem + off[j] + i * 16 * 512) = pack4<CC_BF16>(v);
-  }
+  CC_DEV char* at(int i, int j) const { return (i < 4 ? lo : hi) + off[j] + (i & 3) * 16 * 512; }
+  CC_DEV bf16x4 in4(int i, int j) const { return *(const bf16x4*)at(i, j); }
+  CC_DEV void out4(int i, int j, const float v[4]) const { *(bf16x4*)at(i, j) = pack4<CC_BF16>(v); }
 };
 
+// Source/destination offset (bytes, in a tile-anchored descriptor) of this lane's 16 B of 1-KB
+// image piece ci (tile rows 2ci, 2ci+1), or OOB past the matrix edge.
+CC_DEV uint32_t piece_off(int ci, int lane, int rows, int cols, int ldo) {
+  const int row = 2 * ci + (lane >> 5);
+  const int c = (lane & 31) ^ (row & 15);
+  return (row < rows && 8 * c < cols) ? (uint32_t)((row * ldo + 8 * c) * 2) : OOB;
+}
+
 template <int EPI>
-CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char* smem, int tm, int m0, int n0,
-                            int wr, int wc, int lane, int wave, int wave_slot) {
-  const FragGeom<256> fg(args, m0, n0, wr, wc, lane);
+CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char* smem, const int (&qb)[4],
+                            bool input_staged, int tm, int m0, int n0, int wr, int wc, int lane, int wave,
+                            int wave_slot, const FragGeom<256>& fg, const EpiCols<CC_BF16, 256>& ecols) {
   const int rows = args.M - m0, cols = args.N - n0, ldo = (int)args.ldo;
-  // source/destination offset of this lane's 16 B of 1-KB piece ci (tile rows 2ci, 2ci+1)
-  auto xoff = [&](int ci) -> uint32_t {
-    const int row = 2 * ci + (lane >> 5);
-    const int c = (lane & 31) ^ (row & 15);
-    return (row < rows && 8 * c < cols) ? (uint32_t)((row * ldo + 8 * c) * 2) : OOB;
-  };
   const void* in = EPI == EPI_DACTS ? args.mask_src : (EPI == EPI_WGDEC && args.scale0 != 0.f ? args.w_src : nullptr);
   float cw[8][4];  // dW_dec L1-term factors (EPI_WGDEC only)
   if (in) {
-    const __amdgpu_buffer_rsrc_t rin = tile_rsrc(in, args.ldo, m0, n0, args.M, args.N, 2);
+    if (!input_staged) {
+      const __amdgpu_buffer_rsrc_t rin = tile_rsrc(in, args.ldo, m0, n0, args.M, args.N, 2);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int ci = q * 8 + wave;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_void*)(smem + ci * 1024), 16, (int)xoff(ci), 0, 0, 0);
+      for (int q = 0; q < 16; ++q) {
+        const int ci = q * 8 + wave;
+#ifdef CC_EXP_EPI_NOLOAD  // timing-only experiment build (never shipped): no epilogue input transfer
+        if (EPI != EPI_WGDEC)
+#endif
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_void*)(smem + qb[q >> 2] + (ci & 31) * 1024), 16,
+                                                 (int)piece_off(ci, lane, rows, cols, ldo), 0, 0, 0);
+      }
     }
     // the L1-term factors' loads fly with the tile DMA (one latency for both)
     if constexpr (EPI == EPI_WGDEC) wgdec_factors<256>(args, fg, m0, n0, cw);
     wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
   }
-  const LdsIO io(smem, wr, wc, lane);
-  epilogue_core<CC_BF16, EPI, 256>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, cw);
+  const LdsIO io(smem, qb, wr, wc, lane);
+  epilogue_core<CC_BF16, EPI, 256>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, ecols, cw);
   __syncthreads();
   const __amdgpu_buffer_rsrc_t rout = tile_rsrc(args.out, args.ldo, m0, n0, args.M, args.N, 2);
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int ci = q * 8 + wave;
-    const bf16x8 v = *(const bf16x8*)(smem + ci * 1024 + lane * 16);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, (int)xoff(ci), 0, 0);
+    const bf16x8 v = *(const bf16x8*)(smem + qb[q >> 2] + (ci & 31) * 1024 + lane * 16);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout,
+                                           (int)piece_off(ci, lane, rows, cols, ldo), 0, 0);
   }
 }
 
 constexpr int PP_LDS = 4 * 256 * 128;  // 2 buffers x (A | B) K-step images
+// + one 32 KB quarter of the W_dec tile, prefetched at tile start (dW_dec kernels: 160 KB in all)
+#ifndef CC_PP_NO_WPF
+constexpr int PP_LDS_W = PP_LDS + 256 * 128;
+#else
+constexpr int PP_LDS_W = PP_LDS;
+#endif
 
 // One output tile of one GEMM; bid = the tile's block index within that GEMM's grid.
 template <bool AKC, bool BKC, int EPI>
@@ -186,11 +210,43 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
   const int kA = pp_dma_k<AKC>(wave, lane), kB = pp_dma_k<BKC>(wave, lane);
   const int nk = (K + 63) / 64;
 
+  // dW_dec's epilogue input (the W_dec tile, 128 KB) is prefetched instead of loaded after the
+  // loop: quarter 3 at tile start into the extra 32 KB of LDS, quarters 0-2 by the DMA slots of
+  // the steps past the end (T >= nk), which would otherwise zero-fill regions the loop no longer
+  // reads (buffer nk&1's B and A images, buffer (nk+1)&1's B image).
+#ifndef CC_PP_NO_WPF
+  const bool pf = EPI == EPI_WGDEC && args.scale0 != 0.f;
+#else  // experiment build: W_dec tile loaded after the loop (no prefetch, 128 KB LDS)
+  const bool pf = false;
+#endif
+  const int erows = M - m0, ecols = N - n0, eldo = (int)args.ldo;
+  __amdgpu_buffer_rsrc_t rw = ra;
+  int qb[4] = {0, TILE, 2 * TILE, 3 * TILE};
+  if (pf) {
+    rw = tile_rsrc(args.w_src, args.ldo, m0, n0, M, N, 2);
+    qb[0] = (nk & 1) * BUF + TILE;
+    qb[1] = (nk & 1) * BUF;
+    qb[2] = ((nk + 1) & 1) * BUF + TILE;
+    qb[3] = 2 * BUF;
+  }
+
   // issue phase p's DMAs for step T (target buffer T & 1)
-  auto issue = [&](int p, int T) {
+  // TAIL: the step may lie past the end (prologue and the last two K steps only: the steady-state
+  // loop stays free of the branch)
+  auto issue_t = [&](auto tail, int p, int T) {
     const bool isA = p < 2;
     const int k0 = T * 64;
     char* dst = smem + (T & 1) * BUF + (isA ? 0 : TILE);
+    if (decltype(tail)::value && pf && T >= nk) {  // W_dec quarter 0 (B, T = nk), 1 (A, T = nk) or 2 (B, T = nk + 1)
+      const int quarter = isA ? 1 : (T == nk ? 0 : 2);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int ci = pp_ci(p, q, wave);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void*)(dst + ci * 1024), 16,
+                                                 (int)piece_off(32 * quarter + ci, lane, erows, ecols, eldo), 0, 0, 0);
+      }
+      return;
+    }
     const int64_t ld = isA ? args.lda : args.ldb;
     const bool kc = isA ? AKC : BKC;
     const uint32_t kadd = (uint32_t)(kc ? (int64_t)k0 * 2 : (int64_t)k0 * ld * 2);
@@ -207,6 +263,7 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
                                                (int)off, 0, 0, 0);
     }
   };
+  auto issue = [&](int p, int T) { issue_t(std::true_type{}, p, T); };
 
   // fragment lane offsets
   int kc_off[2], mn_off[4];
@@ -226,7 +283,16 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
 #pragma unroll
     for (int j = 0; j < WG::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: the DMAs steady state would have issued in steps -2 and -1
+  // prologue: W_dec quarter 3 (retired with the first operand DMAs), then the DMAs steady state
+  // would have issued in steps -2 and -1
+  if (pf) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ci = q * 8 + wave;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void*)(smem + qb[3] + ci * 1024), 16,
+                                               (int)piece_off(96 + ci, lane, erows, ecols, eldo), 0, 0, 0);
+    }
+  }
   issue(2, 0);
   issue(3, 0);
   issue(0, 0);
@@ -238,12 +304,14 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
   if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs half a phase behind
 
   bf16x8 bfr[WG::TN][2];
-  for (int t = 0; t < nk; ++t) {
+  auto kstep = [&](auto tail, int t) {
     const char* la = smem + (t & 1) * BUF;
     const char* lb = la + TILE;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       __builtin_amdgcn_sched_barrier(0);
+#if CC_PP_ORDER == 0
+      // phase p: A tiles 2p, 2p+1 x both k-slices; all B fragments read in phase 0
       if (p == 0) {
 #pragma unroll
         for (int j = 0; j < WG::TN; ++j) {
@@ -261,9 +329,33 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
         for (int kk = 0; kk < 2; ++kk)
           afr[ii][kk] = AKC ? pp_frag_kc(la, r0, kc_off[kk]) : pp_frag_mn(la, r0, kk, mn_off[(r0 >> 4) & 3]);
       }
-      issue(p, p < 2 ? t + 1 : t + 2);
+#else
+      // phase p: A tiles 4*(p>>1) .. +3 x k-slice p&1; the B fragments of k-slice p&1 are read in
+      // phase p&1 (B read load per phase 8/8/0/0 fragments instead of 16/0/0/0).  Every output
+      // still accumulates k-slice 0 before k-slice 1 of a step (bitwise the same sums).
+      const int kk = p & 1, ib = (p >> 1) * 4;
+      if (p < 2) {
+#pragma unroll
+        for (int j = 0; j < WG::TN; ++j) {
+          const int c0 = wc * WG::WTN + 16 * j;
+          bfr[j][kk] = BKC ? pp_frag_kc(lb, c0, kc_off[kk]) : pp_frag_mn(lb, c0, kk, mn_off[(c0 >> 4) & 3]);
+        }
+      }
+      bf16x8 afr[4];
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int r0 = wr * WG::WTM + 16 * (ib + ii);
+        afr[ii] = AKC ? pp_frag_kc(la, r0, kc_off[kk]) : pp_frag_mn(la, r0, kk, mn_off[(r0 >> 4) & 3]);
+      }
+#endif
+      issue_t(tail, p, p < 2 ? t + 1 : t + 2);
 #ifndef CC_PP_EXP_NOWAIT  // timing-only experiment builds (never shipped): skip the DMA wait
       wait_vmcnt<6>();
+#endif
+#if CC_PP_ORDER != 0
+      // the B region of this buffer is re-staged in phase 2 (one phase after these reads): retire
+      // them before this phase's first barrier (WAR across the staggered wave groups)
+      if (p == 1) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
 #endif
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
@@ -271,6 +363,7 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
 #if CC_PP_PRIO
       __builtin_amdgcn_s_setprio(1);
 #endif
+#if CC_PP_ORDER == 0
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -279,28 +372,65 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
           for (int j = 0; j < WG::TN; ++j)
             acc[2 * p + ii][j] =
                 __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii][kk], acc[2 * p + ii][j], 0, 0, 0);
+#else
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int j = 0; j < WG::TN; ++j)
+          acc[ib + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii], acc[ib + ii][j], 0, 0, 0);
+#endif
 #if CC_PP_PRIO
       __builtin_amdgcn_s_setprio(0);
 #endif
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
     }
-  }
+  };
+  int t = 0;
+  for (; t < nk - 2; ++t) kstep(std::false_type{}, t);  // steady state: every DMA is an operand DMA
+  for (; t < nk; ++t) kstep(std::true_type{}, t);       // last two steps: DMAs past the end prefetch W_dec
   if (wr == 0) __builtin_amdgcn_s_barrier();
+  // the epilogue's column vectors fly while the last (zero-fill) DMAs drain
+  const FragGeom<256> fg(args, m0, n0, wr, wc, lane);
+  EpiCols<CC_BF16, 256> cols;
+  if constexpr (EPI != EPI_F32 && EPI != EPI_DEC) load_epi_cols<CC_BF16, EPI, 256>(cols, args, fg, n0);
   wait_vmcnt<0>();
+#ifdef CC_PP_STAMPS  // diagnostic build only: per-block wall-clock timeline (100 MHz counter)
+  if (threadIdx.x == 0 && args.dbg) ((uint64_t*)args.dbg)[(int64_t)args.stamp_base + bid * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
 
   if constexpr (EPI == EPI_F32 || EPI == EPI_DEC) {
     gemm_epilogue<CC_BF16, EPI, 256>(args, acc, tm, m0, n0, wr, wc, lane, bid * 8 + wave);
   } else {  // (the host routes N % 8 != 0 to gemm_kernel)
     __builtin_amdgcn_s_barrier();  // every wave's zero-fill DMAs landed: the LDS is free
-    pp_epilogue_lds<EPI>(args, acc, smem, tm, m0, n0, wr, wc, lane, wave, bid * 8 + wave);
+    pp_epilogue_lds<EPI>(args, acc, smem, qb, pf, tm, m0, n0, wr, wc, lane, wave, bid * 8 + wave, fg, cols);
   }
 }
 
+#ifdef CC_PP_STAMPS
+// block record [start, main-loop end, end, hw id | xcc id << 32] at stamp_base + 4 * bid
+CC_DEV uint64_t pp_stamp_start() { return __builtin_amdgcn_s_memrealtime(); }
+CC_DEV void pp_stamp_end(const GemmArgs& a, int bid, uint64_t t0) {
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0 && a.dbg) {
+    uint64_t* o = (uint64_t*)a.dbg + a.stamp_base + (int64_t)bid * 4;
+    o[0] = t0;
+    o[2] = t1;
+    o[3] = (uint64_t)__builtin_amdgcn_s_getreg(0xF804) | ((uint64_t)__builtin_amdgcn_s_getreg(0xF814) << 32);
+  }
+}
+#endif
+
 template <bool AKC, bool BKC, int EPI>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
-  __shared__ __attribute__((aligned(16))) char smem[PP_LDS];
+  __shared__ __attribute__((aligned(16))) char smem[EPI == EPI_WGDEC ? PP_LDS_W : PP_LDS];
+#ifdef CC_PP_STAMPS
+  const uint64_t t0 = pp_stamp_start();
+#endif
   pp_tile<AKC, BKC, EPI>(args, smem, blockIdx.x);
+#ifdef CC_PP_STAMPS
+  pp_stamp_end(args, blockIdx.x, t0);
+#endif
 }
 
 // Two independent GEMMs of one layout in one launch: blocks [0, nb0) are a0's tiles, the rest
@@ -308,8 +438,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
 // 2304 tiles = 9 full waves, and one kernel boundary disappears.
 template <bool AKC, bool BKC, int EPI0, int EPI1>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_kernel(const GemmArgs a0, const GemmArgs a1) {
-  __shared__ __attribute__((aligned(16))) char smem[PP_LDS];
+  __shared__ __attribute__((aligned(16))) char smem[EPI0 == EPI_WGDEC || EPI1 == EPI_WGDEC ? PP_LDS_W : PP_LDS];
   const int nb0 = a0.nbm * a0.nbn;
+#ifdef CC_PP_STAMPS
+  const uint64_t t0 = pp_stamp_start();
+#endif
   if ((int)blockIdx.x < nb0) pp_tile<AKC, BKC, EPI0>(a0, smem, blockIdx.x);
   else pp_tile<AKC, BKC, EPI1>(a1, smem, blockIdx.x - nb0);
+#ifdef CC_PP_STAMPS
+  if ((int)blockIdx.x < nb0) pp_stamp_end(a0, blockIdx.x, t0);
+  else pp_stamp_end(a1, blockIdx.x - nb0, t0);
+#endif
 }
