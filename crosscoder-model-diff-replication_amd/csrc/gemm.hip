@@ -32,7 +32,7 @@ constexpr int BM = 256, NTHR = 512;
 constexpr uint32_t OOB = 0x7ffffff0u;  // voffset that the range check always rejects
 constexpr uint32_t MAX_RECORDS = 0x7fffffe0u;
 
-enum Epi { EPI_F32 = 0, EPI_ENC = 1, EPI_DEC = 2, EPI_DACTS = 3, EPI_WGDEC = 4, EPI_WGENC = 5 };
+enum Epi { EPI_F32 = 0, EPI_ENC = 1, EPI_DEC = 2, EPI_DACTS = 3, EPI_WGDEC = 4, EPI_WGENC = 5, EPI_SPLIT = 6 };
 
 struct GemmArgs {
   const void* A;
@@ -57,6 +57,7 @@ struct GemmArgs {
   int d_model, n_models;
   void* dbg;            // diagnostic stamp buffer (CC_STAMPS / CC_PP_STAMPS builds only)
   int stamp_base;       // first record of this GEMM in dbg (CC_PP_STAMPS)
+  int k_step0, k_steps; // ping-pong split-K: contraction steps [k_step0, k_step0 + k_steps) (0 steps: all)
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -647,6 +648,7 @@ static int pick_bn(int64_t N, bool akc, bool bkc, int dtype) {
 static int64_t n_blocks(int64_t M, int64_t N, int bn) { return ((M + BM - 1) / BM) * ((N + bn - 1) / bn); }
 
 #if defined(CC_STAMPS) || defined(CC_PP_STAMPS)
+static bool g_split_stamps_only = true;  // decode_fwd_ws: stamp the split pass, not the main launch
 static void* g_stamp_buf = nullptr;
 extern "C" void cc_debug_set_stamp_buffer(void* p) { g_stamp_buf = p; }
 #endif
@@ -765,6 +767,112 @@ int cc_decode_fwd(const void* acts, const void* W_dec, const void* b_dec, float*
   int rc = check_gemm(a, dtype, true, false);
   if (rc) return rc;
   return launch_dt<EPI_DEC, true, false>(dtype, a, (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+// ---- G2 with the leftover tiles split over K (bf16, fp32 output, no bias) ----
+// 256-tile waves: the tiles of the first `nbn_main` column blocks fill whole waves (ping-pong
+// kernel, full contraction); the remaining column blocks' tiles (a partial wave, e.g. 32 of 288
+// at 4096 x 4608) run as S-way split-K passes (S * tiles <= 256 blocks, one wave of 1/S length)
+// whose fp32 partials a fixed-order reduce sums: deterministic, and ~1/S of a wave instead of a
+// whole one.
+struct DecPlan {
+  int nbn_main;   // column blocks (of 256) in the whole-wave launch
+  int tail_cols;  // columns handled by the split passes
+  int nsplit, steps_per, nk;
+};
+static bool dec_plan(int64_t B, int64_t h, int64_t K, int dtype, DecPlan& p) {
+  p = DecPlan{};
+  if (dtype != CC_BF16 || K % 8 || h % 8) return false;
+  const int64_t nbm = (B + BM - 1) / BM, nbn = (K + 255) / 256, tiles = nbm * nbn;
+  const int64_t waves = tiles / 256;
+  if (waves == 0 || tiles % 256 == 0 || (256 * waves) % nbm) return false;
+  p.nbn_main = (int)(256 * waves / nbm);
+  if (p.nbn_main >= nbn) return false;
+  p.tail_cols = (int)(K - (int64_t)p.nbn_main * 256);
+  const int64_t tail_tiles = nbm * (nbn - p.nbn_main);
+  p.nk = (int)((h + 63) / 64);
+  int S = (int)(256 / tail_tiles);
+  if (S < 2) return false;
+  if (S > p.nk) S = p.nk;
+  p.steps_per = (p.nk + S - 1) / S;
+  p.nsplit = (p.nk + p.steps_per - 1) / p.steps_per;
+  return p.nsplit >= 2;
+}
+
+// Sum of the S split-K partial slabs (fixed order) into out[m][n] (ldo): the slabs hold each tile
+// in accumulator-fragment order (EPI_SPLIT: tile, wave, fragment, lane -> 4 floats), so the split
+// passes store whole 1-KB pieces; one thread per (tile, wave, fragment, lane).
+__global__ __launch_bounds__(256) void reduce_splits_kernel(const float* __restrict__ part, int S, int64_t split_stride,
+                                                            int M, int N, int nbm, int nbn, float* __restrict__ out,
+                                                            int64_t ldo) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)nbm * nbn * 8 * 32 * 64) return;
+  const int lane = (int)(t & 63), f = (int)((t >> 6) & 31), wave = (int)((t >> 11) & 7);
+  const int tile = (int)(t >> 14);
+  int tm, tn;
+  tile_of_block(tile, nbm, nbn, tm, tn);
+  const int row = tm * BM + (wave >> 2) * 128 + 16 * (f >> 2) + (lane & 15);
+  const int col = tn * 256 + (wave & 3) * 64 + 16 * (f & 3) + 4 * (lane >> 4);
+  if (row >= M || col >= N) return;
+  f32x4 a = *(const f32x4*)(part + t * 4);
+  for (int q = 1; q < S; ++q) a += *(const f32x4*)(part + q * split_stride + t * 4);
+  *(f32x4*)(out + (int64_t)row * ldo + col) = a;
+}
+
+extern "C" {
+
+// floats of one split's partial slab: whole 256 x 256 tiles of the leftover columns
+static int64_t split_stride_of(int64_t B, const DecPlan& p) {
+  return ((B + BM - 1) / BM) * ((p.tail_cols + 255) / 256) * (int64_t)BM * 256;
+}
+
+int64_t cc_decode_ws_floats(int64_t B, int64_t h, int64_t K, int dtype) {
+  DecPlan p;
+  if (!dec_plan(B, h, K, dtype, p)) return 0;
+  return (int64_t)p.nsplit * split_stride_of(B, p);
+}
+
+int cc_decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, float* ws, int64_t ws_floats, int64_t B,
+                     int64_t h, int64_t K, int dtype, void* stream) {
+  if (!recon_f32) return CC_ERR_NULL;
+  DecPlan p;
+  const bool split = dec_plan(B, h, K, dtype, p);
+  if (!split) return cc_decode_fwd(acts, W_dec, nullptr, recon_f32, nullptr, B, h, K, dtype, stream);
+  if (!ws) return CC_ERR_NULL;
+  const int64_t split_stride = split_stride_of(B, p);
+  if (ws_floats < (int64_t)p.nsplit * split_stride) return CC_ERR_SHAPE;
+  if (((uintptr_t)ws & 15) || ((uintptr_t)recon_f32 & 15)) return CC_ERR_ALIGN;
+  hipStream_t st = (hipStream_t)stream;
+  GemmArgs a = {};
+  a.A = acts; a.lda = h; a.B = W_dec; a.ldb = K;
+  a.M = (int)B; a.N = p.nbn_main * 256; a.K = (int)h;
+  a.out_f32 = recon_f32; a.ldo = K;
+  int rc = check_gemm(a, dtype, true, false);
+  if (rc) return rc;
+#ifdef CC_PP_STAMPS
+  if (g_split_stamps_only) a.dbg = nullptr;
+#endif
+  rc = launch_pp<true, false, EPI_DEC>(a, st);  // whole waves
+  if (rc) return rc;
+  GemmArgs t = {};
+  t.A = acts; t.lda = h; t.B = (const bf16_t*)W_dec + (int64_t)p.nbn_main * 256; t.ldb = K;
+  t.M = (int)B; t.N = p.tail_cols; t.K = (int)h;
+  t.out = ws; t.ldo = p.tail_cols;
+  t.nbm = (t.M + BM - 1) / BM;
+  t.nbn = (t.N + 255) / 256;
+#ifdef CC_PP_STAMPS
+  t.dbg = g_stamp_buf;
+#endif
+  hipLaunchKernelGGL((gemm_pp_splitk_kernel<true, false>), dim3(p.nsplit * t.nbm * t.nbn), dim3(NTHR), 0, st, t,
+                     p.steps_per, p.nk, split_stride);
+  CC_LAUNCH_CHECK();
+  const int64_t threads = (int64_t)t.nbm * t.nbn * 8 * 32 * 64;
+  hipLaunchKernelGGL(reduce_splits_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, ws, p.nsplit,
+                     split_stride, t.M, t.N, t.nbm, t.nbn, recon_f32 + (int64_t)p.nbn_main * 256, (int64_t)K);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
 }
 
 int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,

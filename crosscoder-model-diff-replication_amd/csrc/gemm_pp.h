@@ -208,7 +208,9 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
       vo[p][q] = p < 2 ? pp_dma_off<AKC>(pp_ci(p, q, wave), M - m0, args.lda, lane)
                        : pp_dma_off<BKC>(pp_ci(p, q, wave), N - n0, args.ldb, lane);
   const int kA = pp_dma_k<AKC>(wave, lane), kB = pp_dma_k<BKC>(wave, lane);
-  const int nk = (K + 63) / 64;
+  // this block's contraction steps (split-K passes run a slice of them)
+  const int nk = args.k_steps ? args.k_steps : (K + 63) / 64;
+  const int kb0 = args.k_step0;
 
   // dW_dec's epilogue input (the W_dec tile, 128 KB) is prefetched instead of loaded after the
   // loop: quarter 3 at tile start into the extra 32 KB of LDS, quarters 0-2 by the DMA slots of
@@ -235,7 +237,7 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
   // loop stays free of the branch)
   auto issue_t = [&](auto tail, int p, int T) {
     const bool isA = p < 2;
-    const int k0 = T * 64;
+    const int k0 = (kb0 + T) * 64;
     char* dst = smem + (T & 1) * BUF + (isA ? 0 : TILE);
     if (decltype(tail)::value && pf && T >= nk) {  // W_dec quarter 0 (B, T = nk), 1 (A, T = nk) or 2 (B, T = nk + 1)
       const int quarter = isA ? 1 : (T == nk ? 0 : 2);
@@ -399,7 +401,13 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
   if (threadIdx.x == 0 && args.dbg) ((uint64_t*)args.dbg)[(int64_t)args.stamp_base + bid * 4 + 1] = __builtin_amdgcn_s_memrealtime();
 #endif
 
-  if constexpr (EPI == EPI_F32 || EPI == EPI_DEC) {
+  if constexpr (EPI == EPI_SPLIT) {  // split-K partial: accumulator fragments stored as they are (1 KB each)
+    float* o = (float*)args.out + ((int64_t)bid * 8 + wave) * 32 * 256;
+#pragma unroll
+    for (int i = 0; i < WG::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < WG::TN; ++j) *(f32x4*)(o + ((i * 4 + j) * 64 + lane) * 4) = acc[i][j];
+  } else if constexpr (EPI == EPI_F32 || EPI == EPI_DEC) {
     gemm_epilogue<CC_BF16, EPI, 256>(args, acc, tm, m0, n0, wr, wc, lane, bid * 8 + wave);
   } else {  // (the host routes N % 8 != 0 to gemm_kernel)
     __builtin_amdgcn_s_barrier();  // every wave's zero-fill DMAs landed: the LDS is free
@@ -448,5 +456,31 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_kernel(const GemmArgs a0
 #ifdef CC_PP_STAMPS
   if ((int)blockIdx.x < nb0) pp_stamp_end(a0, blockIdx.x, t0);
   else pp_stamp_end(a1, blockIdx.x - nb0, t0);
+#endif
+}
+
+// Split-K pass (fp32 partial tiles, no epilogue work): block b runs contraction slice
+// s = b / ntiles (steps [s * steps_per, ...)) of tile b % ntiles and stores its fp32 partial tile
+// (accumulator-fragment order, EPI_SPLIT) at out + s * split_stride.  Used for the tiles left over after the whole 256-tile waves of a
+// launch, so the leftover costs ~1/S of a wave instead of a full one; cc_reduce_splits sums them.
+template <bool AKC, bool BKC>
+__global__ __launch_bounds__(NTHR, 1) void gemm_pp_splitk_kernel(const GemmArgs args, int steps_per, int nk_total,
+                                                               int64_t split_stride) {
+  __shared__ __attribute__((aligned(16))) char smem[PP_LDS];
+  // split s = b / ntiles: consecutive blocks share a contraction slice (measured 64 us per block at
+  // config 2, vs 80-134 us with each split pinned to one XCD: s = b % 8)
+  const int s = blockIdx.x / (args.nbm * args.nbn);
+  const int tb = blockIdx.x - s * args.nbm * args.nbn;
+#ifdef CC_PP_STAMPS
+  const uint64_t t0 = pp_stamp_start();
+#endif
+  GemmArgs a = args;
+  a.k_step0 = s * steps_per;
+  a.k_steps = nk_total - a.k_step0 < steps_per ? nk_total - a.k_step0 : steps_per;
+  a.out = (float*)args.out + s * split_stride;
+  a.stamp_base = 4 * s * args.nbm * args.nbn;
+  pp_tile<AKC, BKC, EPI_SPLIT>(a, smem, tb);
+#ifdef CC_PP_STAMPS
+  pp_stamp_end(a, tb, t0);
 #endif
 }

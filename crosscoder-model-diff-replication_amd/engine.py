@@ -94,6 +94,8 @@ class StepWorkspace:
         self.l1_part = E(self.n_wave)
         self.l0_part = E(self.n_wave)
         self.recon = E(B, K)
+        nws = ops.decode_ws_floats(B, h, K, dtype)
+        self.dec_ws = E(nws) if nws else None  # G2 split-K partials
         self.g_recon = E(B, K, dt=dtype)
         self.ncb = ops.loss_col_blocks(d)
         self.row_part = E(2, n * self.ncb, B)
@@ -129,7 +131,7 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
         ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, tn=ws.tn, colsum_part=ws.acts_colpart,
                        l1_part=ws.l1_part, l0_part=ws.l0_part)
     with _span("G2_decode"):
-        ops.decode_fwd(ws.acts, P.W_dec_hk, None, recon_f32=ws.recon)
+        ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
     if loss:
         loss_from_recon(ws, P, grad_scale)
 

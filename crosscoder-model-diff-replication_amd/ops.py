@@ -138,6 +138,18 @@ def decode_fwd(acts, W_dec_hk, b_dec=None, recon_f32=None, recon_t=None):
                               dtype_code(acts.dtype), _stream(acts)))
 
 
+def decode_ws_floats(B, h, K, dtype):
+    return int(lib().cc_decode_ws_floats(B, h, K, dtype_code(dtype)))
+
+
+def decode_partial(acts, W_dec_hk, recon_f32, ws=None):
+    """fp32 acts . W_dec without bias, whole-wave schedule + split-K leftover (cc_decode_fwd_ws)."""
+    B, h = acts.shape
+    K = W_dec_hk.shape[1]
+    check(lib().cc_decode_fwd_ws(_ptr(acts), _ptr(W_dec_hk), _ptr(recon_f32), _ptr(ws),
+                                 0 if ws is None else ws.numel(), B, h, K, dtype_code(acts.dtype), _stream(acts)))
+
+
 def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_scale, B, n, d, row0=0, rows=None):
     """Loss terms + g_recon for batch rows [row0, row0 + rows) (default: all B rows)."""
     rows = B - row0 if rows is None else rows

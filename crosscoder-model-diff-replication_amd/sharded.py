@@ -104,7 +104,7 @@ class HipShardBackend:
             ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, tn=ws.tn, colsum_part=ws.acts_colpart,
                            l1_part=ws.l1_part, l0_part=ws.l0_part)
         with engine._span("G2_decode"):
-            ops.decode_fwd(ws.acts, P.W_dec_hk, None, recon_f32=ws.recon)
+            ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
         return ws.recon
 
     def row_chunks(self):

@@ -103,6 +103,15 @@ int cc_encode_fwd(const void* x, const void* W_enc, const void* b_enc, const flo
 int cc_decode_fwd(const void* acts, const void* W_dec, const void* b_dec, float* recon_f32, void* recon_t,
                   int64_t B, int64_t h, int64_t K, int dtype, void* stream);
 
+/* cc_decode_fwd's fp32 partial reconstruction (no bias), scheduled for whole 256-tile waves: the
+ * column blocks that fill whole waves run in one launch, the leftover tiles as S-way split-K passes
+ * over caller workspace `ws` (cc_decode_ws_floats(B, h, K, dtype) floats; 0 = no split for this
+ * shape, ws may then be NULL) summed in fixed order -- deterministic.  Same results as
+ * cc_decode_fwd up to fp32 summation order in the leftover columns. */
+int64_t cc_decode_ws_floats(int64_t B, int64_t h, int64_t K, int dtype);
+int cc_decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, float* ws, int64_t ws_floats, int64_t B,
+                     int64_t h, int64_t K, int dtype, void* stream);
+
 /* get_losses reconstruction terms + their backward (crosscoder.py:104-121, autograd):
  * r = recon_f32 + b_dec; g_recon = dtype(grad_scale * (r - x)) with grad_scale = 2/B.
  * row_part [2][n*cc_loss_col_blocks(d)][B]: [0] sum (r-x)^2, [1] sum (x - x_mean)^2 per

@@ -472,3 +472,34 @@ def test_sharded_trainer_world1_matches_trainer(gpu):
         assert (p_single - p_sharded).abs().max().item() <= 4 * 5e-5 + 1e-3 * p_single.abs().max().item()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shape", [(4096, 16384, 4608), (4096, 2048, 4608), (4000, 1024, 4600), (1024, 1024, 2304),
+                                   (300, 512, 200)])
+def test_decode_split_schedule(gpu, shape):
+    """cc_decode_fwd_ws (whole 256-tile waves + split-K leftover tiles) vs the single-launch decode:
+    the whole-wave columns bit for bit, the split columns to fp32 summation order, both vs fp64
+    (ragged batch / column tails included)."""
+    B, h, K = shape
+    g = torch.Generator().manual_seed(B + h + K)
+    acts = torch.relu(torch.randn(B, h, generator=g)).to(torch.bfloat16).to(gpu)
+    W = (torch.randn(h, K, generator=g) * 0.05).to(torch.bfloat16).to(gpu)
+    nws = ops.decode_ws_floats(B, h, K, torch.bfloat16)
+    nbm, nbn = -(-B // 256), -(-K // 256)
+    waves = nbm * nbn // 256
+    split = waves > 0 and (nbm * nbn) % 256 and (256 * waves) % nbm == 0
+    assert bool(nws) == bool(split)
+    ws = torch.full((nws,), float("nan"), device=gpu) if nws else None
+    r_split = torch.empty(B, K, device=gpu)
+    r_one = torch.empty(B, K, device=gpu)
+    ops.decode_partial(acts, W, r_split, ws)
+    ops.decode_fwd(acts, W, None, recon_f32=r_one)
+    torch.cuda.synchronize()
+    if (B, h, K) == (4096, 16384, 4608):
+        assert nws == 8 * 4096 * 512  # 32 leftover tiles of 288 -> 8-way split
+    ref = acts.double().cpu() @ W.double().cpu()
+    assert rel(r_split, ref) < 1e-5
+    assert rel(r_split, r_one) < 1e-6
+    if nws:
+        col0 = 256 * (256 * waves // nbm)
+        assert torch.equal(r_split[:, :col0], r_one[:, :col0])

@@ -24,7 +24,8 @@ def analyse(name, rec, nb0=None):
     cu_key = (xcc << 16) | ((hw >> 8) & 0xFF)
     span = en.max().item()
     dur, epi = en - st, en - mid
-    print(f"{name}: blocks {rec.shape[0]}, kernel span {span:.1f} us, tile {dur.mean():.1f} us "
+    print(f"{name}: blocks {rec.shape[0]}, kernel span {span:.1f} us, last block start {st.max():.1f} us, "
+          f"tile {dur.mean():.1f} us "
           f"(min {dur.min():.1f} max {dur.max():.1f}), epilogue {epi.mean():.1f} us, main loop {(mid - st).mean():.1f} us")
     if nb0 is not None:
         for lab, sl in (("first GEMM", slice(0, nb0)), ("second GEMM", slice(nb0, None))):
@@ -93,6 +94,12 @@ def main():
         "G4 no L1 term (MN/MN)": (lambda: L.cc_wgrad_dec(P(acts), P(g_recon), P(W), P(norms), P(colsum), 0.0, P(gW),
                                                          P(parts), B, h, n, d, 1, st), None),
     }
+    W2 = (torch.randn(h, K, device=dev, generator=g) * 0.02).to(bf)
+    rec = torch.empty(B, K, device=dev)
+    nws = L.cc_decode_ws_floats(B, h, K, 1)
+    ws = torch.empty(max(1, nws), device=dev)
+    cases["G2 split-K leftover pass"] = (lambda: L.cc_decode_fwd_ws(P(acts), P(W2), P(rec), P(ws), nws, B, h, K, 1, st),
+                                         None)
     for name, (fn, nb0) in cases.items():
         for _ in range(20):  # warm clocks
             assert fn() == 0
