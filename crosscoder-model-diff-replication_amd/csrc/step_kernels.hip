@@ -251,9 +251,28 @@ __global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const float*
     acc[4] += ev_part[i * 4 + 2];
     acc[5] += ev_part[i * 4 + 3];
   }
-  for (int64_t i = threadIdx.x; i < n_wave; i += SCAL_THREADS) {
-    if (l1_part) acc[1] += l1_part[i];
-    if (l0_part) acc[2] += l0_part[i];
+  // 4 independent loads per array in flight per trip (clamped index, no branch around a load)
+  if (l1_part && l0_part) {
+    for (int64_t i = threadIdx.x; i < n_wave; i += 4 * SCAL_THREADS) {
+      float a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t j = i + u * SCAL_THREADS;
+        const int64_t jc = j < n_wave ? j : 0;
+        a[u] = j < n_wave ? l1_part[jc] : 0.f;
+        b[u] = j < n_wave ? l0_part[jc] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc[1] += a[u];
+        acc[2] += b[u];
+      }
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < n_wave; i += SCAL_THREADS) {
+      if (l1_part) acc[1] += l1_part[i];
+      if (l0_part) acc[2] += l0_part[i];
+    }
   }
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
@@ -290,8 +309,20 @@ __global__ __launch_bounds__(SCAL_THREADS) void clip_kernel(const ClipArgs a) {
   double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
-    if (p < a.nparams)
-      for (int64_t i = a.off[p] + threadIdx.x; i < a.off[p + 1]; i += SCAL_THREADS) s[p] += (double)a.sq[i];
+    if (p < a.nparams) {
+      const int64_t lo = a.off[p], hi = a.off[p + 1];
+      // 4 independent loads in flight per trip (clamped index, no branch around a load)
+      for (int64_t i = lo + threadIdx.x; i < hi; i += 4 * SCAL_THREADS) {
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t j = i + u * SCAL_THREADS;
+          v[u] = j < hi ? a.sq[j < hi ? j : lo] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s[p] += (double)v[u];
+      }
+    }
   }
 #pragma unroll
   for (int p = 0; p < 8; ++p) {

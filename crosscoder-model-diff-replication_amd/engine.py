@@ -119,6 +119,29 @@ class StepWorkspace:
         return self.sq[self.sq_off[i]:self.sq_off[i + 1]]
 
 
+def _norms_token(P):
+    # the decoder norms stay valid while W_dec is the same storage and has not been written in
+    # place through torch (every such write bumps the view's version counter; our own Adam kernel
+    # does not, and norms_for_next() is launched right after it)
+    return (P.W_dec_hk.data_ptr(), P.W_dec_hk._version)
+
+
+def norms_for_next(ws, P):
+    """Launch the next step's decoder norms now (right after Adam wrote W_dec), so they run while
+    the host turns this step's loss scalars into the loss dict; forward() then skips them."""
+    ops.dec_norms(P.W_dec_hk, ws.h, ws.n, ws.d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
+    ws.norms_token = _norms_token(P)
+
+
+def decoder_norms(ws, P):
+    """||W_dec[h, m]||, their sum over m and inverses (crosscoder.py:123-125), unless still fresh."""
+    if getattr(ws, "norms_token", None) == _norms_token(P):
+        ws.norms_token = None  # consumed: W_dec changes with this step's Adam
+        return
+    ws.norms_token = None
+    ops.dec_norms(P.W_dec_hk, ws.h, ws.n, ws.d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
+
+
 def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True):
     """Forward + reconstruction-loss gradient.  P: params Arena.  x_in [B, n, d] any of
     fp32/bf16, factor [n] or None.  Leaves losses in ws.scalars / ws.ev*, g_recon ready
@@ -126,7 +149,7 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
     ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart)
     ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
-    ops.dec_norms(P.W_dec_hk, h, n, d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
+    decoder_norms(ws, P)
     with _span("G1_encode"):
         ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, tn=ws.tn, colsum_part=ws.acts_colpart,
                        l1_part=ws.l1_part, l0_part=ws.l0_part)

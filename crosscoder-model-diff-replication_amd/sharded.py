@@ -99,7 +99,7 @@ class HipShardBackend:
         B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
         ops.prep_input(raw, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart)
         ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
-        ops.dec_norms(P.W_dec_hk, h, n, d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
+        engine.decoder_norms(ws, P)
         with engine._span("G1_encode"):
             ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, tn=ws.tn, colsum_part=ws.acts_colpart,
                            l1_part=ws.l1_part, l0_part=ws.l0_part)

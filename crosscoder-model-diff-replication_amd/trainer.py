@@ -72,6 +72,7 @@ class Trainer:
         self.scheduler = LambdaLRHost(self.optimizer, self.lr_lambda)
         self.step_counter = 0
         self.logger = logger
+        self._host = None  # pinned loss-scalar landing buffer (allocated on the first step)
 
     def lr_lambda(self, step):
         if step < 0.8 * self.total_steps:
@@ -88,6 +89,7 @@ class Trainer:
         cc = self.crosscoder
         raw, factor = self.buffer.next_raw()
         ws = cc._workspace(raw.shape[0])
+        self._last_B = raw.shape[0]
         P = cc.arena()
         opt = self.optimizer
         engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None)
@@ -104,7 +106,16 @@ class Trainer:
     def step(self):
         scalars = self.step_async()
         l1c = self._last_l1c
-        s = scalars[:6].tolist()  # the step's single device->host copy
+        # the step's single device->host copy; the next step's decoder norms are launched behind it
+        # and run while the host builds the loss dict
+        if self._host is None:
+            self._host = torch.empty(8, dtype=torch.float32, pin_memory=True)
+            self._copied = torch.cuda.Event()
+        self._host.copy_(scalars[:8], non_blocking=True)
+        self._copied.record()
+        engine.norms_for_next(self.crosscoder._workspace(self._last_B), self.crosscoder.arena())
+        self._copied.synchronize()
+        s = self._host[:6].tolist()
         dt = self.crosscoder.dtype
         rd = (lambda v: float(torch.tensor(v, dtype=dt))) if dt != torch.float32 else float
         l2, l1, l0 = s[0], rd(s[1]), s[2]
