@@ -69,6 +69,29 @@ class EventTimer:
         return {k: sum(s.elapsed_time(e) for s, e in v) / len(v) for k, v in self.rec.items()}
 
 
+# span name -> kernel-name prefix in the rocprofv3 traces
+SPAN_KERNEL = {"G1_encode": "gemm_pp_kernel<true, true, 1>", "G2_decode": "gemm_pp_kernel<true, false, 2>",
+               "G3_dacts": "gemm_pp_kernel<true, true, 3>", "G4G5_wgrad": "gemm_pp_dual_kernel<false, false, 4, 5>",
+               "adam": "adam_bulk_kernel"}
+
+
+def pmc_traffic(span):
+    """HBM bytes per launch of the span's kernel from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate FETCH_SIZE /
+    WRITE_SIZE passes of this bench), or None."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files or span not in SPAN_KERNEL:
+        return None, None
+    with open(files[-1]) as f:
+        doc = json.load(f)
+    for name, v in doc["kernels"].items():
+        if name.startswith(SPAN_KERNEL[span]):
+            return v["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def make_cfg(h, steps_total):
     return {
         "seed": 49, "batch_size": B, "buffer_mult": 128, "lr": 5e-5, "num_tokens": 400_000_000, "l1_coeff": 2,
@@ -173,6 +196,15 @@ def main():
     dom_flop = gemm_flop * (2 if dom == "G4G5_wgrad" else 1)
     achieved = dom_flop / (dom_ms * 1e-3) / 1e12
     step_flop = 5 * gemm_flop
+    traffic, traffic_src = pmc_traffic(dom)
+    # algorithmic operand/output bytes of the dominant launch (each input read once, output written once)
+    es = 2  # bf16
+    K_ = N_MODELS * D_MODEL
+    alg = {"G1_encode": (B * K_ + H_LOCAL * K_ + B * H_LOCAL) * es,
+           "G2_decode": (B * H_LOCAL + H_LOCAL * K_) * es + B * K_ * 4,
+           "G3_dacts": (B * K_ + H_LOCAL * K_ + 2 * B * H_LOCAL) * es,
+           "G4G5_wgrad": (2 * B * H_LOCAL + 2 * B * K_ + 3 * H_LOCAL * K_) * es}
+    dom_alg_bytes = alg.get(dom)
     result = {
         "metric": "activations/sec per train step (fwd+bwd+Adam), 2x2304->16384; % bf16 MFMA peak",
         "value": round(value, 1),
@@ -192,8 +224,10 @@ def main():
                    "parallelism": f"latent{world}"},
         "step_mfma_frac": round(step_flop / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
         "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items())},
-        "roofline": {"bound": "mfma", "kernel": dom, "kernel_ms": round(dom_ms, 4), "achieved": round(achieved, 1), "peak": round(PEAK_BF16_TFLOPS, 1),
-                     "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None},
+        "roofline": {"bound": "mfma", "kernel": dom, "kernel_ms": round(dom_ms, 4), "achieved": round(achieved, 1),
+                     "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                     "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
+                     "algorithmic_bytes": dom_alg_bytes},
         "last_loss": {k: round(v, 6) for k, v in last.items()},
     }
     if rank == 0:
