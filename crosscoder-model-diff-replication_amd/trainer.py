@@ -84,8 +84,10 @@ class Trainer:
             return self.cfg["l1_coeff"] * self.step_counter / (0.05 * self.total_steps)
         return self.cfg["l1_coeff"]
 
-    def step_async(self):
-        """Launch one full step; returns the device scalars tensor (no host sync)."""
+    def step_async(self, on_losses=None):
+        """Launch one full step (no host sync); returns the device scalars tensor.
+        on_losses(scalars): called right after the forward's loss scalars are enqueued, before the
+        backward / clip / Adam launches."""
         cc = self.crosscoder
         raw, factor = self.buffer.next_raw()
         ws = cc._workspace(raw.shape[0])
@@ -93,27 +95,38 @@ class Trainer:
         P = cc.arena()
         opt = self.optimizer
         engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None)
+        if on_losses is not None:
+            on_losses(ws.scalars)
         l1c = self.get_l1_coeff()
         engine.backward(ws, P, opt.grads, l1c)
         g = opt.param_groups[0]
         opt.t += 1
         b1, b2 = g["betas"]
         engine.clip_and_adam(ws, P, opt.grads, opt.exp_avg, opt.exp_avg_sq, g["lr"], b1, b2, g["eps"], opt.t)
+        # the next step's decoder norms, straight behind Adam (consumed by the next forward)
+        engine.norms_for_next(ws, P)
         self.scheduler.step()
         self._last_l1c = l1c
         return ws.scalars
 
-    def step(self):
-        scalars = self.step_async()
-        l1c = self._last_l1c
-        # the step's single device->host copy; the next step's decoder norms are launched behind it
-        # and run while the host builds the loss dict
+    def _copy_losses(self, scalars):
+        # the step's single device->host copy, enqueued as soon as the forward has produced the
+        # losses: the host waits for the forward only, and enqueues the next step while this
+        # step's backward / Adam still run (torch's stream orders every later use of the params)
         if self._host is None:
             self._host = torch.empty(8, dtype=torch.float32, pin_memory=True)
             self._copied = torch.cuda.Event()
         self._host.copy_(scalars[:8], non_blocking=True)
         self._copied.record()
-        engine.norms_for_next(self.crosscoder._workspace(self._last_B), self.crosscoder.arena())
+
+    early_loss_copy = True  # False: copy the losses after the whole step (A/B switch for tools/)
+
+    def step(self):
+        if self.early_loss_copy:
+            self.step_async(on_losses=self._copy_losses)
+        else:
+            self._copy_losses(self.step_async())
+        l1c = self._last_l1c
         self._copied.synchronize()
         s = self._host[:6].tolist()
         dt = self.crosscoder.dtype
