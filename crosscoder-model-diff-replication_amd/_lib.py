@@ -35,7 +35,7 @@ SIGNATURES = {
     "cc_loss_scalars_len": (_i64, [_i64]),
     "cc_gemm_f32out": (_i, [_p, _i, _i64, _p, _i, _i64, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_prep_input": (_i, [_p, _i, _p, _i, _p, _p, _i64, _i64, _i64, _i, _p]),
-    "cc_reduce_rows": (_i, [_p, _i64, _i64, _i64, _f, _p, _p, _i, _p, _p]),
+    "cc_reduce_rows": (_i, [_p, _i64, _i64, _i64, _f, _p, _p, _i, _p, _p, _p, _p]),
     "cc_reduce_parts": (_i64, [_i64]),
     "cc_dec_norms": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_encode_fwd": (_i, [_p, _p, _p, _p, _p, _i, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
@@ -44,13 +44,13 @@ SIGNATURES = {
     "cc_decode_fwd_ws": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_loss_fwd_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i, _p]),
     "cc_loss_fwd_bwd_rows": (_i, [_p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i64, _i64, _i, _p]),
-    "cc_loss_finalize": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "cc_loss_finalize": (_i, [_p, _p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
     "cc_dacts_bwd": (_i, [_p, _p, _p, _p, _f, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_dec": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_enc": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_both": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_clip_finalize": (_i, [_p, ctypes.POINTER(_i64), _i, _f, _i, _p, _p]),
-    "cc_adam_step": (_i, [_p, _p, _p, _p, _i64, _p, _d, _d, _d, _d, _i64, _i, _p]),
+    "cc_adam_step": (_i, [_p, _p, _p, _p, _i64, _p, _d, _d, _d, _d, _i64, _i64, _i, _p]),
 }
 
 _lib = None

@@ -125,6 +125,7 @@ class CrossCoder(nn.Module):
     def decode(self, acts):
         """acts [batch, d_hidden] -> [batch, n_models, d_model] incl. b_dec (crosscoder.py:82-89)."""
         a = self.arena()
+        a.wait_pending()
         acts = acts.to(self.dtype).contiguous()
         B = acts.shape[0]
         out = torch.empty(B, self.n_models * self.cfg["d_in"], dtype=self.dtype, device=acts.device)
@@ -139,6 +140,12 @@ class CrossCoder(nn.Module):
         (backward runs the fused HIP backward kernels)."""
         a = self.arena()
         return LossOutput(*_LossFn.apply(self, x, a.data, self.W_enc, self.W_dec, self.b_enc, self.b_dec))
+
+    def state_dict(self, *args, **kwargs):
+        # the decoder half may still be updating on the trainer's side stream
+        if getattr(self, "_arena", None) is not None:
+            self._arena.wait_pending()
+        return super().state_dict(*args, **kwargs)
 
     # ------------------------------------------------------------------ checkpoints
     def create_save_dir(self):

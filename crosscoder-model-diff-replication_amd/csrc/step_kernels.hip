@@ -48,14 +48,16 @@ __global__ __launch_bounds__(256) void prep_kernel(const void* __restrict__ x_in
 }
 
 // ---------------------------------------------------------------------------------------
-// out[j] = scale * sum_i part[i*ld + j]; optional dtype copy and squared-sum partial per block.
+// out[j] = scale * sum_i part[i*ld + j]; optional dtype copy, squared-sum partial per block and
+// dot partial per block (sum_j out[j] * dot_w[j]: the L1 loss from the activation column sums).
 // Block = 64 columns x 4 waves; wave w sums rows w, w+4, ... (independent loads in flight),
-// then a fixed-order combine of the 4 wave partials.  One sq partial per block.
+// then a fixed-order combine of the 4 wave partials.  One sq / dot partial per block.
 constexpr int RED_COLS = 64;
 template <int DT>
 __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ part, int R, int C, int64_t ld,
                                                           float scale, float* __restrict__ out_f32,
-                                                          void* __restrict__ out_t, float* __restrict__ sq_part) {
+                                                          void* __restrict__ out_t, float* __restrict__ sq_part,
+                                                          const float* __restrict__ dot_w, float* __restrict__ dot_part) {
   __shared__ float red[4][RED_COLS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int j = blockIdx.x * RED_COLS + lane;
@@ -73,7 +75,7 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
   red[wave][lane] = s;
   __syncthreads();
   if (wave != 0) return;
-  float sq = 0.f;
+  float sq = 0.f, dot = 0.f;
   if (j < C) {
     s = (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]) * scale;
     if (out_f32) out_f32[j] = s;
@@ -83,10 +85,16 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
       float vq = Elem<DT>::to_f(q);
       sq = vq * vq;
     }
+    if (dot_part) dot = s * dot_w[j];
   }
-  if (!sq_part) return;
-  sq = wave_sum(sq);
-  if (lane == 0) sq_part[blockIdx.x] = sq;
+  if (sq_part) {
+    sq = wave_sum(sq);
+    if (lane == 0) sq_part[blockIdx.x] = sq;
+  }
+  if (dot_part) {
+    dot = wave_sum(dot);
+    if (lane == 0) dot_part[blockIdx.x] = dot;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -239,7 +247,7 @@ __global__ __launch_bounds__(256) void ev_kernel(const float* __restrict__ row_p
 // Single block: scalars = {l2, l1, l0, mean ev, mean ev_a, mean ev_b}.
 constexpr int SCAL_THREADS = 1024;
 __global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const float* __restrict__ ev_part, int nblk,
-                                                                    const float* __restrict__ l1_part,
+                                                                    const float* __restrict__ l1_part, int64_t n_l1,
                                                                     const float* __restrict__ l0_part, int64_t n_wave,
                                                                     int B, float* __restrict__ scalars) {
   constexpr int NW = SCAL_THREADS / 64;
@@ -251,29 +259,21 @@ __global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const float*
     acc[4] += ev_part[i * 4 + 2];
     acc[5] += ev_part[i * 4 + 3];
   }
-  // 4 independent loads per array in flight per trip (clamped index, no branch around a load)
-  if (l1_part && l0_part) {
+  // 4 independent loads in flight per trip (clamped index, no branch around a load)
+  if (l0_part) {
     for (int64_t i = threadIdx.x; i < n_wave; i += 4 * SCAL_THREADS) {
-      float a[4], b[4];
+      float b[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t j = i + u * SCAL_THREADS;
-        const int64_t jc = j < n_wave ? j : 0;
-        a[u] = j < n_wave ? l1_part[jc] : 0.f;
-        b[u] = j < n_wave ? l0_part[jc] : 0.f;
+        b[u] = j < n_wave ? l0_part[j < n_wave ? j : 0] : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        acc[1] += a[u];
-        acc[2] += b[u];
-      }
-    }
-  } else {
-    for (int64_t i = threadIdx.x; i < n_wave; i += SCAL_THREADS) {
-      if (l1_part) acc[1] += l1_part[i];
-      if (l0_part) acc[2] += l0_part[i];
+      for (int u = 0; u < 4; ++u) acc[2] += b[u];
     }
   }
+  if (l1_part)
+    for (int64_t i = threadIdx.x; i < n_l1; i += SCAL_THREADS) acc[1] += l1_part[i];
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
     double s = wave_sum_d(acc[q]);
@@ -535,18 +535,19 @@ int cc_prep_input(const void* x_in, int in_dtype, const void* factor, int factor
 }
 
 int cc_reduce_rows(const float* part, int64_t R, int64_t C, int64_t ld, float scale, float* out_f32, void* out_t,
-                   int dtype, float* sq_part, void* stream) {
+                   int dtype, float* sq_part, const float* dot_w, float* dot_part, void* stream) {
   if (!part) return CC_ERR_NULL;
   if (R <= 0 || C <= 0) return CC_ERR_SHAPE;
   if (sq_part && !out_t) return CC_ERR_NULL;
+  if (dot_part && !dot_w) return CC_ERR_NULL;
   dim3 grid((unsigned)((C + RED_COLS - 1) / RED_COLS));
   hipStream_t st = (hipStream_t)stream;
   if (out_t) {
     DISPATCH_DT(dtype, hipLaunchKernelGGL((reduce_rows_kernel<DT_>), grid, dim3(256), 0, st, part, (int)R, (int)C, ld,
-                                          scale, out_f32, out_t, sq_part));
+                                          scale, out_f32, out_t, sq_part, dot_w, dot_part));
   } else {
     hipLaunchKernelGGL((reduce_rows_kernel<CC_F32>), grid, dim3(256), 0, st, part, (int)R, (int)C, ld, scale, out_f32,
-                       nullptr, nullptr);
+                       nullptr, nullptr, dot_w, dot_part);
   }
   CC_LAUNCH_CHECK();
   return CC_OK;
@@ -590,8 +591,9 @@ int cc_loss_fwd_bwd(const float* recon_f32, const void* b_dec, const void* x, co
                               dtype, stream);
 }
 
-int cc_loss_finalize(const float* row_part, const float* l1_part, const float* l0_part, int64_t n_wave, float* ev,
-                     float* ev_a, float* ev_b, float* scalars, int64_t B, int64_t n, int64_t d, void* stream) {
+int cc_loss_finalize(const float* row_part, const float* l1_part, int64_t n_l1, const float* l0_part, int64_t n_l0,
+                     float* ev, float* ev_a, float* ev_b, float* scalars, int64_t B, int64_t n, int64_t d,
+                     void* stream) {
   if (!row_part || !scalars) return CC_ERR_NULL;
   if (B <= 0 || n <= 0 || d <= 0) return CC_ERR_SHAPE;
   // the per-block partials of the row terms use the tail of `scalars` (cc_loss_scalars_len)
@@ -600,8 +602,8 @@ int cc_loss_finalize(const float* row_part, const float* l1_part, const float* l
   float* ev_part = scalars + 8;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(ev_kernel, dim3(nblk), dim3(256), 0, st, row_part, (int)B, (int)n, ncb, ev, ev_a, ev_b, ev_part);
-  hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(SCAL_THREADS), 0, st, ev_part, nblk, l1_part, l0_part, n_wave, (int)B,
-                     scalars);
+  hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(SCAL_THREADS), 0, st, ev_part, nblk, l1_part, n_l1, l0_part,
+                     n_l0, (int)B, scalars);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }
@@ -623,7 +625,7 @@ int cc_clip_finalize(const float* sq, const int64_t* off, int nparams, float max
 }
 
 int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, double lr, double beta1,
-                 double beta2, double eps, int64_t step, int dtype, void* stream) {
+                 double beta2, double eps, int64_t step, int64_t max_blocks, int dtype, void* stream) {
   if (!p || !g || !m || !v) return CC_ERR_NULL;
   if (numel <= 0 || step <= 0) return CC_ERR_SHAPE;
   if (!al16(p) || !al16(g) || !al16(m) || !al16(v)) return CC_ERR_ALIGN;
@@ -639,6 +641,14 @@ int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const 
   a.bc2s = (float)sqrt(bc2);
   a.neg_step = (float)(-((double)lr / bc1));
   hipStream_t st = (hipStream_t)stream;
+  if (max_blocks > 0) {  // capped grid-stride form: leaves most CUs to a concurrent GEMM
+    int64_t work = (numel + 7) / 8;
+    int64_t blocks = (work + 255) / 256;
+    if (blocks > max_blocks) blocks = max_blocks;
+    DISPATCH_DT(dtype, hipLaunchKernelGGL((adam_kernel<DT_>), dim3((unsigned)blocks), dim3(256), 0, st, a));
+    CC_LAUNCH_CHECK();
+    return CC_OK;
+  }
 #if CC_ADAM_U > 0
   const int64_t nchunks = numel / 8;
   if (nchunks > 0) {

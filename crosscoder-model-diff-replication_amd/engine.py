@@ -38,7 +38,9 @@ def _span(name):
 
 
 class Arena:
-    """Flat storage for the four parameters (or their grads / Adam moments)."""
+    """Flat storage for the four parameters (or their grads / Adam moments):
+    [ W_enc h-major [h][K] | b_enc [h] | W_dec [h][K] | b_dec [K] ] -- the encoder half and the
+    decoder half are contiguous, so Adam can update them as two launches (enc_part / dec_part)."""
 
     def __init__(self, h, n, d, dtype, device, data=None):
         self.h, self.n, self.d = h, n, d
@@ -49,11 +51,25 @@ class Arena:
         o = 0
         self.W_enc_hk = self.data[o:o + h * K].view(h, K)
         o += h * K
-        self.W_dec_hk = self.data[o:o + h * K].view(h, K)
-        o += h * K
         self.b_enc = self.data[o:o + h]
         o += h
+        self.split = o  # enc_part = data[:split], dec_part = data[split:]
+        self.W_dec_hk = self.data[o:o + h * K].view(h, K)
+        o += h * K
         self.b_dec_flat = self.data[o:o + K]
+        self.pending = None  # event the decoder half's Adam (side stream) records; see clip_and_adam
+
+    def enc_part(self):
+        return self.data[:self.split]
+
+    def dec_part(self):
+        return self.data[self.split:]
+
+    def wait_pending(self):
+        """Order torch's current stream after the decoder half's Adam if it ran on a side stream."""
+        if self.pending is not None:
+            torch.cuda.current_stream(self.data.device).wait_event(self.pending)
+            self.pending = None
 
     # reference-shaped views
     def W_enc(self):  # [n, d, h], strides (d, 1, K)
@@ -91,7 +107,8 @@ class StepWorkspace:
         self.acts_colpart = E(ops.col_part_rows(B), h)
         self.colsum_acts = E(h)
         self.n_wave = ops.wave_parts(B, h)
-        self.l1_part = E(self.n_wave)
+        self.n_l1 = ops.reduce_parts(h)
+        self.l1_part = E(self.n_l1)  # per 64-latent block: sum_h colsum_acts[h] * tn[h] (= B * l1)
         self.l0_part = E(self.n_wave)
         self.recon = E(B, K)
         nws = ops.decode_ws_floats(B, h, K, dtype)
@@ -114,6 +131,7 @@ class StepWorkspace:
             self.sq_off.append(self.sq_off[-1] + s)
         self.sq = E(self.sq_off[-1])
         self.clip_out = E(8)
+        self.norms_token = None
 
     def sq_slice(self, i):
         return self.sq[self.sq_off[i]:self.sq_off[i + 1]]
@@ -128,7 +146,10 @@ def _norms_token(P):
 
 def norms_for_next(ws, P):
     """Launch the next step's decoder norms now (right after Adam wrote W_dec), so they run while
-    the host turns this step's loss scalars into the loss dict; forward() then skips them."""
+    the host turns this step's loss scalars into the loss dict; forward() then skips them.
+    (clip_and_adam(side_stream=...) launches them on the side stream itself.)"""
+    if ws.norms_token == _norms_token(P):
+        return
     ops.dec_norms(P.W_dec_hk, ws.h, ws.n, ws.d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
     ws.norms_token = _norms_token(P)
 
@@ -149,10 +170,14 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
     ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart)
     ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
-    decoder_norms(ws, P)
+    # G1 reads only the encoder half: it may overlap the previous step's decoder-half Adam
     with _span("G1_encode"):
-        ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, tn=ws.tn, colsum_part=ws.acts_colpart,
-                       l1_part=ws.l1_part, l0_part=ws.l0_part)
+        ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, colsum_part=ws.acts_colpart, l0_part=ws.l0_part)
+    P.wait_pending()
+    decoder_norms(ws, P)
+    # sum_b acts (for dL1/dW_dec) and B * l1 = sum_h colsum_acts[h] * tn[h] (crosscoder.py:126)
+    ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts, dot_w=ws.tn,
+                    dot_part=ws.l1_part)
     with _span("G2_decode"):
         ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
     if loss:
@@ -167,8 +192,8 @@ def loss_rows(ws, P, r0, r1, grad_scale=None):
 
 
 def loss_finalize(ws):
-    ops.loss_finalize(ws.row_part, ws.l1_part, ws.l0_part, ws.n_wave, ws.ev, ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n,
-                      ws.d)
+    ops.loss_finalize(ws.row_part, ws.l1_part, ws.n_l1, ws.l0_part, ws.n_wave, ws.ev, ws.ev_a, ws.ev_b, ws.scalars,
+                      ws.B, ws.n, ws.d)
 
 
 def loss_from_recon(ws, P, grad_scale=None):
@@ -200,8 +225,6 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False):
     l1_scale = float(l1_coeff) * l1_grad_weight / B
     if not dacts_done:
         dacts_rows(ws, P, l1_coeff, 0, B, l1_grad_weight)
-    if l1_scale != 0.0:
-        ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts)
     with _span("G4G5_wgrad"):
         ops.wgrad_both(ws.acts, ws.g_recon, P.W_dec_hk, ws.inv_norms, ws.colsum_acts, l1_scale, G.W_dec_hk,
                        ws.sq_slice(1), ws.g_pre, ws.x, G.W_enc_hk, ws.sq_slice(0), n, d)
@@ -209,8 +232,35 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False):
     ops.reduce_rows(ws.loss_colpart, ws.loss_colpart.shape[0], K, out_t=G.b_dec_flat, sq_part=ws.sq_slice(3))
 
 
-def clip_and_adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, max_norm=1.0):
+# workgroups of the decoder-half Adam that runs beside the next step's G1 (0: uncapped one-pass)
+DEC_ADAM_BLOCKS = 256
+
+
+def clip_and_adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, max_norm=1.0, side_stream=None):
+    """clip_grad_norm_ + Adam.  side_stream: the decoder half's Adam (+ the next step's decoder
+    norms) runs there, so it overlaps the next step's encoder GEMM (G1 reads only the encoder half,
+    which Adam updates on torch's stream); P.pending orders every later decoder-half use
+    (forward() waits before the decoder norms; CrossCoder's methods wait; Trainer.synchronize())."""
     emulate = ws.dtype == torch.bfloat16
     ops.clip_finalize(ws.sq, ws.sq_off, max_norm, emulate, ws.clip_out)
+    if side_stream is None:
+        with _span("adam"):
+            ops.adam_step(P.data, G.data, M.data, V.data, ws.clip_out[0:1], lr, beta1, beta2, eps, step)
+        return
+    main = torch.cuda.current_stream(P.data.device)
     with _span("adam"):
-        ops.adam_step(P.data, G.data, M.data, V.data, ws.clip_out[0:1], lr, beta1, beta2, eps, step)
+        ops.adam_step(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), ws.clip_out[0:1], lr, beta1, beta2,
+                      eps, step)
+    # the decoder half starts after the encoder half (both are HBM-bound: run together they only
+    # share the bandwidth), i.e. beside the next step's prep / G1 on the main stream
+    enc_done = torch.cuda.Event()
+    enc_done.record(main)
+    with torch.cuda.stream(side_stream):
+        side_stream.wait_event(enc_done)
+        with _span("adam_dec"):
+            ops.adam_step(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), ws.clip_out[0:1], lr, beta1,
+                          beta2, eps, step, max_blocks=DEC_ADAM_BLOCKS)
+        norms_for_next(ws, P)
+        done = torch.cuda.Event()
+        done.record(side_stream)
+    P.pending = done

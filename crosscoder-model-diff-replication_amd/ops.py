@@ -101,10 +101,10 @@ def prep_input(x_in, factor, dtype, out=None, colsum_part=None):
     return out
 
 
-def reduce_rows(part, R, C, scale=1.0, out_f32=None, out_t=None, sq_part=None, ld=None):
+def reduce_rows(part, R, C, scale=1.0, out_f32=None, out_t=None, sq_part=None, ld=None, dot_w=None, dot_part=None):
     dt = dtype_code(out_t.dtype) if out_t is not None else CC_F32
     check(lib().cc_reduce_rows(_ptr(part), R, C, C if ld is None else ld, scale, _ptr(out_f32), _ptr(out_t),
-                               dt, _ptr(sq_part), _stream(part)))
+                               dt, _ptr(sq_part), _ptr(dot_w), _ptr(dot_part), _stream(part)))
 
 
 def reduce_parts(C):
@@ -158,8 +158,8 @@ def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_
                                      dtype_code(x.dtype), _stream(x)))
 
 
-def loss_finalize(row_part, l1_part, l0_part, n_wave, ev, ev_a, ev_b, scalars, B, n, d):
-    check(lib().cc_loss_finalize(_ptr(row_part), _ptr(l1_part), _ptr(l0_part), n_wave, _ptr(ev), _ptr(ev_a),
+def loss_finalize(row_part, l1_part, n_l1, l0_part, n_l0, ev, ev_a, ev_b, scalars, B, n, d):
+    check(lib().cc_loss_finalize(_ptr(row_part), _ptr(l1_part), n_l1, _ptr(l0_part), n_l0, _ptr(ev), _ptr(ev_a),
                                  _ptr(ev_b), _ptr(scalars), B, n, d, _stream(row_part)))
 
 
@@ -198,6 +198,6 @@ def clip_finalize(sq, offsets, max_norm, emulate_bf16, out):
                                  _stream(sq)))
 
 
-def adam_step(p, g, m, v, coef, lr, beta1, beta2, eps, step):
+def adam_step(p, g, m, v, coef, lr, beta1, beta2, eps, step, max_blocks=0):
     check(lib().cc_adam_step(_ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(coef), lr, beta1, beta2, eps,
-                             int(step), dtype_code(p.dtype), _stream(p)))
+                             int(step), int(max_blocks), dtype_code(p.dtype), _stream(p)))

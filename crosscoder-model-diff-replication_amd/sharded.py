@@ -95,16 +95,7 @@ class HipShardBackend:
     def forward_partial(self, raw, factor):
         cc = self.cc
         ws = self.ws = cc._workspace(raw.shape[0])
-        P = cc.arena()
-        B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
-        ops.prep_input(raw, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart)
-        ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
-        engine.decoder_norms(ws, P)
-        with engine._span("G1_encode"):
-            ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, tn=ws.tn, colsum_part=ws.acts_colpart,
-                           l1_part=ws.l1_part, l0_part=ws.l0_part)
-        with engine._span("G2_decode"):
-            ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
+        engine.forward(ws, cc.arena(), raw, factor, loss=False)  # G1, norms, G2 -> fp32 partial recon
         return ws.recon
 
     def row_chunks(self):

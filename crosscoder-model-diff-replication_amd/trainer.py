@@ -73,6 +73,7 @@ class Trainer:
         self.step_counter = 0
         self.logger = logger
         self._host = None  # pinned loss-scalar landing buffer (allocated on the first step)
+        self._side = None  # stream of the decoder half's Adam (created on the first step)
 
     def lr_lambda(self, step):
         if step < 0.8 * self.total_steps:
@@ -102,7 +103,8 @@ class Trainer:
         g = opt.param_groups[0]
         opt.t += 1
         b1, b2 = g["betas"]
-        engine.clip_and_adam(ws, P, opt.grads, opt.exp_avg, opt.exp_avg_sq, g["lr"], b1, b2, g["eps"], opt.t)
+        engine.clip_and_adam(ws, P, opt.grads, opt.exp_avg, opt.exp_avg_sq, g["lr"], b1, b2, g["eps"], opt.t,
+                             side_stream=self._side_stream())
         # the next step's decoder norms, straight behind Adam (consumed by the next forward)
         engine.norms_for_next(ws, P)
         self.scheduler.step()
@@ -120,6 +122,19 @@ class Trainer:
         self._copied.record()
 
     early_loss_copy = True  # False: copy the losses after the whole step (A/B switch for tools/)
+    overlap_decoder_adam = True  # False: one Adam launch on torch's stream (A/B switch for tools/)
+
+    def _side_stream(self):
+        if not self.overlap_decoder_adam:
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.crosscoder.arena().data.device)
+        return self._side
+
+    def synchronize(self):
+        """Order torch's current stream after every launch of the last step (the decoder half of
+        Adam may still run on the side stream; CrossCoder's own methods wait by themselves)."""
+        self.crosscoder.arena().wait_pending()
 
     def step(self):
         if self.early_loss_copy:
@@ -152,6 +167,7 @@ class Trainer:
         print(loss_dict)
 
     def save(self):
+        self.synchronize()
         self.crosscoder.save()
 
     def train(self):

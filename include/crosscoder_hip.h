@@ -76,9 +76,11 @@ int cc_prep_input(const void* x_in, int in_dtype, const void* factor, int factor
                   float* colsum_part, int64_t B, int64_t n, int64_t d, int dtype, void* stream);
 
 /* out[j] = scale * sum_{i<R} part[i*ld + j] (fixed order).  Optional: out_f32, out_t (dtype),
- * sq_part [cc_reduce_parts(C)] (per column block: sum of dtype-rounded out^2, for clip_grad_norm_). */
+ * sq_part [cc_reduce_parts(C)] (per column block: sum of dtype-rounded out^2, for clip_grad_norm_),
+ * dot_part [cc_reduce_parts(C)] (per column block: sum of out[j] * dot_w[j]; with out = the column
+ * sums of acts and dot_w = the total decoder norms this is B * l1_loss, crosscoder.py:126). */
 int cc_reduce_rows(const float* part, int64_t R, int64_t C, int64_t ld, float scale, float* out_f32,
-                   void* out_t, int dtype, float* sq_part, void* stream);
+                   void* out_t, int dtype, float* sq_part, const float* dot_w, float* dot_part, void* stream);
 int64_t cc_reduce_parts(int64_t C);
 
 /* W_dec.norm(dim=-1) and its sum over models (crosscoder.py:123-125):
@@ -129,9 +131,9 @@ int cc_loss_fwd_bwd_rows(const float* recon_f32, const void* b_dec, const void* 
 /* Loss reduction (crosscoder.py:106-128, trainer.py:51-61): per-row explained variances
  * ev/ev_a/ev_b [B] (fp32) and scalars[0:8] = {l2, l1, l0, mean ev, mean ev_a, mean ev_b, 0, 0};
  * `scalars` holds cc_loss_scalars_len(B) floats (the tail is workspace).
- * l1_part / l0_part: the per-wave partials of cc_encode_fwd (n_wave entries each), scaled
- * by 1/B (NULL -> 0). */
-int cc_loss_finalize(const float* row_part, const float* l1_part, const float* l0_part, int64_t n_wave,
+ * l1_part [n_l1] / l0_part [n_l0]: partial sums of B * l1 (cc_reduce_rows dot_part, or the per-wave
+ * partials of cc_encode_fwd) and of the active count (cc_encode_fwd), scaled by 1/B (NULL -> 0). */
+int cc_loss_finalize(const float* row_part, const float* l1_part, int64_t n_l1, const float* l0_part, int64_t n_l0,
                      float* ev, float* ev_a, float* ev_b, float* scalars, int64_t B, int64_t n, int64_t d,
                      void* stream);
 
@@ -171,9 +173,11 @@ int cc_clip_finalize(const float* sq, const int64_t* off, int nparams, float max
 /* torch.optim.Adam step (trainer.py:16-20,47; torch/optim/adam.py single-tensor path, no weight
  * decay / amsgrad) fused with the clip multiply: g' = dtype(g * coef[0]); m, v, p updated in place
  * over `numel` flat elements; step = the Adam step count AFTER increment; lr from LambdaLR.
- * dtype-rounding between torch's ops is reproduced (bf16 state like the reference). */
+ * dtype-rounding between torch's ops is reproduced (bf16 state like the reference).
+ * max_blocks > 0: grid-stride over at most that many 256-thread workgroups (for an update that
+ * runs beside a GEMM on another stream); 0: one pass, one 8-element chunk per thread. */
 int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, double lr,
-                 double beta1, double beta2, double eps, int64_t step, int dtype, void* stream);
+                 double beta1, double beta2, double eps, int64_t step, int64_t max_blocks, int dtype, void* stream);
 
 #ifdef __cplusplus
 }

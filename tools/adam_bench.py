@@ -35,7 +35,7 @@ def main():
     res = {}
     for rnd in range(6):
         for name, L in libs:
-            fn = lambda: L.cc_adam_step(P(p), P(gr), P(m), P(v), NUMEL, P(coef), 5e-5, 0.9, 0.999, 1e-8, 7, 1, st)  # noqa
+            fn = lambda: L.cc_adam_step(P(p), P(gr), P(m), P(v), NUMEL, P(coef), 5e-5, 0.9, 0.999, 1e-8, 7, 0, 1, st)  # noqa
             assert fn() == 0
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
