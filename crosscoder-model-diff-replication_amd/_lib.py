@@ -50,6 +50,9 @@ SIGNATURES = {
     "cc_wgrad_enc": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_both": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_clip_finalize": (_i, [_p, ctypes.POINTER(_i64), _i, _f, _i, _p, _p]),
+    "cc_gather_rows": (_i, [_p, _i64, _p, _p, _i64, _i64, _p]),
+    "cc_fold_scaling": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_decoder_stats": (_i, [_p, _i64, _i64, _i64, _i, _p, _p, _p, _p]),
     "cc_adam_step": (_i, [_p, _p, _p, _p, _i64, _p, _d, _d, _d, _d, _i64, _i64, _i, _p]),
 }
 

@@ -4,7 +4,8 @@
 from two (or more) models through their `run_with_cache` hook API, estimates the per-model
 norm-scaling factors (sqrt(d_model) / mean ||x||, buffer.py:44-63), keeps the buffer in HBM
 in enc_dtype, shuffles it on refresh and hands out batches.  The LM forward itself is the
-caller's model (out of scope for the kernels).  `next_raw()` is the zero-copy form used by
+caller's model (out of scope for the kernels); the shuffle is a GPU row gather (cc_gather_rows),
+so the buffer lives on a ROCm device.  `next_raw()` is the zero-copy form used by
 the fused Trainer: a [batch, n, d] slice of the HBM buffer plus the factors, which the
 prologue kernel (cc_prep_input) scales and casts in one pass.
 
@@ -15,6 +16,7 @@ import numpy as np
 import torch
 import tqdm
 
+from . import ops
 from .crosscoder import DTYPES
 
 
@@ -47,6 +49,7 @@ class Buffer(_BufferProtocol):
         self.first = True
         self.normalize = True
         self.all_tokens = all_tokens
+        self._spare = None
         factors = [self.estimate_norm_scaling_factor(cfg["model_batch_size"], m) for m in self.models]
         self.normalisation_factor = torch.tensor(factors, device=cfg["device"], dtype=self.dtype)
         self.refresh()
@@ -77,7 +80,15 @@ class Buffer(_BufferProtocol):
             self.buffer_pointer += acts.shape[0]
         self.token_pointer += num_batches
         self.buffer_pointer = 0
-        self.buffer = self.buffer[torch.randperm(self.buffer.shape[0]).to(self.buffer.device)]
+        # buffer = buffer[randperm(rows)] (buffer.py:111-113): the permutation from torch's global CPU
+        # generator exactly as the reference draws it, the row gather on the GPU (cc_gather_rows)
+        # into a second resident buffer; the two buffers swap roles every refresh
+        perm = torch.randperm(self.buffer.shape[0]).to(self.buffer.device)
+        spare = self._spare
+        if spare is None or spare.shape != self.buffer.shape or spare.dtype != self.buffer.dtype:
+            spare = torch.empty_like(self.buffer)
+        ops.gather_rows(self.buffer, perm, out=spare)
+        self._spare, self.buffer = self.buffer, spare
 
     def next_raw(self):
         B = self.cfg["batch_size"]

@@ -1,0 +1,175 @@
+// HBM-bound kernels around the training step: the activation buffer's shuffle
+// (Buffer.refresh, buffer.py:111-113), the activation-scale fold of the demo notebook
+// (fold_activation_scaling_factor, Crosscoder_model_diff.ipynb:35368-35378) and the decoder-norm
+// analytics of analysis.py:9-40.  gfx950; 16 B per lane everywhere.
+#include "cc_common.h"
+
+namespace cc {
+
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+
+// dst[i] = src[perm[i]] for rows of row_bytes (a multiple of 16).  One wave per destination row,
+// 16 B per lane, 4 rows per 256-thread block; the permutation entry is read once per wave.
+// An index outside [0, src_rows) yields a zero row (no out-of-bounds read).
+__global__ __launch_bounds__(256) void gather_rows_kernel(const char* __restrict__ src, int64_t src_rows,
+                                                          const int64_t* __restrict__ perm, char* __restrict__ dst,
+                                                          int64_t rows, int64_t row_bytes) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t s = perm[row];
+  const bool ok = s >= 0 && s < src_rows;
+  const u32x4_t* sp = (const u32x4_t*)(src + (ok ? s : 0) * row_bytes);
+  u32x4_t* dp = (u32x4_t*)(dst + row * row_bytes);
+  const int64_t n16 = row_bytes / 16;
+  int64_t c = lane;
+  for (; c + 64 < n16; c += 128) {  // two 16-B loads in flight per lane
+    const u32x4_t a = __builtin_nontemporal_load(sp + c), b = __builtin_nontemporal_load(sp + c + 64);
+    __builtin_nontemporal_store(ok ? a : u32x4_t{0, 0, 0, 0}, dp + c);
+    __builtin_nontemporal_store(ok ? b : u32x4_t{0, 0, 0, 0}, dp + c + 64);
+  }
+  if (c < n16) __builtin_nontemporal_store(ok ? __builtin_nontemporal_load(sp + c) : u32x4_t{0, 0, 0, 0}, dp + c);
+}
+
+// In place: W_enc[m] *= s[m], W_dec[:, m] /= s[m], b_dec[m] /= s[m] (W_dec / b_dec optional) with the parameter dtype's
+// rounding after each op (torch: dtype tensor * python float computes in fp32, rounds once).
+// W_enc / W_dec are [h][n*d] (W_enc's physical h-major layout), b_dec [n*d].  Thread -> 8 columns.
+template <int DT>
+__global__ __launch_bounds__(256) void fold_scaling_kernel(void* __restrict__ W_enc, void* __restrict__ W_dec,
+                                                           void* __restrict__ b_dec, const float* __restrict__ scale,
+                                                           int64_t h, int n, int d) {
+  using E = Elem<DT>;
+  const int64_t K = (int64_t)n * d;
+  const int64_t i8 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;  // element index in [h + 1][K]
+  if (i8 >= (h + 1) * K) return;
+  const int64_t row = i8 / K, col = i8 - row * K;
+  const float s = scale[col / d];
+  float v[8];
+  if (row < h) {
+    load8<DT>(W_enc, i8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = E::round(v[j] * s);
+    store8<DT>(W_enc, i8, v);
+    if (W_dec) {
+      load8<DT>(W_dec, i8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = E::round(v[j] / s);
+      store8<DT>(W_dec, i8, v);
+    }
+  } else if (b_dec) {  // the extra row: b_dec
+    load8<DT>(b_dec, col, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = E::round(v[j] / s);
+    store8<DT>(b_dec, col, v);
+  }
+}
+
+// Per latent (one wave): norms[h][m] = ||W_dec[h, m]||, relative[h] = norms[h][1] / sum_m norms[h][m],
+// cosine[h] = <W_dec[h,0], W_dec[h,1]> / (norms[h][0] * norms[h][1])  (analysis.py:9-12, 40).
+template <int DT>
+__global__ __launch_bounds__(256) void decoder_stats_kernel(const void* __restrict__ W, int64_t h, int n, int d,
+                                                            float* __restrict__ norms, float* __restrict__ relative,
+                                                            float* __restrict__ cosine) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= h) return;
+  const int64_t base = row * n * d;
+  float sq0 = 0.f, sq1 = 0.f, dot = 0.f;
+  for (int c = lane * 8; c < d; c += 512) {
+    float a[8], b[8];
+    load8<DT>(W, base + c, a);
+    if (n > 1) load8<DT>(W, base + d + c, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sq0 += a[j] * a[j];
+      if (n > 1) {
+        sq1 += b[j] * b[j];
+        dot += a[j] * b[j];
+      }
+    }
+  }
+  sq0 = wave_sum(sq0);
+  sq1 = wave_sum(sq1);
+  dot = wave_sum(dot);
+  const float n0 = sqrtf(sq0), n1 = sqrtf(sq1);
+  float tot = n0 + n1;
+  for (int m = 2; m < n; ++m) {  // further models: norms only
+    float s = 0.f;
+    for (int c = lane * 8; c < d; c += 512) {
+      float a[8];
+      load8<DT>(W, base + (int64_t)m * d + c, a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += a[j] * a[j];
+    }
+    s = sqrtf(wave_sum(s));
+    if (lane == 0) norms[row * n + m] = s;
+    tot += s;
+  }
+  if (lane == 0) {
+    norms[row * n] = n0;
+    if (n > 1) norms[row * n + 1] = n1;
+    if (relative) relative[row] = n > 1 ? n1 / tot : 0.f;
+    if (cosine) cosine[row] = n > 1 ? dot / (n0 * n1) : 0.f;
+  }
+}
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace cc
+
+using namespace cc;
+
+extern "C" {
+
+int cc_gather_rows(const void* src, int64_t src_rows, const int64_t* perm, void* dst, int64_t rows, int64_t row_bytes,
+                   void* stream) {
+  if (rows == 0) return CC_OK;  // (empty tensors may carry NULL data pointers)
+  if (rows < 0 || src_rows < 0 || row_bytes <= 0 || row_bytes % 16) return CC_ERR_SHAPE;
+  if (!src || !perm || !dst) return CC_ERR_NULL;
+  if (!al16(src) || !al16(dst)) return CC_ERR_ALIGN;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                     (const char*)src, src_rows, perm, (char*)dst, rows, row_bytes);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+int cc_fold_scaling(void* W_enc, void* W_dec, void* b_dec, const float* scale, int64_t h, int64_t n, int64_t d,
+                    int dtype, void* stream) {
+  if (!W_enc || !scale) return CC_ERR_NULL;
+  if (h <= 0 || n <= 0 || d <= 0 || d % 8) return CC_ERR_SHAPE;
+  if (!al16(W_enc) || (W_dec && !al16(W_dec)) || (b_dec && !al16(b_dec))) return CC_ERR_ALIGN;
+  const int64_t chunks = (h + 1) * n * d / 8;
+  dim3 grid((unsigned)((chunks + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == CC_BF16)
+    hipLaunchKernelGGL((fold_scaling_kernel<CC_BF16>), grid, dim3(256), 0, st, W_enc, W_dec, b_dec, scale, h, (int)n,
+                       (int)d);
+  else if (dtype == CC_F32)
+    hipLaunchKernelGGL((fold_scaling_kernel<CC_F32>), grid, dim3(256), 0, st, W_enc, W_dec, b_dec, scale, h, (int)n,
+                       (int)d);
+  else
+    return CC_ERR_DTYPE;
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+int cc_decoder_stats(const void* W_dec, int64_t h, int64_t n, int64_t d, int dtype, float* norms, float* relative,
+                     float* cosine, void* stream) {
+  if (!W_dec || !norms) return CC_ERR_NULL;
+  if (h <= 0 || n <= 0 || d <= 0 || d % 8) return CC_ERR_SHAPE;
+  if (!al16(W_dec)) return CC_ERR_ALIGN;
+  dim3 grid((unsigned)((h + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == CC_BF16)
+    hipLaunchKernelGGL((decoder_stats_kernel<CC_BF16>), grid, dim3(256), 0, st, W_dec, h, (int)n, (int)d, norms,
+                       relative, cosine);
+  else if (dtype == CC_F32)
+    hipLaunchKernelGGL((decoder_stats_kernel<CC_F32>), grid, dim3(256), 0, st, W_dec, h, (int)n, (int)d, norms,
+                       relative, cosine);
+  else
+    return CC_ERR_DTYPE;
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+}  // extern "C"

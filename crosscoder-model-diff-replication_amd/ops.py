@@ -201,3 +201,41 @@ def clip_finalize(sq, offsets, max_norm, emulate_bf16, out):
 def adam_step(p, g, m, v, coef, lr, beta1, beta2, eps, step, max_blocks=0):
     check(lib().cc_adam_step(_ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(coef), lr, beta1, beta2, eps,
                              int(step), int(max_blocks), dtype_code(p.dtype), _stream(p)))
+
+
+# ---------------------------------------------------------------- around the step
+def gather_rows(src, perm, out=None):
+    """out[i] = src[perm[i]] over dim 0 (Buffer.refresh's shuffle); perm int64 on the same device."""
+    _contig(src, "src")
+    if perm.dtype != torch.int64 or perm.device != src.device:
+        raise ValueError("perm must be an int64 tensor on the source's device")
+    rows = perm.numel()
+    if out is None:
+        out = torch.empty((rows,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+    _contig(out, "out")
+    row_bytes = src.element_size()
+    for s_ in src.shape[1:]:
+        row_bytes *= s_
+    check(lib().cc_gather_rows(_ptr(src), src.shape[0], _ptr(perm.contiguous()), _ptr(out), rows, row_bytes,
+                               _stream(src)))
+    return out
+
+
+def fold_scaling(W_enc_hk, W_dec_hk, b_dec_flat, scale, n, d):
+    """In place W_enc[m] *= s[m], W_dec[:, m] /= s[m], b_dec[m] /= s[m] (scale: fp32 device [n];
+    W_dec_hk / b_dec_flat may be None: encoder-only fold)."""
+    h = W_enc_hk.shape[0]
+    check(lib().cc_fold_scaling(_ptr(W_enc_hk), _ptr(W_dec_hk), _ptr(b_dec_flat), _ptr(scale), h, n, d,
+                                dtype_code(W_enc_hk.dtype), _stream(W_enc_hk)))
+
+
+def decoder_stats(W_dec_hk, n, d):
+    """norms [h, n], relative norms [h], cosine similarities [h] (fp32) of W_dec."""
+    h = W_dec_hk.shape[0]
+    dev = W_dec_hk.device
+    norms = torch.empty(h, n, device=dev, dtype=torch.float32)
+    rel = torch.empty(h, device=dev, dtype=torch.float32)
+    cos = torch.empty(h, device=dev, dtype=torch.float32)
+    check(lib().cc_decoder_stats(_ptr(W_dec_hk), h, n, d, dtype_code(W_dec_hk.dtype), _ptr(norms), _ptr(rel),
+                                 _ptr(cos), _stream(W_dec_hk)))
+    return norms, rel, cos

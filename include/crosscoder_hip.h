@@ -179,6 +179,27 @@ int cc_clip_finalize(const float* sq, const int64_t* off, int nparams, float max
 int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, double lr,
                  double beta1, double beta2, double eps, int64_t step, int64_t max_blocks, int dtype, void* stream);
 
+/* ---- around the step ---- */
+
+/* Buffer.refresh's shuffle (buffer.py:111-113: buffer = buffer[randperm(rows)]): dst[i] = src[perm[i]]
+ * for `rows` rows of `row_bytes` bytes (multiple of 16); perm: int64 device array (an index outside
+ * [0, src_rows) gives a zero row).  dst must not overlap src. */
+int cc_gather_rows(const void* src, int64_t src_rows, const int64_t* perm, void* dst, int64_t rows,
+                   int64_t row_bytes, void* stream);
+
+/* fold_activation_scaling_factor (Crosscoder_model_diff.ipynb:35368-35378), in place:
+ * W_enc[m] *= scale[m], W_dec[:, m] /= scale[m], b_dec[m] /= scale[m] (W_dec / b_dec may be NULL), each op
+ * rounded to the parameter dtype like torch.  W_enc / W_dec in their [h][n*d] physical layout;
+ * scale: n fp32 device values. */
+int cc_fold_scaling(void* W_enc, void* W_dec, void* b_dec, const float* scale, int64_t h, int64_t n, int64_t d,
+                    int dtype, void* stream);
+
+/* Decoder-norm analytics (analysis.py:9-12,40), one pass over W_dec [h][n][d]:
+ * norms[h*n + m] = ||W_dec[h,m]||; relative[h] = norms[h,1] / sum_m norms[h,m] (optional);
+ * cosine[h] = <W_dec[h,0], W_dec[h,1]> / (norms[h,0] norms[h,1]) (optional).  fp32 outputs. */
+int cc_decoder_stats(const void* W_dec, int64_t h, int64_t n, int64_t d, int dtype, float* norms, float* relative,
+                     float* cosine, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

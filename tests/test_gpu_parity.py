@@ -503,3 +503,95 @@ def test_decode_split_schedule(gpu, shape):
     if nws:
         col0 = 256 * (256 * waves // nbm)
         assert torch.equal(r_split[:, :col0], r_one[:, :col0])
+
+
+# ----------------------------------------------------------------------------- around the step (§8f)
+def test_buffer_matches_reference_with_fake_lms(gpu):
+    """Buffer (buffer.py:12-125) with deterministic fake LMs: normalisation factors and every next()
+    batch bit-identical to the reference's, across refreshes (the shuffle is cc_gather_rows)."""
+    import json
+    import os
+
+    from tests.test_cpu_host import FakeLM
+
+    r = torch.load(os.path.join("tests", "golden", "buffer_fake_lm.pt"), weights_only=True)
+    cfg = dict(json.loads(r["cfg"]), device=str(gpu))
+    torch.manual_seed(49)
+    buf = ca.Buffer(cfg, FakeLM(r["A_table"], r["A_pos"]), FakeLM(r["B_table"], r["B_pos"]), r["tokens"])
+    assert torch.equal(buf.normalisation_factor.cpu(), r["normalisation_factor"])
+    assert buf.buffer.shape[0] == r["buffer_size"] and buf.buffer.is_cuda
+    for want in r["next"]:
+        assert torch.equal(buf.next().cpu(), want)
+
+
+@pytest.mark.parametrize("rows,row_elems,dtype", [(523776 // 64, 2 * 2304, torch.bfloat16), (1000, 24, torch.float32),
+                                                  (7, 8, torch.bfloat16), (0, 8, torch.float32)])
+def test_gather_rows_matches_torch_indexing(gpu, rows, row_elems, dtype):
+    g = torch.Generator().manual_seed(rows + row_elems)
+    src = torch.randn(max(rows, 1), row_elems, generator=g).to(dtype).to(gpu)
+    perm = torch.randperm(rows, generator=g).to(gpu)
+    out = ops.gather_rows(src[:rows] if rows else src[:0], perm)
+    torch.cuda.synchronize()
+    assert torch.equal(out, src[:rows][perm])
+    # an out-of-range index gives a zero row, never a fault
+    if rows:
+        bad = perm.clone()
+        bad[0] = rows + 5
+        out2 = ops.gather_rows(src[:rows], bad)
+        torch.cuda.synchronize()
+        assert torch.equal(out2[0], torch.zeros_like(out2[0])) and torch.equal(out2[1:], src[:rows][perm[1:]])
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("fold_decoder", [True, False])
+def test_fold_activation_scaling_factor_matches_reference(gpu, dtype, fold_decoder):
+    """Crosscoder_model_diff.ipynb:35368-35378 (and the encoder-only variant :35752-35763) restated in
+    torch on the CPU vs cc_fold_scaling: bit-identical parameters."""
+    r = load(f"step_b64_n2_d32_h256_{dtype}")
+    cfg = dict(r["cfg"], device=str(gpu))
+    P = {k: v.clone() for k, v in r["init"].items()}
+    P["b_dec"] = (torch.randn(P["b_dec"].shape, generator=torch.Generator().manual_seed(1)) * 0.1).to(P["b_dec"].dtype)
+    cc = make_cc(cfg, P, gpu, 2)
+    base, chat = 0.2758961493232058, 0.24422852496546169
+    ca.fold_activation_scaling_factor(cc, base, chat, fold_decoder=fold_decoder)
+    ref = {k: v.clone() for k, v in P.items()}
+    ref["W_enc"][0] = ref["W_enc"][0] * base
+    ref["W_enc"][1] = ref["W_enc"][1] * chat
+    if fold_decoder:
+        ref["W_dec"][:, 0, :] = ref["W_dec"][:, 0, :] / base
+        ref["W_dec"][:, 1, :] = ref["W_dec"][:, 1, :] / chat
+        ref["b_dec"][0, :] = ref["b_dec"][0, :] / base
+        ref["b_dec"][1, :] = ref["b_dec"][1, :] / chat
+    sd = cc.state_dict()
+    for k in O.PARAM_ORDER:
+        assert torch.equal(sd[k].cpu(), ref[k]), k
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_decoder_stats_match_reference_analysis(gpu, dtype):
+    """analysis.py:9-40 (norms, relative norms, shared mask, cosine sims) vs an fp64 evaluation of the
+    same weights (fp32 results: rel <= 1e-5) and vs the reference's own dtype arithmetic."""
+    r = load(f"step_b64_n2_d32_h256_{dtype}")
+    cfg = dict(r["cfg"], device=str(gpu))
+    P = {k: v.clone() for k, v in r["init"].items()}
+    g = torch.Generator().manual_seed(2)
+    P["W_dec"] = (P["W_dec"].float() * (0.2 + torch.rand(P["W_dec"].shape[0], 2, 1, generator=g) * 2)).to(
+        P["W_dec"].dtype)
+    cc = make_cc(cfg, P, gpu, 2)
+    st = ca.decoder_stats(cc)
+    W = P["W_dec"].double()
+    norms = W.norm(dim=-1)
+    rel = norms[:, 1] / norms.sum(dim=-1)
+    cos = (W[:, 0, :] * W[:, 1, :]).sum(-1) / (W[:, 0, :].norm(dim=-1) * W[:, 1, :].norm(dim=-1))
+    assert rel_(st["norms"], norms) < 1e-5 and rel_(st["relative_norms"], rel) < 1e-5
+    assert rel_(st["cosine_sims"], cos) < 1e-5
+    assert torch.equal(st["shared_latent_mask"].cpu(), ((rel.float() < 0.7) & (rel.float() > 0.3)))
+    # the reference's own arithmetic in the parameter dtype (what analysis.py prints)
+    Wd = P["W_dec"]
+    ref_norms = Wd.norm(dim=-1)
+    tol = 1e-6 if dtype == "fp32" else 2 ** -7
+    assert ((st["norms"].cpu() - ref_norms.float()).abs() <= tol * ref_norms.float().abs() + 1e-7).all()
+
+
+def rel_(a, b):
+    return rel(a, b)
