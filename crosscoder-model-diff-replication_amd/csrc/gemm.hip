@@ -279,7 +279,10 @@ CC_DEV void tile_of_block(int bid, int nbm, int nbn, int& tm, int& tn) {
   int nwg = nbm * nbn;
   int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  constexpr int GM = 4;
+#ifndef CC_TILE_GM
+#define CC_TILE_GM 4
+#endif
+  constexpr int GM = CC_TILE_GM;
   int per_group = GM * nbn;
   int g = wg / per_group;
   int first = g * GM;

@@ -237,12 +237,18 @@ DEC_ADAM_BLOCKS = 256
 
 
 def clip_and_adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, max_norm=1.0, side_stream=None):
-    """clip_grad_norm_ + Adam.  side_stream: the decoder half's Adam (+ the next step's decoder
-    norms) runs there, so it overlaps the next step's encoder GEMM (G1 reads only the encoder half,
-    which Adam updates on torch's stream); P.pending orders every later decoder-half use
-    (forward() waits before the decoder norms; CrossCoder's methods wait; Trainer.synchronize())."""
+    """clip_grad_norm_ (from the squared-sum slabs of the backward) + Adam (see adam())."""
     emulate = ws.dtype == torch.bfloat16
     ops.clip_finalize(ws.sq, ws.sq_off, max_norm, emulate, ws.clip_out)
+    adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream)
+
+
+def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None):
+    """Adam with the clip coefficient in ws.clip_out[0].  side_stream: the decoder half's Adam (+ the
+    next step's decoder norms) runs there, so it overlaps the next step's encoder GEMM (G1 reads only
+    the encoder half, which Adam updates on torch's stream); P.pending orders every later
+    decoder-half use (forward() waits before the decoder norms; CrossCoder's methods wait;
+    Trainer.synchronize())."""
     if side_stream is None:
         with _span("adam"):
             ops.adam_step(P.data, G.data, M.data, V.data, ws.clip_out[0:1], lr, beta1, beta2, eps, step)

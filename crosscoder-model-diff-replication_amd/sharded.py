@@ -56,7 +56,9 @@ class ShardedStep:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
 
-    def step(self, raw, factor, l1c, lr, betas, eps, t, max_norm=1.0):
+    def step(self, raw, factor, l1c, lr, betas, eps, t, max_norm=1.0, on_losses=None):
+        """One step; on_losses(scalars) is called once the loss scalars are final on the device
+        (before the clip / Adam launches)."""
         b = self.b
         recon = b.forward_partial(raw, factor)
         chunks = b.row_chunks()
@@ -74,6 +76,8 @@ class ShardedStep:
         red[4:6] = scalars[1:3]
         dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
         scalars[1:3] = red[4:6]
+        if on_losses is not None:
+            on_losses(scalars)
         b.clip_and_adam_from_sums(red[0:4], lr, betas, eps, t, max_norm)
         return scalars
 
@@ -81,8 +85,9 @@ class ShardedStep:
 class HipShardBackend:
     """Local compute of one rank on its GPU (engine.py kernels)."""
 
-    def __init__(self, cc, recon_chunks=4):
+    def __init__(self, cc, recon_chunks=4, overlap_decoder_adam=True):
         self.cc = cc
+        self.side = torch.cuda.Stream(device=cc.arena().data.device) if overlap_decoder_adam else None
         a = cc.arena()
         self.G = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
         self.M = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
@@ -123,9 +128,8 @@ class HipShardBackend:
     def clip_and_adam_from_sums(self, sums, lr, betas, eps, t, max_norm):
         ws = self.ws
         ops.clip_finalize(sums, [0, 1, 2, 3, 4], max_norm, ws.dtype == torch.bfloat16, ws.clip_out)
-        with engine._span("adam"):
-            ops.adam_step(self.cc.arena().data, self.G.data, self.M.data, self.V.data, ws.clip_out[0:1], lr,
-                          betas[0], betas[1], eps, t)
+        # encoder half on this stream, decoder half + next step's norms on the side stream (engine.adam)
+        engine.adam(ws, self.cc.arena(), self.G, self.M, self.V, lr, betas[0], betas[1], eps, t, self.side)
 
 
 class ShardedTrainer:
@@ -152,6 +156,7 @@ class ShardedTrainer:
         self.step_counter = 0
         self.t = 0
         self.lr = cfg["lr"] * self.lr_lambda(0)
+        self._host = None
 
     def lr_lambda(self, step):
         if step < 0.8 * self.total_steps:
@@ -163,13 +168,27 @@ class ShardedTrainer:
             return self.cfg["l1_coeff"] * self.step_counter / (0.05 * self.total_steps)
         return self.cfg["l1_coeff"]
 
+    def _copy_losses(self, scalars):
+        # pinned landing buffer: the host waits for the losses only, not for clip / Adam
+        if self._host is None:
+            self._host = torch.empty(8, dtype=torch.float32, pin_memory=True)
+            self._copied = torch.cuda.Event()
+        self._host.copy_(scalars[:8], non_blocking=True)
+        self._copied.record()
+
+    def synchronize(self):
+        """Order torch's current stream after the last step's side-stream (decoder-half) Adam."""
+        self.crosscoder.arena().wait_pending()
+
     def step(self):
         raw, factor = self.buffer.next_raw()
         l1c = self.get_l1_coeff()
         self.t += 1
-        scalars = self.engine.step(raw, factor, l1c, self.lr, (self.cfg["beta1"], self.cfg["beta2"]), 1e-8, self.t)
+        self.engine.step(raw, factor, l1c, self.lr, (self.cfg["beta1"], self.cfg["beta2"]), 1e-8, self.t,
+                         on_losses=self._copy_losses)
         self.lr = self.cfg["lr"] * self.lr_lambda(self.t)
-        s = scalars[:6].tolist()
+        self._copied.synchronize()
+        s = self._host[:6].tolist()
         # the reference's l1 / EV_A / EV_B are param-dtype tensors (crosscoder.py:115-126): same rounding as Trainer.step
         dt = self.crosscoder.dtype
         rd = (lambda v: float(torch.tensor(v, dtype=dt))) if dt != torch.float32 else float
@@ -183,6 +202,7 @@ class ShardedTrainer:
     def gather_state_dict(self):
         """Full reference-layout state_dict on every rank (all_gather of the latent slices)."""
         a = self.crosscoder.arena()
+        a.wait_pending()
         out = {}
         for name, t in (("W_dec", a.W_dec_hk), ("W_enc", a.W_enc_hk), ("b_enc", a.b_enc)):
             parts = [torch.empty_like(t) for _ in range(self.world)]
