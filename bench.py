@@ -134,18 +134,23 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-sharded", action="store_true",
+                    help="diagnostic: run the latent-sharded step even on one rank (1-rank RCCL group)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    sharded_path = world > 1 or args.force_sharded
+    if sharded_path:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), rank=rank, world_size=world)
     h_total = H_LOCAL * world
     cfg = make_cfg(h_total, args.warmup + args.steps)
 
-    if world == 1:
+    if not sharded_path:
         cc = ca.CrossCoder(cfg)
         buf = ca.SyntheticBuffer(cfg, rows=B * 8, seed=0)
         tr = ca.Trainer(cfg, buffer=buf, crosscoder=cc)
@@ -171,18 +176,18 @@ def main():
     dom = max(gemms, key=gemms.get)
     engine.TIMER = timer
     timer.only = dom  # the roofline kernel, measured live inside the timed region
-    if world > 1:
+    if sharded_path:
         dist.barrier()
     timer.enabled = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         last = tr.step()
     torch.cuda.synchronize()
-    if world > 1:
+    if sharded_path:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     timer.enabled = False
-    if world > 1:
+    if sharded_path:
         t = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
@@ -234,7 +239,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline()
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if sharded_path:
         dist.destroy_process_group()
 
 

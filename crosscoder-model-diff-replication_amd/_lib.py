@@ -44,7 +44,8 @@ SIGNATURES = {
     "cc_decode_fwd_ws": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_loss_fwd_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i, _p]),
     "cc_loss_fwd_bwd_rows": (_i, [_p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i64, _i64, _i, _p]),
-    "cc_loss_finalize": (_i, [_p, _p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "cc_loss_finalize": (_i, [_p, _p, _i64, _p, _i64, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "cc_segment_sums": (_i, [_p, ctypes.POINTER(_i64), _i, _i, _p, _p]),
     "cc_dacts_bwd": (_i, [_p, _p, _p, _p, _f, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_dec": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_enc": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),

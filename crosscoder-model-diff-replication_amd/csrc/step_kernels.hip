@@ -249,7 +249,8 @@ constexpr int SCAL_THREADS = 1024;
 __global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const float* __restrict__ ev_part, int nblk,
                                                                     const float* __restrict__ l1_part, int64_t n_l1,
                                                                     const float* __restrict__ l0_part, int64_t n_wave,
-                                                                    int B, float* __restrict__ scalars) {
+                                                                    int B, float* __restrict__ scalars,
+                                                                    float* __restrict__ l1l0_out) {
   constexpr int NW = SCAL_THREADS / 64;
   __shared__ double red[NW][6];
   double acc[6] = {0, 0, 0, 0, 0, 0};
@@ -285,6 +286,7 @@ __global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const float*
     double s = 0.0;
     for (int w = 0; w < NW; ++w) s += red[w][q];
     scalars[q] = (float)(s / (double)B);
+    if (l1l0_out && (q == 1 || q == 2)) l1l0_out[q - 1] = (float)(s / (double)B);
   }
   if (threadIdx.x == 6) scalars[6] = 0.f;
   if (threadIdx.x == 7) scalars[7] = 0.f;
@@ -300,6 +302,8 @@ struct ClipArgs {
   float max_norm;
   int emulate_bf16;
   float* out;
+  int sums_only;   // cc_segment_sums: out[p] = the raw per-parameter sum (0 where zero_mask has bit p)
+  int zero_mask;
 };
 __global__ __launch_bounds__(SCAL_THREADS) void clip_kernel(const ClipArgs a) {
   constexpr int NW = SCAL_THREADS / 64;
@@ -330,6 +334,15 @@ __global__ __launch_bounds__(SCAL_THREADS) void clip_kernel(const ClipArgs a) {
     if ((threadIdx.x & 63) == 0) red[p][threadIdx.x >> 6] = t;
   }
   __syncthreads();
+  if (a.sums_only) {
+    if (threadIdx.x < a.nparams) {
+      const int p = threadIdx.x;
+      double t = 0.0;
+      for (int w = 0; w < NW; ++w) t += red[p][w];
+      a.out[p] = (a.zero_mask >> p) & 1 ? 0.f : (float)t;
+    }
+    return;
+  }
   if (threadIdx.x < a.nparams) {
     const int p = threadIdx.x;
     double t = 0.0;
@@ -592,8 +605,8 @@ int cc_loss_fwd_bwd(const float* recon_f32, const void* b_dec, const void* x, co
 }
 
 int cc_loss_finalize(const float* row_part, const float* l1_part, int64_t n_l1, const float* l0_part, int64_t n_l0,
-                     float* ev, float* ev_a, float* ev_b, float* scalars, int64_t B, int64_t n, int64_t d,
-                     void* stream) {
+                     float* ev, float* ev_a, float* ev_b, float* scalars, float* l1l0_out, int64_t B, int64_t n,
+                     int64_t d, void* stream) {
   if (!row_part || !scalars) return CC_ERR_NULL;
   if (B <= 0 || n <= 0 || d <= 0) return CC_ERR_SHAPE;
   // the per-block partials of the row terms use the tail of `scalars` (cc_loss_scalars_len)
@@ -603,7 +616,7 @@ int cc_loss_finalize(const float* row_part, const float* l1_part, int64_t n_l1, 
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(ev_kernel, dim3(nblk), dim3(256), 0, st, row_part, (int)B, (int)n, ncb, ev, ev_a, ev_b, ev_part);
   hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(SCAL_THREADS), 0, st, ev_part, nblk, l1_part, n_l1, l0_part,
-                     n_l0, (int)B, scalars);
+                     n_l0, (int)B, scalars, l1l0_out);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }
@@ -619,6 +632,21 @@ int cc_clip_finalize(const float* sq, const int64_t* off, int nparams, float max
   a.max_norm = max_norm;
   a.emulate_bf16 = emulate_bf16;
   a.out = out;
+  hipLaunchKernelGGL(clip_kernel, dim3(1), dim3(SCAL_THREADS), 0, (hipStream_t)stream, a);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+int cc_segment_sums(const float* sq, const int64_t* off, int nparams, int zero_mask, float* out, void* stream) {
+  if (!sq || !off || !out) return CC_ERR_NULL;
+  if (nparams <= 0 || nparams > 8) return CC_ERR_SHAPE;
+  ClipArgs a = {};
+  a.sq = sq;
+  for (int i = 0; i <= nparams; ++i) a.off[i] = off[i];
+  a.nparams = nparams;
+  a.out = out;
+  a.sums_only = 1;
+  a.zero_mask = zero_mask;
   hipLaunchKernelGGL(clip_kernel, dim3(1), dim3(SCAL_THREADS), 0, (hipStream_t)stream, a);
   CC_LAUNCH_CHECK();
   return CC_OK;

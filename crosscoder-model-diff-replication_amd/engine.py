@@ -191,9 +191,9 @@ def loss_rows(ws, P, r0, r1, grad_scale=None):
                      ws.n, ws.d, row0=r0, rows=r1 - r0)
 
 
-def loss_finalize(ws):
+def loss_finalize(ws, l1l0_out=None):
     ops.loss_finalize(ws.row_part, ws.l1_part, ws.n_l1, ws.l0_part, ws.n_wave, ws.ev, ws.ev_a, ws.ev_b, ws.scalars,
-                      ws.B, ws.n, ws.d)
+                      ws.B, ws.n, ws.d, l1l0_out=l1l0_out)
 
 
 def loss_from_recon(ws, P, grad_scale=None):

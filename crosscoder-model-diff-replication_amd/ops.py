@@ -158,9 +158,15 @@ def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_
                                      dtype_code(x.dtype), _stream(x)))
 
 
-def loss_finalize(row_part, l1_part, n_l1, l0_part, n_l0, ev, ev_a, ev_b, scalars, B, n, d):
+def loss_finalize(row_part, l1_part, n_l1, l0_part, n_l0, ev, ev_a, ev_b, scalars, B, n, d, l1l0_out=None):
     check(lib().cc_loss_finalize(_ptr(row_part), _ptr(l1_part), n_l1, _ptr(l0_part), n_l0, _ptr(ev), _ptr(ev_a),
-                                 _ptr(ev_b), _ptr(scalars), B, n, d, _stream(row_part)))
+                                 _ptr(ev_b), _ptr(scalars), _ptr(l1l0_out), B, n, d, _stream(row_part)))
+
+
+def segment_sums(sq, offsets, out, zero_mask=0):
+    """out[p] = sum(sq[offsets[p]:offsets[p+1]]) (0 where bit p of zero_mask is set)."""
+    arr = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
+    check(lib().cc_segment_sums(_ptr(sq), arr, len(offsets) - 1, int(zero_mask), _ptr(out), _stream(sq)))
 
 
 def dacts_bwd(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre, colsum_part=None):

@@ -57,8 +57,9 @@ class ShardedStep:
         self.world = dist.get_world_size(group)
 
     def step(self, raw, factor, l1c, lr, betas, eps, t, max_norm=1.0, on_losses=None):
-        """One step; on_losses(scalars) is called once the loss scalars are final on the device
-        (before the clip / Adam launches)."""
+        """One step -> (scalars, red): the loss scalars (l1 / l0 of this rank's latents only) and the
+        all-reduced [4 squared-gradient sums, l1, l0].  on_losses(scalars, red) is called once both
+        are final on the device (before the clip / Adam launches)."""
         b = self.b
         recon = b.forward_partial(raw, factor)
         chunks = b.row_chunks()
@@ -69,17 +70,14 @@ class ShardedStep:
         for (r0, r1), w in zip(chunks, works):
             w.wait()
             b.rows_ready(r0, r1, l1c)                # loss rows + g_recon + d_acts rows of the slice
-        scalars = b.loss_finalize()                  # [l2, l1_local, l0_local, ev, ev_a, ev_b, ...]
-        sums = b.backward(l1c)                       # [4] local squared sums
-        red = b.reduce_buffer()                      # [6]: 4 clip sums + l1, l0
-        red[0:4] = clip_sums_for_allreduce(sums, self.rank)
-        red[4:6] = scalars[1:3]
+        red = b.reduce_buffer()                      # [6]: 4 clip sums + l1, l0 (latent-local)
+        scalars = b.loss_finalize(red)               # [l2, l1, l0, ev, ev_a, ev_b, ...]; red[4:6] = local l1, l0
+        b.backward(l1c, red, self.rank)              # red[0:4] = local squared sums (b_dec on rank 0 only)
         dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
-        scalars[1:3] = red[4:6]
         if on_losses is not None:
-            on_losses(scalars)
+            on_losses(scalars, red)
         b.clip_and_adam_from_sums(red[0:4], lr, betas, eps, t, max_norm)
-        return scalars
+        return scalars, red
 
 
 class HipShardBackend:
@@ -92,7 +90,6 @@ class HipShardBackend:
         self.G = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
         self.M = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
         self.V = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
-        self.sums = torch.zeros(4, dtype=torch.float32, device=a.data.device)
         self.red = torch.zeros(6, dtype=torch.float32, device=a.data.device)
         self.recon_chunks = recon_chunks
         self.ws = None
@@ -111,16 +108,16 @@ class HipShardBackend:
         engine.loss_rows(self.ws, P, r0, r1)
         engine.dacts_rows(self.ws, P, l1c, r0, r1)
 
-    def loss_finalize(self):
-        engine.loss_finalize(self.ws)
+    def loss_finalize(self, red):
+        engine.loss_finalize(self.ws, l1l0_out=red[4:6])
         return self.ws.scalars
 
-    def backward(self, l1c):
+    def backward(self, l1c, red, rank):
         ws = self.ws
         engine.backward(ws, self.cc.arena(), self.G, l1c, dacts_done=True)
-        for i in range(4):
-            self.sums[i] = ws.sq_slice(i).sum()
-        return self.sums
+        # per-parameter squared sums straight into the all-reduce buffer; the replicated b_dec's
+        # counts on rank 0 only
+        ops.segment_sums(ws.sq, ws.sq_off, red[0:4], zero_mask=0 if rank == 0 else 1 << 3)
 
     def reduce_buffer(self):
         return self.red
@@ -168,12 +165,14 @@ class ShardedTrainer:
             return self.cfg["l1_coeff"] * self.step_counter / (0.05 * self.total_steps)
         return self.cfg["l1_coeff"]
 
-    def _copy_losses(self, scalars):
-        # pinned landing buffer: the host waits for the losses only, not for clip / Adam
+    def _copy_losses(self, scalars, red):
+        # pinned landing buffers: the host waits for the losses only, not for clip / Adam
         if self._host is None:
             self._host = torch.empty(8, dtype=torch.float32, pin_memory=True)
+            self._host_red = torch.empty(6, dtype=torch.float32, pin_memory=True)
             self._copied = torch.cuda.Event()
         self._host.copy_(scalars[:8], non_blocking=True)
+        self._host_red.copy_(red[:6], non_blocking=True)
         self._copied.record()
 
     def synchronize(self):
@@ -189,6 +188,7 @@ class ShardedTrainer:
         self.lr = self.cfg["lr"] * self.lr_lambda(self.t)
         self._copied.synchronize()
         s = self._host[:6].tolist()
+        s[1], s[2] = self._host_red[4:6].tolist()  # l1, l0 over all ranks' latents
         # the reference's l1 / EV_A / EV_B are param-dtype tensors (crosscoder.py:115-126): same rounding as Trainer.step
         dt = self.crosscoder.dtype
         rd = (lambda v: float(torch.tensor(v, dtype=dt))) if dt != torch.float32 else float

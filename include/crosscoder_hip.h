@@ -134,8 +134,9 @@ int cc_loss_fwd_bwd_rows(const float* recon_f32, const void* b_dec, const void* 
  * l1_part [n_l1] / l0_part [n_l0]: partial sums of B * l1 (cc_reduce_rows dot_part, or the per-wave
  * partials of cc_encode_fwd) and of the active count (cc_encode_fwd), scaled by 1/B (NULL -> 0). */
 int cc_loss_finalize(const float* row_part, const float* l1_part, int64_t n_l1, const float* l0_part, int64_t n_l0,
-                     float* ev, float* ev_a, float* ev_b, float* scalars, int64_t B, int64_t n, int64_t d,
-                     void* stream);
+                     float* ev, float* ev_a, float* ev_b, float* scalars, float* l1l0_out, int64_t B, int64_t n,
+                     int64_t d, void* stream);
+/* (l1l0_out, optional: a second copy of scalars[1:3] -- the latent-sharded step all-reduces it) */
 
 /* Backward through decode + L1 + ReLU (autograd of crosscoder.py:77,84-89,126):
  * g_pre[B,h] = (g_recon . W_dec^T + l1_scale * tn[h]) * (acts > 0),  l1_scale = l1_coeff / B.
@@ -169,6 +170,11 @@ int cc_wgrad_both(const void* acts, const void* g_recon, const void* W_dec, cons
  * out[0] = coef, out[1] = total norm, out[2 + i] = norm_i  (fp32, device). */
 int cc_clip_finalize(const float* sq, const int64_t* off, int nparams, float max_norm, int emulate_bf16,
                      float* out, void* stream);
+
+/* Per-parameter sums of the squared-gradient partials, sq[off[p] .. off[p+1]) (nparams <= 8, off on
+ * the HOST), for the latent-sharded step's all-reduce: out[p] = the sum (fp32), or 0 where bit p of
+ * zero_mask is set (a replicated parameter counted on one rank only). */
+int cc_segment_sums(const float* sq, const int64_t* off, int nparams, int zero_mask, float* out, void* stream);
 
 /* torch.optim.Adam step (trainer.py:16-20,47; torch/optim/adam.py single-tensor path, no weight
  * decay / amsgrad) fused with the clip multiply: g' = dtype(g * coef[0]); m, v, p updated in place

@@ -595,3 +595,14 @@ def test_decoder_stats_match_reference_analysis(gpu, dtype):
 
 def rel_(a, b):
     return rel(a, b)
+
+
+def test_segment_sums(gpu):
+    g = torch.Generator().manual_seed(4)
+    sq = torch.rand(5000, generator=g).to(gpu)
+    off = [0, 1000, 4100, 4200, 5000]
+    out = torch.empty(4, device=gpu)
+    ops.segment_sums(sq, off, out, zero_mask=1 << 3)
+    torch.cuda.synchronize()
+    ref = [sq[a:b].double().sum().item() for a, b in zip(off, off[1:])]
+    assert all(math.isclose(out[i].item(), ref[i], rel_tol=1e-6) for i in range(3)) and out[3].item() == 0.0

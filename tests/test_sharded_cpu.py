@@ -39,8 +39,10 @@ class CpuShardBackend:
     def reduce_buffer(self):
         return torch.zeros(6)
 
-    def loss_finalize(self):
-        return self.loss_from_full_recon()
+    def loss_finalize(self, red):
+        scalars = self.loss_from_full_recon()
+        red[4:6] = scalars[1:3]
+        return scalars
 
     def loss_from_full_recon(self):
         self.R = self.recon.clone().requires_grad_(True)
@@ -56,13 +58,14 @@ class CpuShardBackend:
         return torch.stack([self.l2.detach(), self.l1.detach(), l0, ev.mean().detach(), ev.mean().detach(),
                             ev.mean().detach()])
 
-    def backward(self, l1c):
+    def backward(self, l1c, red, rank):
         for p in self.P.values():
             p.grad = None
         gl2 = torch.autograd.grad(self.l2, [self.R, self.P["b_dec"]], retain_graph=True)
         (self.partial * gl2[0]).sum().add(l1c * self.l1).backward()
         self.P["b_dec"].grad = gl2[1]
-        return torch.stack([self.P[k].grad.pow(2).sum() for k in O.PARAM_ORDER])
+        sums = torch.stack([self.P[k].grad.pow(2).sum() for k in O.PARAM_ORDER])
+        red[0:4] = sharded.clip_sums_for_allreduce(sums, rank)
 
     def clip_and_adam_from_sums(self, sums, lr, betas, eps, t, max_norm):
         total = sums.sqrt().norm()
@@ -97,8 +100,8 @@ def _worker(rank, world, port, q):
         outs = []
         for t in range(STEPS):
             l1c = 2.0 if t else 0.0
-            s = step.step(raws[t], factor, l1c, cfg["lr"], (0.9, 0.999), 1e-8, t + 1)
-            outs.append(s[:3].clone())
+            s, red = step.step(raws[t], factor, l1c, cfg["lr"], (0.9, 0.999), 1e-8, t + 1)
+            outs.append(torch.stack([s[0], red[4], red[5]]).clone())
         q.put((rank, [o.tolist() for o in outs], {k: v.detach().clone() for k, v in backend.P.items()}))
     finally:
         dist.destroy_process_group()
