@@ -606,3 +606,50 @@ def test_segment_sums(gpu):
     torch.cuda.synchronize()
     ref = [sq[a:b].double().sum().item() for a, b in zip(off, off[1:])]
     assert all(math.isclose(out[i].item(), ref[i], rel_tol=1e-6) for i in range(3)) and out[3].item() == 0.0
+
+
+# ----------------------------------------------------------------------------- BASELINE configs 4 / 5 shapes
+@pytest.mark.parametrize("B,n,d,h", [(8192, 2, 3584, 8192),     # config 4 per-GPU shard (2x3584->65536 / 8)
+                                     (4096, 4, 2304, 32768)])   # config 5: 4x2304->32768 on one GPU
+def test_baseline_config_shapes_spot_check(gpu, B, n, d, h):
+    """One fused fwd+bwd at the BASELINE config shapes (bf16): sampled rows / latents of every
+    GEMM output checked against the oracle formulas evaluated in fp64 on the GPU's own bf16
+    inputs of that GEMM (size-independent: no error compounding across kernels)."""
+    cfg = {"seed": 7, "dict_size": h, "d_in": d, "enc_dtype": "bf16", "dec_init_norm": 0.08, "device": str(gpu),
+           "batch_size": B}
+    cc = ca.CrossCoder(cfg, n_models=n)
+    g = torch.Generator(device=gpu).manual_seed(3)
+    raw = (torch.randn(B, n, d, generator=g, device=gpu) * 3).to(torch.bfloat16)
+    factor = torch.full((n,), 0.35, device=gpu).to(torch.bfloat16)
+    ws = cc._workspace(B)
+    a = cc.arena()
+    G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+    engine.forward(ws, a, raw, factor)
+    engine.backward(ws, a, G, l1_coeff=2.0)
+    torch.cuda.synchronize()
+    K = n * d
+    gi = torch.Generator().manual_seed(B + h)
+    rows = torch.randint(0, B, (24,), generator=gi)
+    lat = torch.randint(0, h, (12,), generator=gi)
+    D = lambda t: t.double().cpu()  # noqa: E731
+    x, We, Wd, be = D(ws.x), D(a.W_enc_hk), D(a.W_dec_hk), D(a.b_enc)
+    acts, grec, gpre = D(ws.acts), D(ws.g_recon), D(ws.g_pre)
+    tn = Wd.view(h, n, d).norm(dim=-1).sum(-1)
+    # G1: acts rows
+    pre = x[rows] @ We.t() + be
+    assert rel(acts[rows], pre.clamp_min(0)) < 1e-2
+    # G2: fp32 partial reconstruction rows (split-K leftover columns included)
+    assert rel(D(ws.recon)[rows], acts[rows] @ Wd) < 1e-5
+    # G3: g_pre rows = (g_recon W_dec^T + l1c tn / B) * [acts > 0]
+    ref3 = (grec[rows] @ Wd.t() + 2.0 * tn / B) * (acts[rows] > 0)
+    assert rel(gpre[rows], ref3) < 1e-2
+    # G4: dW_dec latents = acts^T g_recon + l1c/B * colsum(acts) * W_dec / ||W_dec||
+    inv = 1.0 / Wd.view(h, n, d).norm(dim=-1)
+    l1t = (2.0 / B) * acts.sum(0)[lat, None, None] * Wd.view(h, n, d)[lat] * inv[lat, :, None]
+    ref4 = acts[:, lat].t() @ grec + l1t.reshape(len(lat), K)
+    assert rel(D(G.W_dec_hk)[lat], ref4) < 1e-2
+    # G5: dW_enc latents = g_pre^T x
+    assert rel(D(G.W_enc_hk)[lat], gpre[:, lat].t() @ x) < 1e-2
+    # bias gradients
+    assert rel(D(G.b_enc), gpre.sum(0)) < 1e-2
+    assert rel(D(G.b_dec_flat), grec.sum(0)) < 1e-2
