@@ -201,6 +201,8 @@ def main():
     dom_flop = gemm_flop * (2 if dom == "G4G5_wgrad" else 1)
     achieved = dom_flop / (dom_ms * 1e-3) / 1e12
     step_flop = 5 * gemm_flop
+    if engine.transposed_wgrad(B, N_MODELS * D_MODEL, H_LOCAL, torch.bfloat16):  # KC/KC form (cc_wgrad_both_t)
+        SPAN_KERNEL["G4G5_wgrad"] = "gemm_pp_dual_kernel<true, true, 4, 5>"
     traffic, traffic_src = pmc_traffic(dom)
     # algorithmic operand/output bytes of the dominant launch (each input read once, output written once)
     es = 2  # bf16

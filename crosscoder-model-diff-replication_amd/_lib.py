@@ -49,8 +49,13 @@ SIGNATURES = {
     "cc_dacts_bwd": (_i, [_p, _p, _p, _p, _f, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_dec": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_enc": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_wgrad_both_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_both": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_clip_finalize": (_i, [_p, ctypes.POINTER(_i64), _i, _f, _i, _p, _p]),
+    "cc_transposed_ok": (_i, [_i64, _i64, _i64, _i]),
+    "cc_encode_fwd_t": (_i, [_p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_dacts_bwd_t": (_i, [_p, _p, _p, _p, _f, _p, _i64, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_transpose_b16": (_i, [_p, _i64, _i64, _i64, _p, _i64, _p]),
     "cc_gather_rows": (_i, [_p, _i64, _p, _p, _i64, _i64, _p]),
     "cc_fold_scaling": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_decoder_stats": (_i, [_p, _i64, _i64, _i64, _i, _p, _p, _p, _p]),

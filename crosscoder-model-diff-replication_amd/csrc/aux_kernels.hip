@@ -113,6 +113,42 @@ __global__ __launch_bounds__(256) void decoder_stats_kernel(const void* __restri
   }
 }
 
+// dst[c][r] = src[r][c] for 16-bit elements (rows, cols % 8 == 0).  64 x 64 tiles: 16-B loads into
+// an LDS image [64 rows][128 B] (phys chunk = chunk ^ (row & 7)), read back column-wise with
+// ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane group -> lane i holds column i); two reads
+// give a lane 8 consecutive rows = one 16-B store of a transposed row.
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+__global__ __launch_bounds__(256) void transpose_b16_kernel(const char* __restrict__ src, int rows, int cols,
+                                                            int64_t ld_src, char* __restrict__ dst, int64_t ld_dst) {
+  __shared__ __attribute__((aligned(16))) char tile[64 * 128];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = threadIdx.x + 256 * k, r = idx >> 3, ch = idx & 7;
+    u32x4_t v = {0, 0, 0, 0};
+    if (r0 + r < rows && c0 + 8 * ch < cols)
+      v = __builtin_nontemporal_load((const u32x4_t*)(src + ((int64_t)(r0 + r) * ld_src + c0 + 8 * ch) * 2));
+    *(u32x4_t*)(tile + r * 128 + ((ch ^ (r & 7)) << 4)) = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int ca = 16 * w + 4 * p, ch = ca >> 3;  // address column of this lane
+  const int c = 16 * w + i;                      // column delivered to this lane
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int R = (4 * s + g) * 8;
+    const int l0 = R + q, l1 = R + 4 + q;
+    const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_bf16x4_t*)(tile + l0 * 128 + ((ch ^ (l0 & 7)) << 4) + (ca & 4) * 2));
+    const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_bf16x4_t*)(tile + l1 * 128 + ((ch ^ (l1 & 7)) << 4) + (ca & 4) * 2));
+    const bf16x8 v = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    if (c0 + c < cols && r0 + R < rows)
+      *(bf16x8*)(dst + ((int64_t)(c0 + c) * ld_dst + r0 + R) * 2) = v;
+  }
+}
+
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace cc
@@ -129,6 +165,20 @@ int cc_gather_rows(const void* src, int64_t src_rows, const int64_t* perm, void*
   if (!al16(src) || !al16(dst)) return CC_ERR_ALIGN;
   hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                      (const char*)src, src_rows, perm, (char*)dst, rows, row_bytes);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+int cc_transpose_b16(const void* src, int64_t rows, int64_t cols, int64_t ld_src, void* dst, int64_t ld_dst,
+                     void* stream) {
+  if (rows == 0 || cols == 0) return CC_OK;
+  if (rows < 0 || cols < 0 || rows % 8 || cols % 8 || ld_src < cols || ld_dst < rows || ld_src % 8 || ld_dst % 8 ||
+      rows / 64 >= 65535)
+    return CC_ERR_SHAPE;
+  if (!src || !dst) return CC_ERR_NULL;
+  if (!al16(src) || !al16(dst)) return CC_ERR_ALIGN;
+  hipLaunchKernelGGL(transpose_b16_kernel, dim3((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64)), dim3(256),
+                     0, (hipStream_t)stream, (const char*)src, (int)rows, (int)cols, ld_src, (char*)dst, ld_dst);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }

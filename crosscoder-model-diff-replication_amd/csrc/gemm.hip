@@ -58,6 +58,8 @@ struct GemmArgs {
   void* dbg;            // diagnostic stamp buffer (CC_STAMPS / CC_PP_STAMPS builds only)
   int stamp_base;       // first record of this GEMM in dbg (CC_PP_STAMPS)
   int k_step0, k_steps; // ping-pong split-K: contraction steps [k_step0, k_step0 + k_steps) (0 steps: all)
+  void* out_t;          // ping-pong bf16 epilogue: also store the tile transposed, out_t[n][m] (ld ldt)
+  int64_t ldt;
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -644,6 +646,12 @@ static bool use_pp(int64_t N, bool akc, bool bkc, int dtype) {
   return (g_pp_mask >> bit) & 1;
 }
 extern "C" void cc_debug_set_pp_mask(int mask) { g_pp_mask = mask; }
+// 1 when the transposed-operand entries (cc_encode_fwd_t, cc_dacts_bwd_t, cc_wgrad_both_t's fused
+// form) serve this step shape.
+extern "C" int cc_transposed_ok(int64_t B, int64_t K, int64_t h, int dtype) {
+  return dtype == CC_BF16 && B % 8 == 0 && K % 8 == 0 && h % 8 == 0 && use_pp(h, true, true, dtype) &&
+         use_pp(K, true, true, dtype);
+}
 static int pick_bn(int64_t N, bool akc, bool bkc, int dtype) {
   if (use_pp(N, akc, bkc, dtype)) return 256;
   return (!bkc && dtype == CC_BF16 && N % 288 == 0) ? 288 : 256;
@@ -758,6 +766,25 @@ int cc_encode_fwd(const void* x, const void* W_enc, const void* b_enc, const flo
   int rc = check_gemm(a, dtype, true, true);
   if (rc) return rc;
   return launch_dt<EPI_ENC, true, true>(dtype, a, (hipStream_t)stream);
+}
+
+// cc_encode_fwd that also stores acts transposed, acts_t [h][B] (the batch-contiguous operand of
+// the KC/KC weight-gradient GEMM, cc_wgrad_both_t).  bf16, B % 8 == 0, ping-pong path only.
+int cc_encode_fwd_t(const void* x, const void* W_enc, const void* b_enc, const float* tn, void* acts, void* acts_t,
+                    int apply_relu, float* colsum_part, float* l1_part, float* l0_part, int64_t B, int64_t K, int64_t h,
+                    int dtype, void* stream) {
+  if (!acts || !acts_t) return CC_ERR_NULL;
+  if (l1_part && !tn) return CC_ERR_NULL;
+  GemmArgs a = {};
+  a.A = x; a.lda = K; a.B = W_enc; a.ldb = K;
+  a.M = (int)B; a.N = (int)h; a.K = (int)K;
+  a.out = acts; a.ldo = h; a.bias = b_enc; a.tn = tn; a.flag = apply_relu;
+  a.col_part = colsum_part; a.wave_part0 = l1_part; a.wave_part1 = l0_part;
+  a.out_t = acts_t; a.ldt = B;
+  int rc = check_gemm(a, dtype, true, true);
+  if (rc) return rc;
+  if (B % 8 || !al16(acts_t) || !use_pp(a.N, true, true, dtype)) return CC_ERR_SHAPE;
+  return launch_pp<true, true, EPI_ENC>(a, (hipStream_t)stream);
 }
 
 int cc_decode_fwd(const void* acts, const void* W_dec, const void* b_dec, float* recon_f32, void* recon_t, int64_t B,
@@ -893,28 +920,49 @@ int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const
 
 }  // extern "C"
 
+extern "C" {
+// cc_dacts_bwd storing d pre-activations TRANSPOSED only: g_pre_t[j][b] for b < B (row stride ldt
+// >= B; a batch slice passes g_pre_t + r0).  bf16, B % 8 == 0, ldt % 8 == 0, ping-pong path only.
+int cc_dacts_bwd_t(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
+                   void* g_pre_t, int64_t ldt, float* colsum_part, int64_t B, int64_t K, int64_t h, int dtype,
+                   void* stream) {
+  if (!g_pre_t || !acts) return CC_ERR_NULL;
+  GemmArgs a = {};
+  a.A = g_recon; a.lda = K; a.B = W_dec; a.ldb = K;
+  a.M = (int)B; a.N = (int)h; a.K = (int)K;
+  a.out = nullptr; a.ldo = h; a.mask_src = acts; a.tn = tn; a.scale0 = l1_scale;
+  a.col_part = colsum_part; a.out_t = g_pre_t; a.ldt = ldt;
+  int rc = check_gemm(a, dtype, true, true);
+  if (rc) return rc;
+  if (B % 8 || ldt % 8 || ldt < B || !al16(g_pre_t) || !use_pp(a.N, true, true, dtype)) return CC_ERR_SHAPE;
+  return launch_pp<true, true, EPI_DACTS>(a, (hipStream_t)stream);
+}
+}  // extern "C"
+
+// tr: the batch-major operands are given transposed ([h][B] / [K][B], the contraction index B
+// contiguous): both GEMM operands are then KC (row-contiguous LDS images, ds_read_b128).
 static int wgrad_dec_args(GemmArgs& a, const void* acts, const void* g_recon, const void* W_dec, const float* inv_norms,
                           const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_part, int64_t B,
-                          int64_t h, int64_t n, int64_t d, int dtype) {
+                          int64_t h, int64_t n, int64_t d, int dtype, bool tr = false) {
   if (!grad_W_dec) return CC_ERR_NULL;
   if (l1_scale != 0.f && (!W_dec || !inv_norms || !colsum_acts)) return CC_ERR_NULL;
   a = GemmArgs{};
   int64_t K = n * d;
-  a.A = acts; a.lda = h; a.B = g_recon; a.ldb = K;
+  a.A = acts; a.lda = tr ? B : h; a.B = g_recon; a.ldb = tr ? B : K;
   a.M = (int)h; a.N = (int)K; a.K = (int)B;
   a.out = grad_W_dec; a.ldo = K; a.w_src = W_dec; a.norms = inv_norms; a.colsum = colsum_acts;
   a.scale0 = l1_scale; a.wave_part0 = sq_part; a.d_model = (int)d; a.n_models = (int)n;
-  return check_gemm(a, dtype, false, false);
+  return check_gemm(a, dtype, tr, tr);
 }
 
 static int wgrad_enc_args(GemmArgs& a, const void* g_pre, const void* x, void* grad_W_enc, float* sq_part, int64_t B,
-                          int64_t h, int64_t K, int dtype) {
+                          int64_t h, int64_t K, int dtype, bool tr = false) {
   if (!grad_W_enc) return CC_ERR_NULL;
   a = GemmArgs{};
-  a.A = g_pre; a.lda = h; a.B = x; a.ldb = K;
+  a.A = g_pre; a.lda = tr ? B : h; a.B = x; a.ldb = tr ? B : K;
   a.M = (int)h; a.N = (int)K; a.K = (int)B;
   a.out = grad_W_enc; a.ldo = K; a.wave_part0 = sq_part;
-  return check_gemm(a, dtype, false, false);
+  return check_gemm(a, dtype, tr, tr);
 }
 
 extern "C" {
@@ -935,6 +983,33 @@ int cc_wgrad_enc(const void* g_pre, const void* x, void* grad_W_enc, float* sq_p
   int rc = wgrad_enc_args(a, g_pre, x, grad_W_enc, sq_part, B, h, K, dtype);
   if (rc) return rc;
   return launch_dt<EPI_WGENC, false, false>(dtype, a, (hipStream_t)stream);
+}
+
+int cc_wgrad_both_t(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
+                    const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_preT,
+                    const void* xT, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
+                    int dtype, void* stream) {
+  GemmArgs a0, a1;
+  int rc = wgrad_dec_args(a0, actsT, g_reconT, W_dec, inv_norms, colsum_acts, l1_scale, grad_W_dec, sq_dec, B, h, n,
+                          d, dtype, true);
+  if (rc) return rc;
+  rc = wgrad_enc_args(a1, g_preT, xT, grad_W_enc, sq_enc, B, h, n * d, dtype, true);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (!use_pp(a0.N, true, true, dtype)) {
+    rc = launch_dt<EPI_WGDEC, true, true>(dtype, a0, st);
+    return rc ? rc : launch_dt<EPI_WGENC, true, true>(dtype, a1, st);
+  }
+  a0.nbm = a1.nbm = (a0.M + BM - 1) / BM;
+  a0.nbn = a1.nbn = (a0.N + 255) / 256;
+#ifdef CC_PP_STAMPS
+  a0.dbg = a1.dbg = g_stamp_buf;
+  a1.stamp_base = 4 * a0.nbm * a0.nbn;
+#endif
+  hipLaunchKernelGGL((gemm_pp_dual_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(2 * a0.nbm * a0.nbn), dim3(NTHR),
+                     0, st, a0, a1);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
 }
 
 int cc_wgrad_both(const void* acts, const void* g_recon, const void* W_dec, const float* inv_norms,

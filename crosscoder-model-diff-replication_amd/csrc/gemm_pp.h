@@ -117,6 +117,39 @@ CC_DEV uint32_t piece_off(int ci, int lane, int rows, int cols, int ldo) {
   return (row < rows && 8 * c < cols) ? (uint32_t)((row * ldo + 8 * c) * 2) : OOB;
 }
 
+// The tile image stored transposed: out_t[n0 + c][m0 + r] (row stride ldt; M % 8 == 0, so an
+// 8-row chunk is all in or all out).  ds_read_b64_tr_b16 turns 4 image rows x 16 columns into
+// 16 lanes x 4 rows; two of them give a lane 8 consecutive rows (16 B) of one column.  Wave w
+// writes transposed rows (tile columns) 32w .. 32w+31, 16 at a time; per store a row gets 64
+// contiguous bytes (lane groups g = 0..3 take row chunks 8g.. of a 32-row band), and a wave's 8
+// bands complete its 16 rows of 512 B.
+CC_DEV void pp_store_transposed(const GemmArgs& args, const char* smem, const int (&qb)[4], int m0, int n0, int rows,
+                                int cols, int lane, int wave) {
+  const int64_t ldt = args.ldt;
+  const __amdgpu_buffer_rsrc_t rt =
+      make_rsrc((const char*)args.out_t + ((int64_t)n0 * ldt + m0) * 2, ((uint64_t)(cols - 1) * ldt + rows) * 2);
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int c0 = wave * 32 + s * 16;
+    const int ca = c0 + 4 * p;  // address column of this lane
+    const int c = c0 + i;       // column delivered to this lane
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int r = t * 32 + g * 8;  // first of the lane's 8 rows
+      const int l0 = (r + q) & 63, l1 = (r + 4 + q) & 63;
+      const char* base = smem + qb[t >> 1] + (ca & 4) * 2;
+      const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_bf16x4*)(base + l0 * 512 + (((ca >> 3) ^ (l0 & 15)) << 4)));
+      const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_bf16x4*)(base + l1 * 512 + (((ca >> 3) ^ (l1 & 15)) << 4)));
+      const bf16x8 v = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const uint32_t off = (c < cols && r < rows) ? (uint32_t)(((int64_t)c * ldt + r) * 2) : OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rt, (int)off, 0, 0);
+    }
+  }
+}
+
 template <int EPI>
 CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char* smem, const int (&qb)[4],
                             bool input_staged, int tm, int m0, int n0, int wr, int wc, int lane, int wave,
@@ -145,14 +178,17 @@ CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char
   const LdsIO io(smem, qb, wr, wc, lane);
   epilogue_core<CC_BF16, EPI, 256>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, ecols, cw);
   __syncthreads();
-  const __amdgpu_buffer_rsrc_t rout = tile_rsrc(args.out, args.ldo, m0, n0, args.M, args.N, 2);
+  if (args.out) {
+    const __amdgpu_buffer_rsrc_t rout = tile_rsrc(args.out, args.ldo, m0, n0, args.M, args.N, 2);
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int ci = q * 8 + wave;
-    const bf16x8 v = *(const bf16x8*)(smem + qb[q >> 2] + (ci & 31) * 1024 + lane * 16);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout,
-                                           (int)piece_off(ci, lane, rows, cols, ldo), 0, 0);
+    for (int q = 0; q < 16; ++q) {
+      const int ci = q * 8 + wave;
+      const bf16x8 v = *(const bf16x8*)(smem + qb[q >> 2] + (ci & 31) * 1024 + lane * 16);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout,
+                                             (int)piece_off(ci, lane, rows, cols, ldo), 0, 0);
+    }
   }
+  if (args.out_t) pp_store_transposed(args, smem, qb, m0, n0, rows, cols, lane, wave);
 }
 
 constexpr int PP_LDS = 4 * 256 * 128;  // 2 buffers x (A | B) K-step images

@@ -131,6 +131,17 @@ def encode_fwd(x, W_enc_hk, b_enc, acts, apply_relu=True, tn=None, colsum_part=N
     return acts
 
 
+def encode_fwd_t(x, W_enc_hk, b_enc, acts, acts_t, apply_relu=True, tn=None, colsum_part=None, l1_part=None,
+                 l0_part=None):
+    """encode_fwd that also stores acts_t [h][B] = acts^T (bf16, B % 8 == 0)."""
+    B, K = x.shape
+    h = W_enc_hk.shape[0]
+    check(lib().cc_encode_fwd_t(_ptr(x), _ptr(W_enc_hk), _ptr(b_enc), _ptr(tn), _ptr(acts), _ptr(acts_t),
+                                int(apply_relu), _ptr(colsum_part), _ptr(l1_part), _ptr(l0_part), B, K, h,
+                                dtype_code(x.dtype), _stream(x)))
+    return acts
+
+
 def decode_fwd(acts, W_dec_hk, b_dec=None, recon_f32=None, recon_t=None):
     B, h = acts.shape
     K = W_dec_hk.shape[1]
@@ -176,6 +187,31 @@ def dacts_bwd(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre, colsum_part=None):
                              _ptr(colsum_part), B, K, h, dtype_code(g_recon.dtype), _stream(g_recon)))
 
 
+def dacts_bwd_t(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre_t, colsum_part=None):
+    """dacts_bwd storing g_pre transposed only: g_pre_t [h][>= B] view (column slice allowed, row stride
+    g_pre_t.stride(0))."""
+    B, K = g_recon.shape
+    h = W_dec_hk.shape[0]
+    if g_pre_t.shape[0] != h or g_pre_t.shape[1] != B or g_pre_t.stride(1) != 1:
+        raise ValueError("g_pre_t must be an [h, B] view with unit column stride")
+    check(lib().cc_dacts_bwd_t(_ptr(g_recon), _ptr(W_dec_hk), _ptr(acts), _ptr(tn), l1_scale, _ptr(g_pre_t),
+                               g_pre_t.stride(0), _ptr(colsum_part), B, K, h, dtype_code(g_recon.dtype),
+                               _stream(g_recon)))
+
+
+def transpose(src, out=None):
+    """out [cols, rows] = src^T for a 2-D 16-bit tensor (rows, cols % 8 == 0); out may be a column slice view."""
+    rows, cols = src.shape
+    if src.element_size() != 2 or src.stride(1) != 1:
+        raise ValueError("transpose: 2-D 16-bit tensor with unit column stride")
+    if out is None:
+        out = torch.empty(cols, rows, dtype=src.dtype, device=src.device)
+    if out.shape != (cols, rows) or out.stride(1) != 1 or out.dtype != src.dtype:
+        raise ValueError("transpose: out must be [cols, rows] of the same dtype, unit column stride")
+    check(lib().cc_transpose_b16(_ptr(src), rows, cols, src.stride(0), _ptr(out), out.stride(0), _stream(src)))
+    return out
+
+
 def wgrad_dec(acts, g_recon, W_dec_hk, norms, colsum_acts, l1_scale, grad, sq_part, n, d):
     B, h = acts.shape
     check(lib().cc_wgrad_dec(_ptr(acts), _ptr(g_recon), _ptr(W_dec_hk), _ptr(norms), _ptr(colsum_acts), l1_scale,
@@ -196,6 +232,15 @@ def wgrad_both(acts, g_recon, W_dec_hk, norms, colsum_acts, l1_scale, grad_dec, 
     check(lib().cc_wgrad_both(_ptr(acts), _ptr(g_recon), _ptr(W_dec_hk), _ptr(norms), _ptr(colsum_acts), l1_scale,
                               _ptr(grad_dec), _ptr(sq_dec), _ptr(g_pre), _ptr(x), _ptr(grad_enc), _ptr(sq_enc), B, h,
                               n, d, dtype_code(acts.dtype), _stream(acts)))
+
+
+def wgrad_both_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, grad_dec, sq_dec, g_preT, xT, grad_enc,
+                 sq_enc, n, d):
+    """wgrad_both from transposed batch operands (actsT / g_preT [h][B], g_reconT / xT [n*d][B]); same results."""
+    h, B = actsT.shape
+    check(lib().cc_wgrad_both_t(_ptr(actsT), _ptr(g_reconT), _ptr(W_dec_hk), _ptr(norms), _ptr(colsum_acts), l1_scale,
+                                _ptr(grad_dec), _ptr(sq_dec), _ptr(g_preT), _ptr(xT), _ptr(grad_enc), _ptr(sq_enc), B,
+                                h, n, d, dtype_code(actsT.dtype), _stream(actsT)))
 
 
 def clip_finalize(sq, offsets, max_norm, emulate_bf16, out):

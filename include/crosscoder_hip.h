@@ -99,6 +99,15 @@ int cc_encode_fwd(const void* x, const void* W_enc, const void* b_enc, const flo
                   int apply_relu, float* colsum_part, float* l1_part, float* l0_part, int64_t B, int64_t K,
                   int64_t h, int dtype, void* stream);
 
+/* 1 when cc_encode_fwd_t / cc_dacts_bwd_t / cc_wgrad_both_t serve a step of this shape and dtype. */
+int cc_transposed_ok(int64_t B, int64_t K, int64_t h, int dtype);
+
+/* cc_encode_fwd that also stores acts transposed, acts_t [h][B] (the batch-contiguous operand of
+ * cc_wgrad_both_t).  bf16 with B, K, h % 8 == 0 (else CC_ERR_SHAPE). */
+int cc_encode_fwd_t(const void* x, const void* W_enc, const void* b_enc, const float* tn, void* acts, void* acts_t,
+                    int apply_relu, float* colsum_part, float* l1_part, float* l0_part, int64_t B, int64_t K,
+                    int64_t h, int dtype, void* stream);
+
 /* CrossCoder.decode (crosscoder.py:82-89): recon = acts[B,h] . W_dec[h][K] (+ b_dec).
  * recon_f32 (optional): fp32 [B][K]; b_dec NULL -> partial sum without bias (latent-sharded use).
  * recon_t (optional): dtype [B][K] = dtype(acc + b_dec). */
@@ -144,6 +153,12 @@ int cc_loss_finalize(const float* row_part, const float* l1_part, int64_t n_l1, 
 int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
                  void* g_pre, float* colsum_part, int64_t B, int64_t K, int64_t h, int dtype, void* stream);
 
+/* cc_dacts_bwd writing g_pre TRANSPOSED only: g_pre_t[j][b], row stride ldt >= B (a batch slice
+ * [r0, r1) passes g_pre_t + r0 and B = r1 - r0).  bf16 with B, K, h, ldt % 8 == 0. */
+int cc_dacts_bwd_t(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
+                   void* g_pre_t, int64_t ldt, float* colsum_part, int64_t B, int64_t K, int64_t h, int dtype,
+                   void* stream);
+
 /* W_dec.grad [h][K] = acts^T . g_recon + l1_scale * sum_b(acts[:,h]) * W_dec[h,m,:]/||W_dec[h,m,:]||
  * (norm backward is 0 where the norm is 0; inv_norms from cc_dec_norms).
  * sq_part [cc_wgrad_parts(h,K,dtype)]: sum of grad^2. */
@@ -162,6 +177,14 @@ int cc_wgrad_both(const void* acts, const void* g_recon, const void* W_dec, cons
                   const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_pre,
                   const void* x, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
                   int dtype, void* stream);
+
+/* cc_wgrad_both with the batch-major operands TRANSPOSED: actsT / g_preT [h][B], g_reconT / xT [K][B]
+ * (the contraction index B contiguous), so both GEMMs read row-contiguous (KC) operand tiles.
+ * Same outputs as cc_wgrad_both (same k order per output element). */
+int cc_wgrad_both_t(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
+                    const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_preT,
+                    const void* xT, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
+                    int dtype, void* stream);
 
 /* clip_grad_norm_(params, max_norm) (trainer.py:46; torch/nn/utils/clip_grad.py): per-param
  * norms from the squared-sum partials sq[off[i] .. off[i+1]) (nparams <= 8, off on the HOST),
@@ -190,6 +213,11 @@ int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const 
 /* Buffer.refresh's shuffle (buffer.py:111-113: buffer = buffer[randperm(rows)]): dst[i] = src[perm[i]]
  * for `rows` rows of `row_bytes` bytes (multiple of 16); perm: int64 device array (an index outside
  * [0, src_rows) gives a zero row).  dst must not overlap src. */
+/* dst[c][r] = src[r][c] for 16-bit elements: src [rows][ld_src], dst [cols][ld_dst];
+ * rows, cols, ld_src, ld_dst % 8 == 0.  (The step's batch-contiguous copies x^T and g_recon^T.) */
+int cc_transpose_b16(const void* src, int64_t rows, int64_t cols, int64_t ld_src, void* dst, int64_t ld_dst,
+                     void* stream);
+
 int cc_gather_rows(const void* src, int64_t src_rows, const int64_t* perm, void* dst, int64_t rows,
                    int64_t row_bytes, void* stream);
 

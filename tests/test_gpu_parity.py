@@ -118,18 +118,22 @@ def test_wgrad_both_matches_separate(gpu, shape):
     colsum = acts.float().sum(0)
     parts = ops.wgrad_parts(h, K, bf)
     outs = []
-    for both in (False, True):
+    for both in (False, True, "T"):
         gd, ge = torch.empty(h, K, dtype=bf, device=gpu), torch.empty(h, K, dtype=bf, device=gpu)
         sd, se = torch.zeros(parts, device=gpu), torch.zeros(parts, device=gpu)
-        if both:
+        if both == "T":  # transposed (KC/KC) operands: same k order per output element -> same bits
+            T = lambda t: t.t().contiguous()  # noqa: E731
+            ops.wgrad_both_t(T(acts), T(g_recon), W, inv, colsum, 3e-4, gd, sd, T(g_pre), T(x), ge, se, n, d)
+        elif both:
             ops.wgrad_both(acts, g_recon, W, inv, colsum, 3e-4, gd, sd, g_pre, x, ge, se, n, d)
         else:
             ops.wgrad_dec(acts, g_recon, W, inv, colsum, 3e-4, gd, sd, n, d)
             ops.wgrad_enc(g_pre, x, ge, se)
         outs.append((gd, ge, sd, se))
     torch.cuda.synchronize()
-    for a, b in zip(*outs):
+    for a, b, c in zip(*outs):
         assert torch.equal(a, b)
+        assert torch.equal(a, c)
     ref = (acts.double().t() @ g_recon.double())
     assert rel(outs[1][0].double() - 3e-4 * colsum.double()[:, None] * (W.double().view(h, n, d) *
                inv.double()[:, :, None]).view(h, K), ref) < 1e-2
@@ -434,6 +438,75 @@ def test_sliced_loss_and_dacts_match_whole_batch(gpu, B):
                                          G.data, ws.sq)])
     for x, y in zip(*outs):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("B", [1024, 1000])
+def test_transposed_wgrad_step_matches_batch_major(gpu, B, monkeypatch):
+    """The step with batch-contiguous copies (x^T, acts^T, g_recon^T, g_pre^T; G4/G5 KC/KC) gives the
+    same gradients, partial sums and losses bit for bit as the batch-major MN/MN form."""
+    n, d, h = 2, 256, 1024
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16", seed=4,
+               device=str(gpu))
+    cc = ca.CrossCoder(cfg, n_models=n)
+    g = torch.Generator().manual_seed(10)
+    raw = (torch.randn(B, n, d, generator=g) * 3).to(gpu)
+    factor = torch.tensor([0.7, 1.3]).to(torch.bfloat16).to(gpu)
+    a = cc.arena()
+    outs = []
+    for tr in ("1", "0"):
+        monkeypatch.setenv("CC_TRANSPOSED_WGRAD", tr)
+        ws = engine.StepWorkspace(B, n, d, h, torch.bfloat16, gpu)
+        assert ws.tr == (tr == "1")
+        G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+        engine.forward(ws, a, raw, factor)
+        engine.backward(ws, a, G, 2.0)
+        torch.cuda.synchronize()
+        if ws.tr:  # the transposed copies are exact transposes
+            assert torch.equal(ws.x_t, ws.x.t()) and torch.equal(ws.acts_t, ws.acts.t())
+            assert torch.equal(ws.g_recon_t, ws.g_recon.t())
+        outs.append([t.clone() for t in (ws.acts, ws.g_recon, ws.g_pre, ws.scalars[:6], G.data, ws.sq)])
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("rows,cols,r0,c0", [(4096, 4608, 0, 0), (72, 136, 0, 0), (200, 64, 8, 16), (8, 8, 0, 0)])
+def test_transpose_b16(gpu, rows, cols, r0, c0):
+    """cc_transpose_b16 over a (possibly offset) sub-matrix into a column slice of a wider output."""
+    g = torch.Generator().manual_seed(rows * 7 + cols)
+    src = torch.randn(rows + r0, cols + c0 + 8, generator=g).to(torch.bfloat16).to(gpu)
+    view = src[r0:, c0:c0 + cols]
+    out = torch.full((cols, rows + 16), 7.0, dtype=torch.bfloat16, device=gpu)
+    ops.transpose(view, out=out[:, 8:8 + rows])
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, 8:8 + rows], view.t())
+    assert bool((out[:, :8] == 7).all()) and bool((out[:, 8 + rows:] == 7).all())  # nothing outside the slice
+
+
+@pytest.mark.parametrize("B,K,h", [(512, 768, 768), (1000, 80, 200), (4096, 4608, 2048)])
+def test_transposed_epilogue_outputs(gpu, B, K, h):
+    """cc_encode_fwd_t's acts_t and cc_dacts_bwd_t's g_pre_t (whole batch and a batch slice written
+    into its columns) are the exact transposes of cc_encode_fwd / cc_dacts_bwd's outputs."""
+    g = torch.Generator().manual_seed(B + K + h)
+    bf = torch.bfloat16
+    mk = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).to(bf).to(gpu)  # noqa: E731
+    x, W, b, Wd = mk(B, K), mk(h, K, sc=0.05), mk(h, sc=0.1), mk(h, K, sc=0.05)
+    g_recon = mk(B, K, sc=1e-2)
+    tn = torch.rand(h, generator=g).to(gpu) + 0.5
+    acts = torch.empty(B, h, dtype=bf, device=gpu)
+    acts2, acts_t = torch.empty_like(acts), torch.empty(h, B, dtype=bf, device=gpu)
+    ops.encode_fwd(x, W, b, acts, True)
+    ops.encode_fwd_t(x, W, b, acts2, acts_t, True)
+    g_pre = torch.empty(B, h, dtype=bf, device=gpu)
+    ops.dacts_bwd(g_recon, Wd, acts, tn, 3e-4, g_pre)
+    g_pre_t = torch.zeros(h, B, dtype=bf, device=gpu)
+    ops.dacts_bwd_t(g_recon, Wd, acts, tn, 3e-4, g_pre_t)
+    r0 = 256 if B > 256 else 0
+    g_pre_t2 = torch.zeros(h, B, dtype=bf, device=gpu)
+    ops.dacts_bwd_t(g_recon[r0:], Wd, acts[r0:], tn, 3e-4, g_pre_t2[:, r0:])
+    torch.cuda.synchronize()
+    assert torch.equal(acts, acts2) and torch.equal(acts_t, acts.t())
+    assert torch.equal(g_pre_t, g_pre.t())
+    assert torch.equal(g_pre_t2[:, r0:], g_pre[r0:].t()) and not bool(g_pre_t2[:, :r0].any())
 
 
 def test_sharded_trainer_world1_matches_trainer(gpu):

@@ -48,6 +48,10 @@ def main():
     gW2 = torch.empty(h, K, device=dev, dtype=bf)
     parts2 = torch.empty(1 << 20, device=dev)
     parts = torch.empty(1 << 20, device=dev)
+    # the transposed operands must carry the real G1 / G3 outputs (all-zero operands run at higher clocks)
+    acts.copy_(torch.relu(torch.randn(B, h, device=dev, generator=g)).to(bf))
+    g_pre.copy_((torch.randn(B, h, device=dev, generator=g) * 1e-3).to(bf))
+    actsT, grT, gpT, xT = acts.t().contiguous(), g_recon.t().contiguous(), g_pre.t().contiguous(), x.t().contiguous()
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     N0 = ctypes.c_void_p(0)
@@ -66,6 +70,9 @@ def main():
             "G5_wgrad_enc": lambda: L.cc_wgrad_enc(P(g_pre), P(x), P(gW), P(parts), B, h, K, 1, st),
             "G4G5_both_x0.5": lambda: L.cc_wgrad_both(P(acts), P(g_recon), P(W2), P(norms), P(colsum), 1e-4, P(gW),
                                                       P(parts), P(g_pre), P(x), P(gW2), P(parts2), B, h, n, d, 1, st),
+            "G4G5_both_T_x0.5": lambda: L.cc_wgrad_both_t(P(actsT), P(grT), P(W2), P(norms), P(colsum), 1e-4, P(gW),
+                                                          P(parts), P(gpT), P(xT), P(gW2), P(parts2), B, h, n, d, 1,
+                                                          st),
             "G5_on_G4_data": lambda: L.cc_wgrad_enc(P(acts), P(g_recon), P(gW), P(parts), B, h, K, 1, st),
         }
 
