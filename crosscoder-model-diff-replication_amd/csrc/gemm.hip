@@ -864,30 +864,42 @@ int64_t cc_decode_ws_floats(int64_t B, int64_t h, int64_t K, int dtype) {
   return (int64_t)p.nsplit * split_stride_of(B, p);
 }
 
-int cc_decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, float* ws, int64_t ws_floats, int64_t B,
-                     int64_t h, int64_t K, int dtype, void* stream) {
+}  // extern "C"
+
+// BKC: W_dec given transposed, W_dec_t [K][h] (both operands contract over h contiguously)
+template <bool BKC>
+static int decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, float* ws, int64_t ws_floats,
+                         int64_t B, int64_t h, int64_t K, int dtype, hipStream_t st) {
   if (!recon_f32) return CC_ERR_NULL;
   DecPlan p;
   const bool split = dec_plan(B, h, K, dtype, p);
-  if (!split) return cc_decode_fwd(acts, W_dec, nullptr, recon_f32, nullptr, B, h, K, dtype, stream);
+  const int64_t ldb = BKC ? h : K;
+  if (!split) {
+    GemmArgs a = {};
+    a.A = acts; a.lda = h; a.B = W_dec; a.ldb = ldb;
+    a.M = (int)B; a.N = (int)K; a.K = (int)h;
+    a.out_f32 = recon_f32; a.ldo = K;
+    int rc = check_gemm(a, dtype, true, BKC);
+    if (rc) return rc;
+    return launch_dt<EPI_DEC, true, BKC>(dtype, a, st);
+  }
   if (!ws) return CC_ERR_NULL;
   const int64_t split_stride = split_stride_of(B, p);
   if (ws_floats < (int64_t)p.nsplit * split_stride) return CC_ERR_SHAPE;
   if (((uintptr_t)ws & 15) || ((uintptr_t)recon_f32 & 15)) return CC_ERR_ALIGN;
-  hipStream_t st = (hipStream_t)stream;
   GemmArgs a = {};
-  a.A = acts; a.lda = h; a.B = W_dec; a.ldb = K;
+  a.A = acts; a.lda = h; a.B = W_dec; a.ldb = ldb;
   a.M = (int)B; a.N = p.nbn_main * 256; a.K = (int)h;
   a.out_f32 = recon_f32; a.ldo = K;
-  int rc = check_gemm(a, dtype, true, false);
+  int rc = check_gemm(a, dtype, true, BKC);
   if (rc) return rc;
 #ifdef CC_PP_STAMPS
   if (g_split_stamps_only) a.dbg = nullptr;
 #endif
-  rc = launch_pp<true, false, EPI_DEC>(a, st);  // whole waves
+  rc = launch_pp<true, BKC, EPI_DEC>(a, st);  // whole waves
   if (rc) return rc;
   GemmArgs t = {};
-  t.A = acts; t.lda = h; t.B = (const bf16_t*)W_dec + (int64_t)p.nbn_main * 256; t.ldb = K;
+  t.A = acts; t.lda = h; t.B = (const bf16_t*)W_dec + (int64_t)p.nbn_main * 256 * (BKC ? h : 1); t.ldb = ldb;
   t.M = (int)B; t.N = p.tail_cols; t.K = (int)h;
   t.out = ws; t.ldo = p.tail_cols;
   t.nbm = (t.M + BM - 1) / BM;
@@ -895,7 +907,7 @@ int cc_decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, floa
 #ifdef CC_PP_STAMPS
   t.dbg = g_stamp_buf;
 #endif
-  hipLaunchKernelGGL((gemm_pp_splitk_kernel<true, false>), dim3(p.nsplit * t.nbm * t.nbn), dim3(NTHR), 0, st, t,
+  hipLaunchKernelGGL((gemm_pp_splitk_kernel<true, BKC>), dim3(p.nsplit * t.nbm * t.nbn), dim3(NTHR), 0, st, t,
                      p.steps_per, p.nk, split_stride);
   CC_LAUNCH_CHECK();
   const int64_t threads = (int64_t)t.nbm * t.nbn * 8 * 32 * 64;
@@ -903,6 +915,18 @@ int cc_decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, floa
                      split_stride, t.M, t.N, t.nbm, t.nbn, recon_f32 + (int64_t)p.nbn_main * 256, (int64_t)K);
   CC_LAUNCH_CHECK();
   return CC_OK;
+}
+
+extern "C" {
+
+int cc_decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, float* ws, int64_t ws_floats, int64_t B,
+                     int64_t h, int64_t K, int dtype, void* stream) {
+  return decode_fwd_ws<false>(acts, W_dec, recon_f32, ws, ws_floats, B, h, K, dtype, (hipStream_t)stream);
+}
+
+int cc_decode_fwd_ws_t(const void* acts, const void* W_dec_t, float* recon_f32, float* ws, int64_t ws_floats,
+                       int64_t B, int64_t h, int64_t K, int dtype, void* stream) {
+  return decode_fwd_ws<true>(acts, W_dec_t, recon_f32, ws, ws_floats, B, h, K, dtype, (hipStream_t)stream);
 }
 
 int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,

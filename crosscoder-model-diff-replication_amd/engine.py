@@ -113,6 +113,8 @@ class StepWorkspace:
         self.norms = E(h, n)
         self.tn = E(h)
         self.acts = E(B, h, dt=dtype)
+        # W_dec^T [K][h]: G2 then reads both operands h-contiguous (refreshed with the decoder norms)
+        self.W_dec_t = E(K, h, dt=dtype) if self.tr else None
         self.acts_t = E(h, B, dt=dtype) if self.tr else None
         self.acts_colpart = E(ops.col_part_rows(B), h)
         self.colsum_acts = E(h)
@@ -171,8 +173,14 @@ def norms_for_next(ws, P):
     (clip_and_adam(side_stream=...) launches them on the side stream itself.)"""
     if ws.norms_token == _norms_token(P):
         return
-    ops.dec_norms(P.W_dec_hk, ws.h, ws.n, ws.d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
+    _decoder_derived(ws, P)
     ws.norms_token = _norms_token(P)
+
+
+def _decoder_derived(ws, P):
+    ops.dec_norms(P.W_dec_hk, ws.h, ws.n, ws.d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
+    if ws.tr:
+        ops.transpose(P.W_dec_hk, out=ws.W_dec_t)
 
 
 def decoder_norms(ws, P):
@@ -181,7 +189,7 @@ def decoder_norms(ws, P):
         ws.norms_token = None  # consumed: W_dec changes with this step's Adam
         return
     ws.norms_token = None
-    ops.dec_norms(P.W_dec_hk, ws.h, ws.n, ws.d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
+    _decoder_derived(ws, P)
 
 
 def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True):
@@ -207,7 +215,10 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts, dot_w=ws.tn,
                     dot_part=ws.l1_part)
     with _span("G2_decode"):
-        ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
+        if ws.tr:
+            ops.decode_partial_t(ws.acts, ws.W_dec_t, ws.recon, ws.dec_ws)
+        else:
+            ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
     if loss:
         loss_from_recon(ws, P, grad_scale)
 

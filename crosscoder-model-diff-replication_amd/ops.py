@@ -161,6 +161,14 @@ def decode_partial(acts, W_dec_hk, recon_f32, ws=None):
                                  0 if ws is None else ws.numel(), B, h, K, dtype_code(acts.dtype), _stream(acts)))
 
 
+def decode_partial_t(acts, W_dec_t, recon_f32, ws=None):
+    """decode_partial from the transposed decoder copy W_dec_t [K][h] (cc_decode_fwd_ws_t); same results."""
+    B, h = acts.shape
+    K = W_dec_t.shape[0]
+    check(lib().cc_decode_fwd_ws_t(_ptr(acts), _ptr(W_dec_t), _ptr(recon_f32), _ptr(ws),
+                                   0 if ws is None else ws.numel(), B, h, K, dtype_code(acts.dtype), _stream(acts)))
+
+
 def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_scale, B, n, d, row0=0, rows=None):
     """Loss terms + g_recon for batch rows [row0, row0 + rows) (default: all B rows)."""
     rows = B - row0 if rows is None else rows

@@ -123,6 +123,11 @@ int64_t cc_decode_ws_floats(int64_t B, int64_t h, int64_t K, int dtype);
 int cc_decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, float* ws, int64_t ws_floats, int64_t B,
                      int64_t h, int64_t K, int dtype, void* stream);
 
+/* cc_decode_fwd_ws with W_dec given transposed, W_dec_t [K][h] (a copy the optimizer keeps, see
+ * cc_adam_step_t): both operands then contract over h contiguously.  Same results. */
+int cc_decode_fwd_ws_t(const void* acts, const void* W_dec_t, float* recon_f32, float* ws, int64_t ws_floats,
+                       int64_t B, int64_t h, int64_t K, int dtype, void* stream);
+
 /* get_losses reconstruction terms + their backward (crosscoder.py:104-121, autograd):
  * r = recon_f32 + b_dec; g_recon = dtype(grad_scale * (r - x)) with grad_scale = 2/B.
  * row_part [2][n*cc_loss_col_blocks(d)][B]: [0] sum (r-x)^2, [1] sum (x - x_mean)^2 per

@@ -567,7 +567,10 @@ def test_decode_split_schedule(gpu, shape):
     r_one = torch.empty(B, K, device=gpu)
     ops.decode_partial(acts, W, r_split, ws)
     ops.decode_fwd(acts, W, None, recon_f32=r_one)
+    r_t = torch.empty(B, K, device=gpu)
+    ops.decode_partial_t(acts, W.t().contiguous(), r_t, ws)  # W_dec^T operand: same schedule, same bits
     torch.cuda.synchronize()
+    assert torch.equal(r_t, r_split)
     if (B, h, K) == (4096, 16384, 4608):
         assert nws == 8 * 4096 * 512  # 32 leftover tiles of 288 -> 8-way split
     ref = acts.double().cpu() @ W.double().cpu()
