@@ -35,6 +35,7 @@ SIGNATURES = {
     "cc_loss_scalars_len": (_i64, [_i64]),
     "cc_gemm_f32out": (_i, [_p, _i, _i64, _p, _i, _i64, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_prep_input": (_i, [_p, _i, _p, _i, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_prep_input_t": (_i, [_p, _i, _p, _i, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_reduce_rows": (_i, [_p, _i64, _i64, _i64, _f, _p, _p, _i, _p, _p, _p, _p]),
     "cc_reduce_parts": (_i64, [_i64]),
     "cc_dec_norms": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
@@ -45,7 +46,10 @@ SIGNATURES = {
     "cc_decode_fwd_ws_t": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_loss_fwd_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i, _p]),
     "cc_loss_fwd_bwd_rows": (_i, [_p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i64, _i64, _i, _p]),
+    "cc_loss_fwd_bwd_rows_t": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_loss_finalize": (_i, [_p, _p, _i64, _p, _i64, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "cc_loss_finalize_mapped": (_i, [_p, _p, _i64, _p, _i64, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _i64, _i64,
+                                     _i64, _p]),
     "cc_segment_sums": (_i, [_p, ctypes.POINTER(_i64), _i, _i, _p, _p]),
     "cc_dacts_bwd": (_i, [_p, _p, _p, _p, _f, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_dec": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
@@ -57,6 +61,8 @@ SIGNATURES = {
     "cc_encode_fwd_t": (_i, [_p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_dacts_bwd_t": (_i, [_p, _p, _p, _p, _f, _p, _i64, _p, _i64, _i64, _i64, _i, _p]),
     "cc_transpose_b16": (_i, [_p, _i64, _i64, _i64, _p, _i64, _p]),
+    "cc_dec_norms_part_floats": (_i64, [_i64, _i64, _i64]),
+    "cc_transpose_dec_norms": (_i, [_p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p]),
     "cc_gather_rows": (_i, [_p, _i64, _p, _p, _i64, _i64, _p]),
     "cc_fold_scaling": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_decoder_stats": (_i, [_p, _i64, _i64, _i64, _i, _p, _p, _p, _p]),

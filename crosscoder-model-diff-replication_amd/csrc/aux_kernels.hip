@@ -118,10 +118,16 @@ __global__ __launch_bounds__(256) void decoder_stats_kernel(const void* __restri
 // ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane group -> lane i holds column i); two reads
 // give a lane 8 consecutive rows = one 16-B store of a transposed row.
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+// NORMS: also the squared sum of each (row, 64-column block) of the source, in dec_norms_kernel's
+// order (8 sequential fma per lane, xor-1/2/4 butterfly over the 8 lanes of a block row), into
+// part[row][block] -- W_dec's decoder norms come out of the same HBM pass as W_dec^T.
+template <bool NORMS>
 __global__ __launch_bounds__(256) void transpose_b16_kernel(const char* __restrict__ src, int rows, int cols,
-                                                            int64_t ld_src, char* __restrict__ dst, int64_t ld_dst) {
+                                                            int64_t ld_src, char* __restrict__ dst, int64_t ld_dst,
+                                                            int rows_fast, float* __restrict__ part, int nblk) {
   __shared__ __attribute__((aligned(16))) char tile[64 * 128];
-  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  // rows_fast: consecutive blocks walk down the source rows (= along the destination rows)
+  const int r0 = (rows_fast ? blockIdx.x : blockIdx.y) * 64, c0 = (rows_fast ? blockIdx.y : blockIdx.x) * 64;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int idx = threadIdx.x + 256 * k, r = idx >> 3, ch = idx & 7;
@@ -129,6 +135,16 @@ __global__ __launch_bounds__(256) void transpose_b16_kernel(const char* __restri
     if (r0 + r < rows && c0 + 8 * ch < cols)
       v = __builtin_nontemporal_load((const u32x4_t*)(src + ((int64_t)(r0 + r) * ld_src + c0 + 8 * ch) * 2));
     *(u32x4_t*)(tile + r * 128 + ((ch ^ (r & 7)) << 4)) = v;
+    if constexpr (NORMS) {
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = __uint_as_float((j & 1 ? v[j >> 1] >> 16 : v[j >> 1] & 0xffffu) << 16);
+        q = __fmaf_rn(f, f, q);
+      }
+      q = block8_sum(q);
+      if (ch == 0 && r0 + r < rows) part[(int64_t)(r0 + r) * nblk + (c0 >> 6)] = q;
+    }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -147,6 +163,26 @@ __global__ __launch_bounds__(256) void transpose_b16_kernel(const char* __restri
     if (c0 + c < cols && r0 + R < rows)
       *(bf16x8*)(dst + ((int64_t)(c0 + c) * ld_dst + r0 + R) * 2) = v;
   }
+}
+
+// norms[r][m] = sqrt(sum of part[r][m*bpm .. (m+1)*bpm) in ascending order), total, inverses:
+// the rest of dec_norms_kernel from the per-block partials.  One thread per row.
+__global__ __launch_bounds__(256) void norms_finalize_kernel(const float* __restrict__ part, int h, int n, int bpm,
+                                                             float* __restrict__ norms, float* __restrict__ total,
+                                                             float* __restrict__ inv_norms) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= h) return;
+  const float* p = part + (int64_t)row * n * bpm;
+  float tot = 0.f;
+  for (int m = 0; m < n; ++m) {
+    float s = 0.f;
+    for (int b = 0; b < bpm; ++b) s += p[m * bpm + b];
+    const float nr = sqrtf(s);
+    norms[(int64_t)row * n + m] = nr;
+    if (inv_norms) inv_norms[(int64_t)row * n + m] = nr > 0.f ? 1.f / nr : 0.f;
+    tot += nr;
+  }
+  total[row] = tot;
 }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -169,16 +205,42 @@ int cc_gather_rows(const void* src, int64_t src_rows, const int64_t* perm, void*
   return CC_OK;
 }
 
+static int g_transpose_rows_fast = -1;  // -1: by shape
+void cc_debug_set_transpose_order(int rows_fast) { g_transpose_rows_fast = rows_fast; }
+
 int cc_transpose_b16(const void* src, int64_t rows, int64_t cols, int64_t ld_src, void* dst, int64_t ld_dst,
                      void* stream) {
   if (rows == 0 || cols == 0) return CC_OK;
   if (rows < 0 || cols < 0 || rows % 8 || cols % 8 || ld_src < cols || ld_dst < rows || ld_src % 8 || ld_dst % 8 ||
-      rows / 64 >= 65535)
+      rows / 64 >= 65535 || cols / 64 >= 65535)
     return CC_ERR_SHAPE;
   if (!src || !dst) return CC_ERR_NULL;
   if (!al16(src) || !al16(dst)) return CC_ERR_ALIGN;
-  hipLaunchKernelGGL(transpose_b16_kernel, dim3((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64)), dim3(256),
-                     0, (hipStream_t)stream, (const char*)src, (int)rows, (int)cols, ld_src, (char*)dst, ld_dst);
+  const unsigned nr = (unsigned)((rows + 63) / 64), nc = (unsigned)((cols + 63) / 64);
+  // measured (tools/transpose_bench.py): walking the source rows first is faster when rows >= cols
+  const int rf = g_transpose_rows_fast < 0 ? (rows >= cols) : g_transpose_rows_fast;
+  hipLaunchKernelGGL(transpose_b16_kernel<false>, rf ? dim3(nr, nc) : dim3(nc, nr), dim3(256), 0,
+                     (hipStream_t)stream, (const char*)src, (int)rows, (int)cols, ld_src, (char*)dst, ld_dst, rf,
+                     nullptr, 0);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+int64_t cc_dec_norms_part_floats(int64_t h, int64_t n, int64_t d) { return d % 64 ? 0 : h * n * (d / 64); }
+
+int cc_transpose_dec_norms(const void* W_dec, int64_t h, int64_t n, int64_t d, void* W_dec_t, float* part,
+                           float* norms, float* total, float* inv_norms, void* stream) {
+  if (!W_dec || !W_dec_t || !part || !norms || !total) return CC_ERR_NULL;
+  const int64_t K = n * d;
+  if (h <= 0 || n <= 0 || d <= 0 || d % 64 || h % 8 || h / 64 >= 65535 || K / 64 >= 65535) return CC_ERR_SHAPE;
+  if (!al16(W_dec) || !al16(W_dec_t)) return CC_ERR_ALIGN;
+  const unsigned nr = (unsigned)((h + 63) / 64), nc = (unsigned)(K / 64);
+  const int rf = g_transpose_rows_fast < 0 ? (h >= K) : g_transpose_rows_fast;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(transpose_b16_kernel<true>, rf ? dim3(nr, nc) : dim3(nc, nr), dim3(256), 0, st,
+                     (const char*)W_dec, (int)h, (int)K, K, (char*)W_dec_t, h, rf, part, (int)(K / 64));
+  hipLaunchKernelGGL(norms_finalize_kernel, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, st, part, (int)h, (int)n,
+                     (int)(d / 64), norms, total, inv_norms);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }

@@ -12,13 +12,47 @@ constexpr int LOSS_ROWS = 32;   // rows per loss block
 constexpr int LOSS_COLS = 512;  // columns per loss block (64 lanes x 8)
 
 // ---------------------------------------------------------------------------------------
+// Transposed copy of a block's [R rows][512 columns] bf16 output, staged in LDS: 16-B chunk c of
+// row r at r * 1024 + ((c ^ (r & 7)) << 4).  ds_read_b64_tr_b16 turns 4 rows x 16 columns into
+// 16 lanes x 4 rows; two of them give a lane 8 consecutive rows of one column (one 16-B store of
+// out_t[col0 + c][row0 + 8k ..]).  The batch-contiguous copies feed the weight-gradient GEMMs.
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_s;
+CC_DEV void tile_put8(char* lds, int r, int chunk, const float v[8]) {
+  bf16x8 b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[j] = (short)f2bf(v[j]);
+  *(bf16x8*)(lds + r * 1024 + ((chunk ^ (r & 7)) << 4)) = b;
+}
+template <int R>
+CC_DEV void tile_store_transposed(const char* lds, void* out_t, int64_t ldt, int64_t col0, int ncols, int64_t row0,
+                                  int nrows) {
+  constexpr int RQ = R / 32;  // 32-row bands
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  for (int it = wave; it < 32 * RQ; it += 4) {
+    const int cg = it / RQ, rb = (it % RQ) * 32 + g * 8;  // 16-column group, first of the lane's 8 rows
+    const int ca = cg * 16 + 4 * p, c = cg * 16 + i;
+    const int l0 = rb + q, l1 = rb + 4 + q;
+    const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_bf16x4_s*)(lds + l0 * 1024 + (((ca >> 3) ^ (l0 & 7)) << 4) + (ca & 4) * 2));
+    const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_bf16x4_s*)(lds + l1 * 1024 + (((ca >> 3) ^ (l1 & 7)) << 4) + (ca & 4) * 2));
+    if (c < ncols && rb < nrows)
+      *(bf16x8*)((bf16_t*)out_t + (col0 + c) * ldt + row0 + rb) =
+          bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // x_out = dtype(x_in * factor[model]);  colsum_part[rb][k] = sum over the block's rows.
 // grid: (ceil(K/512), ceil(B/64)); block 256 = 4 waves; lane -> 8 columns, wave -> 16 rows.
-template <int DIN, int DF, int DT>
+// TR (bf16 out): also x_t [K][B] = x_out^T through an LDS tile.
+template <int DIN, int DF, int DT, bool TR = false>
 __global__ __launch_bounds__(256) void prep_kernel(const void* __restrict__ x_in, const void* __restrict__ factor,
                                                    void* __restrict__ x_out, float* __restrict__ colsum_part, int B,
-                                                   int n, int d) {
+                                                   int n, int d, void* __restrict__ x_t) {
   __shared__ float red[4][512];
+  __shared__ __attribute__((aligned(16))) char tile[TR ? PREP_ROWS * 1024 : 16];
   const int K = n * d;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = blockIdx.x * 512 + lane * 8;
@@ -33,9 +67,15 @@ __global__ __launch_bounds__(256) void prep_kernel(const void* __restrict__ x_in
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = Elem<DT>::round(v[j] * f);
       store8<DT>(x_out, (int64_t)r * K + col, v);
+      if constexpr (TR) tile_put8(tile, r - r0, lane, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) cs[j] += v[j];
     }
+  }
+  if constexpr (TR) {
+    __syncthreads();
+    const int nr = B - r0 < PREP_ROWS ? B - r0 : PREP_ROWS;
+    tile_store_transposed<PREP_ROWS>(tile, x_t, B, (int64_t)blockIdx.x * 512, K - blockIdx.x * 512, r0, nr);
   }
   if (!colsum_part) return;
 #pragma unroll
@@ -99,6 +139,9 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
 
 // ---------------------------------------------------------------------------------------
 // norms[h][m] = ||W_dec[h,m,:]||, total[h] = sum_m.  One wave per (h) row, all models.
+// Summation order (shared with the fused W_dec^T transposition, cc_transpose_dec_norms, so both
+// give the same bits): per 64-column block, each of 8 lanes sums its 8 squares in order (fma),
+// the 8 lane sums combine by an xor-1/2/4 butterfly; block sums are added in ascending order.
 template <int DT>
 __global__ __launch_bounds__(256) void dec_norms_kernel(const void* __restrict__ W, float* __restrict__ norms,
                                                         float* __restrict__ total, float* __restrict__ inv_norms, int h,
@@ -109,22 +152,21 @@ __global__ __launch_bounds__(256) void dec_norms_kernel(const void* __restrict__
   float tot = 0.f;
   for (int m = 0; m < n; ++m) {
     const int64_t base = ((int64_t)row * n + m) * d;
-    float s0 = 0.f, s1 = 0.f;
-    int c = lane * 8;
-    for (; c + 512 < d; c += 1024) {  // two 16-B loads in flight per lane
-      float v[8], u[8];
-      load8<DT>(W, base + c, v);
-      load8<DT>(W, base + c + 512, u);
+    float s = 0.f;
+    for (int c0 = 0; c0 < d; c0 += 512) {  // 8 blocks of 64 columns per pass
+      const int c = c0 + lane * 8;
+      float q = 0.f;
+      if (c < d) {
+        float v[8];
+        load8<DT>(W, base + c, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { s0 += v[j] * v[j]; s1 += u[j] * u[j]; }
-    }
-    if (c < d) {
-      float v[8];
-      load8<DT>(W, base + c, v);
+        for (int j = 0; j < 8; ++j) q = __fmaf_rn(v[j], v[j], q);
+      }
+      q = block8_sum(q);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s0 += v[j] * v[j];
+      for (int g = 0; g < 8; ++g)
+        if (c0 + 64 * g < d) s += __shfl(q, 8 * g, 64);
     }
-    const float s = wave_sum(s0 + s1);
     const float nr = sqrtf(s);
     if (lane == 0) {
       norms[(int64_t)row * n + m] = nr;
@@ -141,13 +183,15 @@ __global__ __launch_bounds__(256) void dec_norms_kernel(const void* __restrict__
 // row range [row0, row_end) (row0 % 32 == 0).  The slabs keep the whole-batch layout, so disjoint
 // row ranges can be separate launches: the latent-sharded step runs each batch slice as soon as
 // its all-reduce has landed.  lane -> 8 columns; wave w -> rows r0 + w + 4i.
-template <int DT>
+// TR (bf16): also g_recon_t [K][B] = g_recon^T (rows [row0, row_end)) through an LDS tile.
+template <int DT, bool TR = false>
 __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ recon, const void* __restrict__ b_dec,
                                                    const void* __restrict__ x, const float* __restrict__ x_mean,
                                                    void* __restrict__ g_recon, float* __restrict__ row_part,
                                                    float* __restrict__ col_part, float grad_scale, int B, int n,
-                                                   int d, int ncb, int row0, int row_end) {
+                                                   int d, int ncb, int row0, int row_end, void* __restrict__ g_t) {
   __shared__ float red[4][512];
+  __shared__ __attribute__((aligned(16))) char tile[TR ? LOSS_ROWS * 1024 : 16];
   using E = Elem<DT>;
   const int K = n * d;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -182,6 +226,7 @@ __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ rec
         cs[j] += g[j];
       }
       store8<DT>(g_recon, (int64_t)r * K + col, g);
+      if constexpr (TR) tile_put8(tile, r - r0, lane, g);
     }
     l2 = wave_sum(l2);
     tv = wave_sum(tv);
@@ -189,6 +234,11 @@ __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ rec
       row_part[(int64_t)blockIdx.x * B + r] = l2;
       row_part[plane + (int64_t)blockIdx.x * B + r] = tv;
     }
+  }
+  if constexpr (TR) {
+    __syncthreads();
+    const int nr = row_end - r0 < LOSS_ROWS ? row_end - r0 : LOSS_ROWS;
+    tile_store_transposed<LOSS_ROWS>(tile, g_t, B, (int64_t)m * d + cb * LOSS_COLS, d - cb * LOSS_COLS, r0, nr);
   }
   if (!col_part) return;
 #pragma unroll
@@ -250,7 +300,8 @@ __global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const float*
                                                                     const float* __restrict__ l1_part, int64_t n_l1,
                                                                     const float* __restrict__ l0_part, int64_t n_wave,
                                                                     int B, float* __restrict__ scalars,
-                                                                    float* __restrict__ l1l0_out) {
+                                                                    float* __restrict__ l1l0_out,
+                                                                    float* __restrict__ host_out, unsigned seq) {
   constexpr int NW = SCAL_THREADS / 64;
   __shared__ double red[NW][6];
   double acc[6] = {0, 0, 0, 0, 0, 0};
@@ -287,9 +338,20 @@ __global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const float*
     for (int w = 0; w < NW; ++w) s += red[w][q];
     scalars[q] = (float)(s / (double)B);
     if (l1l0_out && (q == 1 || q == 2)) l1l0_out[q - 1] = (float)(s / (double)B);
+    if (host_out) host_out[q] = (float)(s / (double)B);
   }
-  if (threadIdx.x == 6) scalars[6] = 0.f;
-  if (threadIdx.x == 7) scalars[7] = 0.f;
+  if (threadIdx.x == 6 || threadIdx.x == 7) {
+    scalars[threadIdx.x] = 0.f;
+    if (host_out) host_out[threadIdx.x] = 0.f;
+  }
+  if (host_out) {
+    // mapped pinned host memory: the 8 values reach the host before the sequence word the host
+    // polls (no copy kernel, no event on the stream)
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store((unsigned*)(host_out + 8), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -522,6 +584,31 @@ int64_t cc_loss_col_blocks(int64_t d) { return (d + LOSS_COLS - 1) / LOSS_COLS; 
 int64_t cc_loss_scalars_len(int64_t B) { return 8 + 4 * ((B + 255) / 256); }
 int64_t cc_reduce_parts(int64_t C) { return (C + RED_COLS - 1) / RED_COLS; }
 
+int cc_prep_input_t(const void* x_in, int in_dtype, const void* factor, int factor_dtype, void* x_out, void* x_t,
+                    float* colsum_part, int64_t B, int64_t n, int64_t d, int dtype, void* stream) {
+  if (!x_t) return cc_prep_input(x_in, in_dtype, factor, factor_dtype, x_out, colsum_part, B, n, d, dtype, stream);
+  if (!x_in || !x_out) return CC_ERR_NULL;
+  if (B <= 0 || n <= 0 || d <= 0 || d % 8 || B % 8) return CC_ERR_SHAPE;
+  if (dtype != CC_BF16) return CC_ERR_DTYPE;
+  if (!al16(x_in) || !al16(x_out) || !al16(x_t)) return CC_ERR_ALIGN;
+  if (factor && factor_dtype != CC_BF16 && factor_dtype != CC_F32) return CC_ERR_DTYPE;
+  if (in_dtype != CC_BF16 && in_dtype != CC_F32) return CC_ERR_DTYPE;
+  dim3 grid((unsigned)((n * d + 511) / 512), (unsigned)cc_prep_part_rows(B));
+  hipStream_t st = (hipStream_t)stream;
+  const bool fb = factor && factor_dtype == CC_BF16;
+#define PREPT(DI, DF) \
+  hipLaunchKernelGGL((prep_kernel<DI, DF, CC_BF16, true>), grid, dim3(256), 0, st, x_in, factor, x_out, colsum_part, \
+                     (int)B, (int)n, (int)d, x_t)
+  if (in_dtype == CC_BF16) {
+    if (fb) PREPT(CC_BF16, CC_BF16); else PREPT(CC_BF16, CC_F32);
+  } else {
+    if (fb) PREPT(CC_F32, CC_BF16); else PREPT(CC_F32, CC_F32);
+  }
+#undef PREPT
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
 int cc_prep_input(const void* x_in, int in_dtype, const void* factor, int factor_dtype, void* x_out,
                   float* colsum_part, int64_t B, int64_t n, int64_t d, int dtype, void* stream) {
   if (!x_in || !x_out) return CC_ERR_NULL;
@@ -532,7 +619,7 @@ int cc_prep_input(const void* x_in, int in_dtype, const void* factor, int factor
   dim3 grid((unsigned)((n * d + 511) / 512), (unsigned)cc_prep_part_rows(B));
   hipStream_t st = (hipStream_t)stream;
 #define PREP(DI, DF, DO) \
-  hipLaunchKernelGGL((prep_kernel<DI, DF, DO>), grid, dim3(256), 0, st, x_in, factor, x_out, colsum_part, (int)B, (int)n, (int)d)
+  hipLaunchKernelGGL((prep_kernel<DI, DF, DO>), grid, dim3(256), 0, st, x_in, factor, x_out, colsum_part, (int)B, (int)n, (int)d, nullptr)
   int fdt = factor ? factor_dtype : CC_F32;
   if (dtype != CC_BF16 && dtype != CC_F32) return CC_ERR_DTYPE;
   if (in_dtype == CC_BF16) {
@@ -579,6 +666,28 @@ int cc_dec_norms(const void* W_dec, float* norms, float* total, float* inv_norms
   return CC_OK;
 }
 
+int cc_loss_fwd_bwd_rows_t(const float* recon_f32, const void* b_dec, const void* x, const float* x_mean,
+                           void* g_recon, void* g_recon_t, float* row_part, float* col_part, float grad_scale,
+                           int64_t row0, int64_t rows, int64_t B, int64_t n, int64_t d, int dtype, void* stream) {
+  if (!g_recon_t)
+    return cc_loss_fwd_bwd_rows(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_scale, row0, rows, B,
+                                n, d, dtype, stream);
+  if (!recon_f32 || !x || !g_recon || !row_part) return CC_ERR_NULL;
+  if (B <= 0 || n <= 0 || d <= 0 || d % 8 || B % 8 || rows % 8) return CC_ERR_SHAPE;
+  if (row0 < 0 || rows <= 0 || row0 + rows > B || row0 % LOSS_ROWS) return CC_ERR_SHAPE;
+  if (dtype != CC_BF16) return CC_ERR_DTYPE;
+  if (!al16(recon_f32) || !al16(x) || !al16(g_recon) || !al16(g_recon_t) || (b_dec && !al16(b_dec)) ||
+      (x_mean && !al16(x_mean)))
+    return CC_ERR_ALIGN;
+  int ncb = (int)cc_loss_col_blocks(d);
+  dim3 grid((unsigned)(n * ncb), (unsigned)cc_loss_part_rows(rows));
+  hipLaunchKernelGGL((loss_kernel<CC_BF16, true>), grid, dim3(256), 0, (hipStream_t)stream, recon_f32, b_dec, x,
+                     x_mean, g_recon, row_part, col_part, grad_scale, (int)B, (int)n, (int)d, ncb, (int)row0,
+                     (int)(row0 + rows), g_recon_t);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
 int cc_loss_fwd_bwd_rows(const float* recon_f32, const void* b_dec, const void* x, const float* x_mean,
                          void* g_recon, float* row_part, float* col_part, float grad_scale, int64_t row0,
                          int64_t rows, int64_t B, int64_t n, int64_t d, int dtype, void* stream) {
@@ -592,7 +701,7 @@ int cc_loss_fwd_bwd_rows(const float* recon_f32, const void* b_dec, const void* 
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_DT(dtype, hipLaunchKernelGGL((loss_kernel<DT_>), grid, dim3(256), 0, st, recon_f32, b_dec, x, x_mean,
                                         g_recon, row_part, col_part, grad_scale, (int)B, (int)n, (int)d, ncb,
-                                        (int)row0, (int)(row0 + rows)));
+                                        (int)row0, (int)(row0 + rows), nullptr));
   CC_LAUNCH_CHECK();
   return CC_OK;
 }
@@ -607,6 +716,13 @@ int cc_loss_fwd_bwd(const float* recon_f32, const void* b_dec, const void* x, co
 int cc_loss_finalize(const float* row_part, const float* l1_part, int64_t n_l1, const float* l0_part, int64_t n_l0,
                      float* ev, float* ev_a, float* ev_b, float* scalars, float* l1l0_out, int64_t B, int64_t n,
                      int64_t d, void* stream) {
+  return cc_loss_finalize_mapped(row_part, l1_part, n_l1, l0_part, n_l0, ev, ev_a, ev_b, scalars, l1l0_out, nullptr,
+                                 0, B, n, d, stream);
+}
+
+int cc_loss_finalize_mapped(const float* row_part, const float* l1_part, int64_t n_l1, const float* l0_part,
+                            int64_t n_l0, float* ev, float* ev_a, float* ev_b, float* scalars, float* l1l0_out,
+                            float* host_out, uint32_t seq, int64_t B, int64_t n, int64_t d, void* stream) {
   if (!row_part || !scalars) return CC_ERR_NULL;
   if (B <= 0 || n <= 0 || d <= 0) return CC_ERR_SHAPE;
   // the per-block partials of the row terms use the tail of `scalars` (cc_loss_scalars_len)
@@ -616,7 +732,7 @@ int cc_loss_finalize(const float* row_part, const float* l1_part, int64_t n_l1, 
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(ev_kernel, dim3(nblk), dim3(256), 0, st, row_part, (int)B, (int)n, ncb, ev, ev_a, ev_b, ev_part);
   hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(SCAL_THREADS), 0, st, ev_part, nblk, l1_part, n_l1, l0_part,
-                     n_l0, (int)B, scalars, l1l0_out);
+                     n_l0, (int)B, scalars, l1l0_out, host_out, (unsigned)seq);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }

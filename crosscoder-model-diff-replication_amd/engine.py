@@ -6,8 +6,9 @@ Data layout in HBM (one arena per role, all views of single allocations):
   x [B][K], acts [B][h], g_recon [B][K], g_pre [B][h] (dtype); recon [B][K] fp32.
   bf16 (transposed_wgrad): also x^T [K][B], acts^T [h][B], g_recon^T [K][B], and g_pre only as
   g_pre^T [h][B] -- G4/G5 contract over the batch, so these make both of their operands
-  row-contiguous.  acts^T / g_pre^T come from G1's / G3's epilogue, x^T / g_recon^T from a
-  transpose kernel.
+  row-contiguous.  acts^T / g_pre^T come from G1's / G3's epilogues, x^T / g_recon^T from the
+  prep / loss kernels (LDS-staged transposed stores), W_dec^T [K][h] (for G2) from the pass that
+  computes the decoder norms after Adam.
 W_enc's logical shape is [n, d, h] with strides (d, 1, K) exactly like the reference's
 rearranged view (crosscoder.py:55-58), so both weight matrices are [h][K] row-major and
 every GEMM streams 128-byte rows.
@@ -115,6 +116,8 @@ class StepWorkspace:
         self.acts = E(B, h, dt=dtype)
         # W_dec^T [K][h]: G2 then reads both operands h-contiguous (refreshed with the decoder norms)
         self.W_dec_t = E(K, h, dt=dtype) if self.tr else None
+        npart = ops.dec_norms_part_floats(h, n, d) if self.tr else 0
+        self.norm_part = E(npart) if npart else None  # fused W_dec^T + norms pass (d % 64 == 0)
         self.acts_t = E(h, B, dt=dtype) if self.tr else None
         self.acts_colpart = E(ops.col_part_rows(B), h)
         self.colsum_acts = E(h)
@@ -147,6 +150,8 @@ class StepWorkspace:
         self.sq = E(self.sq_off[-1])
         self.clip_out = E(8)
         self.norms_token = None
+        self.host = None  # _hip.MappedHostBuffer for the loss scalars (Trainer), or None
+        self.host_seq = 0
 
     def sq_slice(self, i):
         return self.sq[self.sq_off[i]:self.sq_off[i + 1]]
@@ -168,8 +173,8 @@ def _norms_token(P):
 
 
 def norms_for_next(ws, P):
-    """Launch the next step's decoder norms now (right after Adam wrote W_dec), so they run while
-    the host turns this step's loss scalars into the loss dict; forward() then skips them.
+    """Launch the next step's decoder norms (and W_dec^T) now, right after Adam wrote W_dec, so they
+    run while the host turns this step's loss scalars into the loss dict; forward() then skips them.
     (clip_and_adam(side_stream=...) launches them on the side stream itself.)"""
     if ws.norms_token == _norms_token(P):
         return
@@ -178,9 +183,12 @@ def norms_for_next(ws, P):
 
 
 def _decoder_derived(ws, P):
-    ops.dec_norms(P.W_dec_hk, ws.h, ws.n, ws.d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
+    if ws.norm_part is not None:  # W_dec^T and the norms from one pass over W_dec
+        ops.transpose_dec_norms(P.W_dec_hk, ws.n, ws.d, ws.W_dec_t, ws.norm_part, ws.norms, ws.tn, ws.inv_norms)
+        return
     if ws.tr:
         ops.transpose(P.W_dec_hk, out=ws.W_dec_t)
+    ops.dec_norms(P.W_dec_hk, ws.h, ws.n, ws.d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
 
 
 def decoder_norms(ws, P):
@@ -197,11 +205,9 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     fp32/bf16, factor [n] or None.  Leaves losses in ws.scalars / ws.ev*, g_recon ready
     (loss=False: stops at the fp32 reconstruction, for loss_rows / loss_finalize by slices)."""
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
-    ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart)
+    ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart, out_t=ws.x_t)
     ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
     # G1 reads only the encoder half: it may overlap the previous step's decoder-half Adam
-    if ws.tr:
-        ops.transpose(ws.x, out=ws.x_t)
     with _span("G1_encode"):
         if ws.tr:
             ops.encode_fwd_t(ws.x, P.W_enc_hk, P.b_enc, ws.acts, ws.acts_t, True, colsum_part=ws.acts_colpart,
@@ -210,15 +216,15 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
             ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, colsum_part=ws.acts_colpart,
                            l0_part=ws.l0_part)
     P.wait_pending()
-    decoder_norms(ws, P)
-    # sum_b acts (for dL1/dW_dec) and B * l1 = sum_h colsum_acts[h] * tn[h] (crosscoder.py:126)
-    ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts, dot_w=ws.tn,
-                    dot_part=ws.l1_part)
+    decoder_norms(ws, P)  # (+ W_dec^T), unless launched already after the last Adam
     with _span("G2_decode"):
         if ws.tr:
             ops.decode_partial_t(ws.acts, ws.W_dec_t, ws.recon, ws.dec_ws)
         else:
             ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
+    # sum_b acts (for dL1/dW_dec) and B * l1 = sum_h colsum_acts[h] * tn[h] (crosscoder.py:126)
+    ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts, dot_w=ws.tn,
+                    dot_part=ws.l1_part)
     if loss:
         loss_from_recon(ws, P, grad_scale)
 
@@ -227,14 +233,16 @@ def loss_rows(ws, P, r0, r1, grad_scale=None):
     """Loss row terms + g_recon for batch rows [r0, r1) (r0 % 32 == 0); slabs keep the batch layout."""
     gs = 2.0 / ws.B if grad_scale is None else grad_scale
     ops.loss_fwd_bwd(ws.recon, P.b_dec_flat, ws.x, ws.x_mean, ws.g_recon, ws.row_part, ws.loss_colpart, gs, ws.B,
-                     ws.n, ws.d, row0=r0, rows=r1 - r0)
-    if ws.tr:
-        ops.transpose(ws.g_recon[r0:r1], out=ws.g_recon_t[:, r0:r1])
+                     ws.n, ws.d, row0=r0, rows=r1 - r0, g_recon_t=ws.g_recon_t)
 
 
 def loss_finalize(ws, l1l0_out=None):
+    """Loss scalars / EV vectors; with ws.host (a mapped host buffer, set by the Trainer) the
+    scalars also land in host memory followed by the sequence word ws.host_seq."""
+    if ws.host is not None:
+        ws.host_seq = (ws.host_seq + 1) & 0xFFFFFFFF or 1
     ops.loss_finalize(ws.row_part, ws.l1_part, ws.n_l1, ws.l0_part, ws.n_wave, ws.ev, ws.ev_a, ws.ev_b, ws.scalars,
-                      ws.B, ws.n, ws.d, l1l0_out=l1l0_out)
+                      ws.B, ws.n, ws.d, l1l0_out=l1l0_out, host=ws.host, seq=ws.host_seq)
 
 
 def loss_from_recon(ws, P, grad_scale=None):

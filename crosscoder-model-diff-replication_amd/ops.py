@@ -89,15 +89,22 @@ def gemm_f32out(A, a_layout, Bm, b_layout, M, N, K, out=None):
     return out
 
 
-def prep_input(x_in, factor, dtype, out=None, colsum_part=None):
-    """x_out[B, n*d] = dtype(x_in * factor[model]) (Buffer.next normalisation + get_losses cast)."""
+def prep_input(x_in, factor, dtype, out=None, colsum_part=None, out_t=None):
+    """x_out[B, n*d] = dtype(x_in * factor[model]) (Buffer.next normalisation + get_losses cast);
+    out_t (optional, bf16): also x_out^T [n*d, B]."""
     B, n, d = x_in.shape
     _contig(x_in, "x")
     if out is None:
         out = torch.empty(B, n * d, device=x_in.device, dtype=dtype)
     fdt = dtype_code(factor.dtype) if factor is not None else CC_F32
-    check(lib().cc_prep_input(_ptr(x_in), dtype_code(x_in.dtype), _ptr(factor), fdt, _ptr(out),
-                              _ptr(colsum_part), B, n, d, dtype_code(dtype), _stream(x_in)))
+    if out_t is not None:
+        if out_t.shape != (n * d, B) or not out_t.is_contiguous():
+            raise ValueError("out_t must be a contiguous [n*d, B] tensor")
+        check(lib().cc_prep_input_t(_ptr(x_in), dtype_code(x_in.dtype), _ptr(factor), fdt, _ptr(out), _ptr(out_t),
+                                    _ptr(colsum_part), B, n, d, dtype_code(dtype), _stream(x_in)))
+    else:
+        check(lib().cc_prep_input(_ptr(x_in), dtype_code(x_in.dtype), _ptr(factor), fdt, _ptr(out),
+                                  _ptr(colsum_part), B, n, d, dtype_code(dtype), _stream(x_in)))
     return out
 
 
@@ -169,15 +176,31 @@ def decode_partial_t(acts, W_dec_t, recon_f32, ws=None):
                                    0 if ws is None else ws.numel(), B, h, K, dtype_code(acts.dtype), _stream(acts)))
 
 
-def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_scale, B, n, d, row0=0, rows=None):
-    """Loss terms + g_recon for batch rows [row0, row0 + rows) (default: all B rows)."""
+def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_scale, B, n, d, row0=0, rows=None,
+                 g_recon_t=None):
+    """Loss terms + g_recon for batch rows [row0, row0 + rows) (default: all B rows);
+    g_recon_t (optional, bf16 [n*d, B]): also those rows of g_recon^T."""
     rows = B - row0 if rows is None else rows
+    if g_recon_t is not None:
+        if g_recon_t.shape != (n * d, B) or not g_recon_t.is_contiguous():
+            raise ValueError("g_recon_t must be a contiguous [n*d, B] tensor")
+        check(lib().cc_loss_fwd_bwd_rows_t(_ptr(recon_f32), _ptr(b_dec), _ptr(x), _ptr(x_mean), _ptr(g_recon),
+                                           _ptr(g_recon_t), _ptr(row_part), _ptr(col_part), grad_scale, row0, rows,
+                                           B, n, d, dtype_code(x.dtype), _stream(x)))
+        return
     check(lib().cc_loss_fwd_bwd_rows(_ptr(recon_f32), _ptr(b_dec), _ptr(x), _ptr(x_mean), _ptr(g_recon),
                                      _ptr(row_part), _ptr(col_part), grad_scale, row0, rows, B, n, d,
                                      dtype_code(x.dtype), _stream(x)))
 
 
-def loss_finalize(row_part, l1_part, n_l1, l0_part, n_l0, ev, ev_a, ev_b, scalars, B, n, d, l1l0_out=None):
+def loss_finalize(row_part, l1_part, n_l1, l0_part, n_l0, ev, ev_a, ev_b, scalars, B, n, d, l1l0_out=None,
+                  host=None, seq=0):
+    """host (optional): a _hip.MappedHostBuffer that also receives scalars[0:8] and then `seq` in word 8."""
+    if host is not None:
+        check(lib().cc_loss_finalize_mapped(_ptr(row_part), _ptr(l1_part), n_l1, _ptr(l0_part), n_l0, _ptr(ev),
+                                            _ptr(ev_a), _ptr(ev_b), _ptr(scalars), _ptr(l1l0_out), host.device_ptr,
+                                            seq, B, n, d, _stream(row_part)))
+        return
     check(lib().cc_loss_finalize(_ptr(row_part), _ptr(l1_part), n_l1, _ptr(l0_part), n_l0, _ptr(ev), _ptr(ev_a),
                                  _ptr(ev_b), _ptr(scalars), _ptr(l1l0_out), B, n, d, _stream(row_part)))
 
@@ -218,6 +241,17 @@ def transpose(src, out=None):
         raise ValueError("transpose: out must be [cols, rows] of the same dtype, unit column stride")
     check(lib().cc_transpose_b16(_ptr(src), rows, cols, src.stride(0), _ptr(out), out.stride(0), _stream(src)))
     return out
+
+
+def dec_norms_part_floats(h, n, d):
+    return int(lib().cc_dec_norms_part_floats(h, n, d))
+
+
+def transpose_dec_norms(W_dec_hk, n, d, W_dec_t, part, norms, total, inv_norms=None):
+    """W_dec_t = W_dec^T and dec_norms' outputs (same bits) from one pass over W_dec (d % 64 == 0)."""
+    h = W_dec_hk.shape[0]
+    check(lib().cc_transpose_dec_norms(_ptr(W_dec_hk), h, n, d, _ptr(W_dec_t), _ptr(part), _ptr(norms), _ptr(total),
+                                       _ptr(inv_norms), _stream(W_dec_hk)))
 
 
 def wgrad_dec(acts, g_recon, W_dec_hk, norms, colsum_acts, l1_scale, grad, sq_part, n, d):

@@ -9,7 +9,7 @@ reference's) lives in arenas mirroring the parameter arena, exposed through
 import torch
 import tqdm
 
-from . import engine
+from . import _hip, engine
 from .buffer import Buffer
 from .crosscoder import CrossCoder
 
@@ -74,6 +74,7 @@ class Trainer:
         self.logger = logger
         self._host = None  # pinned loss-scalar landing buffer (allocated on the first step)
         self._side = None  # stream of the decoder half's Adam (created on the first step)
+        self._map = None  # mapped host buffer the loss-finalize kernel writes (mapped_losses)
 
     def lr_lambda(self, step):
         if step < 0.8 * self.total_steps:
@@ -93,6 +94,13 @@ class Trainer:
         raw, factor = self.buffer.next_raw()
         ws = cc._workspace(raw.shape[0])
         self._last_B = raw.shape[0]
+        if self.mapped_losses:
+            if self._map is None:
+                self._map = _hip.MappedHostBuffer(16)
+            ws.host = self._map
+        else:
+            ws.host = None
+        self._ws = ws
         P = cc.arena()
         opt = self.optimizer
         engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None)
@@ -122,6 +130,10 @@ class Trainer:
         self._copied.record()
 
     early_loss_copy = True  # False: copy the losses after the whole step (A/B switch for tools/)
+    # True: the loss kernel writes the scalars straight into mapped host memory and the host polls
+    # a sequence word (no copy kernel, no event on the compute stream).  Measured neutral at
+    # config 2 (tools/step_ab.py), so the copy + event stays the default.
+    mapped_losses = False
     overlap_decoder_adam = True  # False: one Adam launch on torch's stream (A/B switch for tools/)
 
     def _side_stream(self):
@@ -137,13 +149,18 @@ class Trainer:
         self.crosscoder.arena().wait_pending()
 
     def step(self):
-        if self.early_loss_copy:
-            self.step_async(on_losses=self._copy_losses)
+        if self.mapped_losses:
+            self.step_async()
+            self._map.wait(8, self._ws.host_seq)
+            s = self._map.f32[:6].tolist()
         else:
-            self._copy_losses(self.step_async())
+            if self.early_loss_copy:
+                self.step_async(on_losses=self._copy_losses)
+            else:
+                self._copy_losses(self.step_async())
+            self._copied.synchronize()
+            s = self._host[:6].tolist()
         l1c = self._last_l1c
-        self._copied.synchronize()
-        s = self._host[:6].tolist()
         dt = self.crosscoder.dtype
         rd = (lambda v: float(torch.tensor(v, dtype=dt))) if dt != torch.float32 else float
         l2, l1, l0 = s[0], rd(s[1]), s[2]

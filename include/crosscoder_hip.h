@@ -74,6 +74,9 @@ int cc_gemm_f32out(const void* A, int a_layout, int64_t lda, const void* Bm, int
  * column sums of x_out -> reduced by cc_reduce_rows into x.mean(0) (crosscoder.py:112). */
 int cc_prep_input(const void* x_in, int in_dtype, const void* factor, int factor_dtype, void* x_out,
                   float* colsum_part, int64_t B, int64_t n, int64_t d, int dtype, void* stream);
+/* cc_prep_input that also stores x_t [n*d][B] = x_out^T (bf16 out, B % 8 == 0; x_t NULL -> cc_prep_input). */
+int cc_prep_input_t(const void* x_in, int in_dtype, const void* factor, int factor_dtype, void* x_out, void* x_t,
+                    float* colsum_part, int64_t B, int64_t n, int64_t d, int dtype, void* stream);
 
 /* out[j] = scale * sum_{i<R} part[i*ld + j] (fixed order).  Optional: out_f32, out_t (dtype),
  * sq_part [cc_reduce_parts(C)] (per column block: sum of dtype-rounded out^2, for clip_grad_norm_),
@@ -141,6 +144,11 @@ int cc_loss_fwd_bwd(const float* recon_f32, const void* b_dec, const void* x, co
 int cc_loss_fwd_bwd_rows(const float* recon_f32, const void* b_dec, const void* x, const float* x_mean,
                          void* g_recon, float* row_part, float* col_part, float grad_scale, int64_t row0,
                          int64_t rows, int64_t B, int64_t n, int64_t d, int dtype, void* stream);
+/* cc_loss_fwd_bwd_rows that also stores g_recon_t [n*d][B] = g_recon^T for its rows (bf16, B and rows
+ * % 8 == 0; g_recon_t NULL -> cc_loss_fwd_bwd_rows). */
+int cc_loss_fwd_bwd_rows_t(const float* recon_f32, const void* b_dec, const void* x, const float* x_mean,
+                           void* g_recon, void* g_recon_t, float* row_part, float* col_part, float grad_scale,
+                           int64_t row0, int64_t rows, int64_t B, int64_t n, int64_t d, int dtype, void* stream);
 
 /* Loss reduction (crosscoder.py:106-128, trainer.py:51-61): per-row explained variances
  * ev/ev_a/ev_b [B] (fp32) and scalars[0:8] = {l2, l1, l0, mean ev, mean ev_a, mean ev_b, 0, 0};
@@ -151,6 +159,12 @@ int cc_loss_finalize(const float* row_part, const float* l1_part, int64_t n_l1, 
                      float* ev, float* ev_a, float* ev_b, float* scalars, float* l1l0_out, int64_t B, int64_t n,
                      int64_t d, void* stream);
 /* (l1l0_out, optional: a second copy of scalars[1:3] -- the latent-sharded step all-reduces it) */
+/* cc_loss_finalize that also writes scalars[0:8] to host_out[0:8] (mapped, coherent pinned host
+ * memory, hipHostMallocMapped | hipHostMallocCoherent) and then, after a system-scope release,
+ * the 32-bit word `seq` to host_out[8]: the host polls that word instead of a copy + event. */
+int cc_loss_finalize_mapped(const float* row_part, const float* l1_part, int64_t n_l1, const float* l0_part,
+                            int64_t n_l0, float* ev, float* ev_a, float* ev_b, float* scalars, float* l1l0_out,
+                            float* host_out, uint32_t seq, int64_t B, int64_t n, int64_t d, void* stream);
 
 /* Backward through decode + L1 + ReLU (autograd of crosscoder.py:77,84-89,126):
  * g_pre[B,h] = (g_recon . W_dec^T + l1_scale * tn[h]) * (acts > 0),  l1_scale = l1_coeff / B.
@@ -222,6 +236,13 @@ int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const 
  * rows, cols, ld_src, ld_dst % 8 == 0.  (The step's batch-contiguous copies x^T and g_recon^T.) */
 int cc_transpose_b16(const void* src, int64_t rows, int64_t cols, int64_t ld_src, void* dst, int64_t ld_dst,
                      void* stream);
+
+/* W_dec_t [K][h] = W_dec^T plus the decoder norms of cc_dec_norms (same bits) from the same pass
+ * over W_dec [h][K] (bf16; d % 64 == 0, h % 8 == 0).  part: cc_dec_norms_part_floats(h, n, d)
+ * floats of workspace (per-row, per-64-column-block squared sums). */
+int64_t cc_dec_norms_part_floats(int64_t h, int64_t n, int64_t d);
+int cc_transpose_dec_norms(const void* W_dec, int64_t h, int64_t n, int64_t d, void* W_dec_t, float* part,
+                           float* norms, float* total, float* inv_norms, void* stream);
 
 int cc_gather_rows(const void* src, int64_t src_rows, const int64_t* perm, void* dst, int64_t rows,
                    int64_t row_bytes, void* stream);

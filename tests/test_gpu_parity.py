@@ -482,6 +482,60 @@ def test_transpose_b16(gpu, rows, cols, r0, c0):
     assert bool((out[:, :8] == 7).all()) and bool((out[:, 8 + rows:] == 7).all())  # nothing outside the slice
 
 
+@pytest.mark.parametrize("h,n,d", [(16384, 2, 2304), (200, 2, 64), (72, 3, 192)])
+def test_transpose_dec_norms_matches_dec_norms(gpu, h, n, d):
+    """The fused W_dec^T + decoder-norms pass gives cc_dec_norms' bits and the exact transpose;
+    both match fp64 norms."""
+    g = torch.Generator().manual_seed(h + d)
+    W = (torch.randn(h, n * d, generator=g) * 0.05).to(torch.bfloat16).to(gpu)
+    W[3] = 0  # zero rows: inverse norm 0
+    E = lambda *s_: torch.empty(*s_, device=gpu)  # noqa: E731
+    nm1, tn1, inv1 = E(h, n), E(h), E(h, n)
+    ops.dec_norms(W, h, n, d, norms=nm1, total=tn1, inv_norms=inv1)
+    Wt = torch.empty(n * d, h, dtype=torch.bfloat16, device=gpu)
+    nm2, tn2, inv2 = E(h, n), E(h), E(h, n)
+    ops.transpose_dec_norms(W, n, d, Wt, E(ops.dec_norms_part_floats(h, n, d)), nm2, tn2, inv2)
+    torch.cuda.synchronize()
+    assert torch.equal(Wt, W.t())
+    assert torch.equal(nm1, nm2) and torch.equal(tn1, tn2) and torch.equal(inv1, inv2)
+    ref = W.double().view(h, n, d).norm(dim=-1).cpu()
+    assert rel(nm1, ref) < 1e-6 and float(inv1[3].abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("B,n,d", [(4096, 2, 2304), (1000, 2, 40), (72, 3, 520)])
+def test_prep_and_loss_transposed_outputs(gpu, B, n, d):
+    """cc_prep_input_t / cc_loss_fwd_bwd_rows_t: the same x / g_recon / partial slabs as the plain
+    kernels, plus exact transposes (loss over two row ranges written into one g_recon_t)."""
+    K = n * d
+    g = torch.Generator().manual_seed(B + K)
+    bf = torch.bfloat16
+    x_in = (torch.randn(B, n, d, generator=g) * 3).to(gpu)
+    factor = (torch.rand(n, generator=g) + 0.5).to(bf).to(gpu)
+    E = lambda *s_, dt=torch.float32: torch.empty(*s_, dtype=dt, device=gpu)  # noqa: E731
+    x1, x2, xt = E(B, K, dt=bf), E(B, K, dt=bf), E(K, B, dt=bf)
+    cp1, cp2 = E(ops.prep_part_rows(B), K), E(ops.prep_part_rows(B), K)
+    ops.prep_input(x_in, factor, bf, out=x1, colsum_part=cp1)
+    ops.prep_input(x_in, factor, bf, out=x2, colsum_part=cp2, out_t=xt)
+    recon = torch.randn(B, K, generator=g).to(gpu)
+    b_dec = (torch.randn(K, generator=g) * 0.1).to(bf).to(gpu)
+    mu = torch.randn(K, generator=g).to(gpu)
+    ncb = ops.loss_col_blocks(d)
+    outs = []
+    for tr in (False, True):
+        gr, gt = E(B, K, dt=bf), torch.zeros(K, B, dtype=bf, device=gpu)
+        rp, lc = E(2, n * ncb, B), E(ops.loss_part_rows(B), K)
+        cut = 32 * (B // 64)
+        for r0, r1 in ((0, cut), (cut, B)) if cut else ((0, B),):
+            ops.loss_fwd_bwd(recon, b_dec, x1, mu, gr, rp, lc, 2.0 / B, B, n, d, row0=r0, rows=r1 - r0,
+                             g_recon_t=gt if tr else None)
+        outs.append((gr, rp, lc, gt))
+    torch.cuda.synchronize()
+    assert torch.equal(x1, x2) and torch.equal(cp1, cp2) and torch.equal(xt, x1.t())
+    for a, b in zip(outs[0][:3], outs[1][:3]):
+        assert torch.equal(a, b)
+    assert torch.equal(outs[1][3], outs[1][0].t())
+
+
 @pytest.mark.parametrize("B,K,h", [(512, 768, 768), (1000, 80, 200), (4096, 4608, 2048)])
 def test_transposed_epilogue_outputs(gpu, B, K, h):
     """cc_encode_fwd_t's acts_t and cc_dacts_bwd_t's g_pre_t (whole batch and a batch slice written

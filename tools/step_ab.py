@@ -1,6 +1,6 @@
 """A/B of whole-step variants on ONE device, interleaved (cdna guide rule 24): config-2 Trainer.step
-with the transposed (KC/KC) weight-gradient operands on/off.  Usage: python tools/step_ab.py
-(per-launch times of the same variants: python tools/step_ab.py --spans)"""
+with individual scheduling features switched off.  Usage: python tools/step_ab.py [--spans]
+(--spans: per-launch HIP-event averages of each variant as well)."""
 import os
 import sys
 import time
@@ -19,23 +19,40 @@ def main():
     tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=bench.B * 8, seed=0), crosscoder=ca.CrossCoder(cfg))
     cc = tr.crosscoder
     dev = torch.device("cuda:0")
-    wss = {}
-    for flag in ("1", "0"):
-        os.environ["CC_TRANSPOSED_WGRAD"] = flag
-        wss["transposed wgrad" if flag == "1" else "batch-major wgrad"] = engine.StepWorkspace(
-            bench.B, cc.n_models, cfg["d_in"], cc.d_hidden, cc.dtype, dev)
+    ws_t = engine.StepWorkspace(bench.B, cc.n_models, cfg["d_in"], cc.d_hidden, cc.dtype, dev)
+    os.environ["CC_TRANSPOSED_WGRAD"] = "0"
+    ws_b = engine.StepWorkspace(bench.B, cc.n_models, cfg["d_in"], cc.d_hidden, cc.dtype, dev)
+    os.environ.pop("CC_TRANSPOSED_WGRAD")
+    part = ws_t.norm_part
+
+    defaults = (tr.mapped_losses, tr.overlap_decoder_adam, engine.DEC_ADAM_BLOCKS)
+
+    def setup(ws, mapped=defaults[0], fused=True, side=defaults[1], blocks=defaults[2]):
+        def f():
+            cc._ws = ws
+            tr.mapped_losses = mapped
+            tr.overlap_decoder_adam = side
+            engine.DEC_ADAM_BLOCKS = blocks
+            ws.norm_part = part if (fused and ws is ws_t) else None
+            ws.norms_token = None
+        return f
+
+    variants = {"default": setup(ws_t), "mapped losses on": setup(ws_t, mapped=True),
+                "no fused W_dec^T+norms": setup(ws_t, fused=False), "decoder Adam serial": setup(ws_t, side=False),
+                "side Adam 512 blocks": setup(ws_t, blocks=512), "side Adam uncapped": setup(ws_t, blocks=0),
+                "batch-major wgrad": setup(ws_b)}
     spans = "--spans" in sys.argv
-    timers = {k: bench.EventTimer() for k in wss} if spans else {}
+    timers = {k: bench.EventTimer() for k in variants} if spans else {}
     for t in timers.values():
         t.enabled = True
-    res = {k: [] for k in wss}
-    for ws in wss.values():
-        cc._ws = ws
+    res = {k: [] for k in variants}
+    for f in variants.values():
+        f()
         for _ in range(3):
             tr.step()
     for _ in range(10):
-        for name, ws in wss.items():
-            cc._ws = ws
+        for name, f in variants.items():
+            f()
             tr.step()
             torch.cuda.synchronize()
             if spans:
