@@ -61,15 +61,24 @@ __global__ __launch_bounds__(256) void prep_kernel(const void* __restrict__ x_in
   if (col < K) {
     float f = 1.f;
     if (factor) f = Elem<DF>::load((const typename Elem<DF>::T*)factor + col / d);
-    for (int r = r0 + wave; r < r0 + PREP_ROWS && r < B; r += 4) {
-      float v[8];
-      load8<DIN>(x_in, (int64_t)r * K + col, v);
+    // 4 rows per trip (rows rb, rb+4, rb+8, rb+12): their loads are in flight together; the
+    // column sums still add rows in the order r0+w, r0+w+4, ...
+    for (int rb = r0 + wave; rb < r0 + PREP_ROWS && rb < B; rb += 16) {
+      float v[4][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = Elem<DT>::round(v[j] * f);
-      store8<DT>(x_out, (int64_t)r * K + col, v);
-      if constexpr (TR) tile_put8(tile, r - r0, lane, v);
+      for (int u = 0; u < 4; ++u)
+        if (rb + 4 * u < B && 4 * u < PREP_ROWS) load8<DIN>(x_in, (int64_t)(rb + 4 * u) * K + col, v[u]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) cs[j] += v[j];
+      for (int u = 0; u < 4; ++u) {
+        const int r = rb + 4 * u;
+        if (r >= B) break;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[u][j] = Elem<DT>::round(v[u][j] * f);
+        store8<DT>(x_out, (int64_t)r * K + col, v[u]);
+        if constexpr (TR) tile_put8(tile, r - r0, lane, v[u]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cs[j] += v[u][j];
+      }
     }
   }
   if constexpr (TR) {
@@ -208,31 +217,44 @@ __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ rec
     if (x_mean) load8f(x_mean, col, mu);
   }
   const int64_t plane = (int64_t)n * ncb * B;  // row_part [2][n*ncb][B]
-  for (int i = 0; i < LOSS_ROWS / 4; ++i) {
-    const int r = r0 + wave + 4 * i;
-    if (r >= row_end) break;  // wave-uniform
-    float l2 = 0.f, tv = 0.f;
+  // two rows per trip (r, r + 4): both rows' loads are in flight together
+  for (int i = 0; i < LOSS_ROWS / 4; i += 2) {
+    const int ra = r0 + wave + 4 * i;
+    if (ra >= row_end) break;  // wave-uniform
+    float rv[2][8], xv[2][8];
     if (cv) {
-      float rv[8], xv[8], g[8];
-      load8f(recon, (int64_t)r * K + col, rv);
-      load8<DT>(x, (int64_t)r * K + col, xv);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float diff = (rv[j] + bd[j]) - xv[j];
-        l2 += diff * diff;
-        float c = xv[j] - mu[j];
-        tv += c * c;
-        g[j] = E::round(grad_scale * diff);
-        cs[j] += g[j];
-      }
-      store8<DT>(g_recon, (int64_t)r * K + col, g);
-      if constexpr (TR) tile_put8(tile, r - r0, lane, g);
+      for (int u = 0; u < 2; ++u)
+        if (ra + 4 * u < row_end) {
+          load8f(recon, (int64_t)(ra + 4 * u) * K + col, rv[u]);
+          load8<DT>(x, (int64_t)(ra + 4 * u) * K + col, xv[u]);
+        }
     }
-    l2 = wave_sum(l2);
-    tv = wave_sum(tv);
-    if (lane == 0) {
-      row_part[(int64_t)blockIdx.x * B + r] = l2;
-      row_part[plane + (int64_t)blockIdx.x * B + r] = tv;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = ra + 4 * u;
+      if (r >= row_end) break;
+      float l2 = 0.f, tv = 0.f;
+      if (cv) {
+        float g[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float diff = (rv[u][j] + bd[j]) - xv[u][j];
+          l2 += diff * diff;
+          float c = xv[u][j] - mu[j];
+          tv += c * c;
+          g[j] = E::round(grad_scale * diff);
+          cs[j] += g[j];
+        }
+        store8<DT>(g_recon, (int64_t)r * K + col, g);
+        if constexpr (TR) tile_put8(tile, r - r0, lane, g);
+      }
+      l2 = wave_sum(l2);
+      tv = wave_sum(tv);
+      if (lane == 0) {
+        row_part[(int64_t)blockIdx.x * B + r] = l2;
+        row_part[plane + (int64_t)blockIdx.x * B + r] = tv;
+      }
     }
   }
   if constexpr (TR) {
