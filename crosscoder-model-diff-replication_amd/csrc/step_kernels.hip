@@ -46,28 +46,56 @@ CC_DEV void tile_store_transposed(const char* lds, void* out_t, int64_t ldt, int
 // ---------------------------------------------------------------------------------------
 // x_out = dtype(x_in * factor[model]);  colsum_part[rb][k] = sum over the block's rows.
 // grid: (ceil(K/512), ceil(B/64)); block 256 = 4 waves; lane -> 8 columns, wave -> 16 rows.
-// TR (bf16 out): also x_t [K][B] = x_out^T through an LDS tile.
+// TR (bf16 out): also x_t [K][B] = x_out^T through a 32-row LDS tile (two halves per block; the
+// column-sum slab shares the tile's LDS, so 32 KB per block: 5 blocks per CU, one round of blocks).
 template <int DIN, int DF, int DT, bool TR = false>
 __global__ __launch_bounds__(256) void prep_kernel(const void* __restrict__ x_in, const void* __restrict__ factor,
                                                    void* __restrict__ x_out, float* __restrict__ colsum_part, int B,
                                                    int n, int d, void* __restrict__ x_t) {
-  __shared__ float red[4][512];
-  __shared__ __attribute__((aligned(16))) char tile[TR ? PREP_ROWS * 1024 : 16];
+  __shared__ __attribute__((aligned(16))) char lds[TR ? 32 * 1024 : 4 * 512 * 4];
+  float(*red)[512] = (float(*)[512])lds;
   const int K = n * d;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = blockIdx.x * 512 + lane * 8;
   const int r0 = blockIdx.y * PREP_ROWS;
   float cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (col < K) {
-    float f = 1.f;
-    if (factor) f = Elem<DF>::load((const typename Elem<DF>::T*)factor + col / d);
-    // 4 rows per trip (rows rb, rb+4, rb+8, rb+12): their loads are in flight together; the
-    // column sums still add rows in the order r0+w, r0+w+4, ...
+  float f = 1.f;
+  if (factor && col < K) f = Elem<DF>::load((const typename Elem<DF>::T*)factor + col / d);
+  if constexpr (TR) {
+    for (int half = 0; half < 2; ++half) {
+      const int base = r0 + 32 * half;
+      if (base >= B) break;  // block-uniform
+      if (col < K) {
+        // the wave's 8 rows of this half (base + w + 4k): all loads in flight; the column sums
+        // still add rows in the order r0+w, r0+w+4, ...
+        float v[8][8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (base + wave + 4 * k < B) load8<DIN>(x_in, (int64_t)(base + wave + 4 * k) * K + col, v[k]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int r = base + wave + 4 * k;
+          if (r >= B) break;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[k][j] = Elem<DT>::round(v[k][j] * f);
+          store8<DT>(x_out, (int64_t)r * K + col, v[k]);
+          tile_put8(lds, r - base, lane, v[k]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) cs[j] += v[k][j];
+        }
+      }
+      __syncthreads();
+      tile_store_transposed<32>(lds, x_t, B, (int64_t)blockIdx.x * 512, K - blockIdx.x * 512, base,
+                                B - base < 32 ? B - base : 32);
+      __syncthreads();
+    }
+  } else if (col < K) {
+    // 4 rows per trip (rows rb, rb+4, rb+8, rb+12): their loads are in flight together
     for (int rb = r0 + wave; rb < r0 + PREP_ROWS && rb < B; rb += 16) {
       float v[4][8];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (rb + 4 * u < B && 4 * u < PREP_ROWS) load8<DIN>(x_in, (int64_t)(rb + 4 * u) * K + col, v[u]);
+        if (rb + 4 * u < B) load8<DIN>(x_in, (int64_t)(rb + 4 * u) * K + col, v[u]);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int r = rb + 4 * u;
@@ -75,16 +103,10 @@ __global__ __launch_bounds__(256) void prep_kernel(const void* __restrict__ x_in
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[u][j] = Elem<DT>::round(v[u][j] * f);
         store8<DT>(x_out, (int64_t)r * K + col, v[u]);
-        if constexpr (TR) tile_put8(tile, r - r0, lane, v[u]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) cs[j] += v[u][j];
       }
     }
-  }
-  if constexpr (TR) {
-    __syncthreads();
-    const int nr = B - r0 < PREP_ROWS ? B - r0 : PREP_ROWS;
-    tile_store_transposed<PREP_ROWS>(tile, x_t, B, (int64_t)blockIdx.x * 512, K - blockIdx.x * 512, r0, nr);
   }
   if (!colsum_part) return;
 #pragma unroll
@@ -199,8 +221,9 @@ __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ rec
                                                    void* __restrict__ g_recon, float* __restrict__ row_part,
                                                    float* __restrict__ col_part, float grad_scale, int B, int n,
                                                    int d, int ncb, int row0, int row_end, void* __restrict__ g_t) {
-  __shared__ float red[4][512];
-  __shared__ __attribute__((aligned(16))) char tile[TR ? LOSS_ROWS * 1024 : 16];
+  // (TR: the column-sum slab reuses the transposition tile's LDS: 32 KB per block)
+  __shared__ __attribute__((aligned(16))) char tile[TR ? LOSS_ROWS * 1024 : 4 * 512 * 4];
+  float(*red)[512] = (float(*)[512])tile;
   using E = Elem<DT>;
   const int K = n * d;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -261,6 +284,7 @@ __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ rec
     __syncthreads();
     const int nr = row_end - r0 < LOSS_ROWS ? row_end - r0 : LOSS_ROWS;
     tile_store_transposed<LOSS_ROWS>(tile, g_t, B, (int64_t)m * d + cb * LOSS_COLS, d - cb * LOSS_COLS, r0, nr);
+    __syncthreads();  // (red reuses the tile)
   }
   if (!col_part) return;
 #pragma unroll
