@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcrosscoder_hip.so")
+# CC_HIP_LIB: an experiment build (tools/build_variant.sh) for in-process A/B timing; default in-tree
+LIB_PATH = os.environ.get("CC_HIP_LIB") or os.path.join(_HERE, "libcrosscoder_hip.so")
 DEFAULT_PP_MASK = 5  # CC_PP_MASK the library is built with (csrc/gemm.hip)
 
 CC_BF16 = 1
@@ -63,6 +64,9 @@ SIGNATURES = {
     "cc_transpose_b16": (_i, [_p, _i64, _i64, _i64, _p, _i64, _p]),
     "cc_dec_norms_part_floats": (_i64, [_i64, _i64, _i64]),
     "cc_transpose_dec_norms": (_i, [_p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p]),
+    "cc_dec_norms_finalize": (_i, [_p, _i64, _i64, _i64, _p, _p, _p, _p]),
+    "cc_adam_dec_transposed": (_i, [_p, _p, _p, _p, _i64, _i64, _p, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                    ctypes.c_double, _i64, _i64, _p, _p, _i, _p]),
     "cc_gather_rows": (_i, [_p, _i64, _p, _p, _i64, _i64, _p]),
     "cc_fold_scaling": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_decoder_stats": (_i, [_p, _i64, _i64, _i64, _i, _p, _p, _p, _p]),

@@ -228,6 +228,16 @@ int cc_transpose_b16(const void* src, int64_t rows, int64_t cols, int64_t ld_src
 
 int64_t cc_dec_norms_part_floats(int64_t h, int64_t n, int64_t d) { return d % 64 ? 0 : h * n * (d / 64); }
 
+int cc_dec_norms_finalize(const float* part, int64_t h, int64_t n, int64_t d, float* norms, float* total,
+                          float* inv_norms, void* stream) {
+  if (!part || !norms || !total) return CC_ERR_NULL;
+  if (h <= 0 || n <= 0 || d <= 0 || d % 64) return CC_ERR_SHAPE;
+  hipLaunchKernelGGL(norms_finalize_kernel, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, (hipStream_t)stream, part,
+                     (int)h, (int)n, (int)(d / 64), norms, total, inv_norms);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
 int cc_transpose_dec_norms(const void* W_dec, int64_t h, int64_t n, int64_t d, void* W_dec_t, float* part,
                            float* norms, float* total, float* inv_norms, void* stream) {
   if (!W_dec || !W_dec_t || !part || !norms || !total) return CC_ERR_NULL;

@@ -33,6 +33,9 @@
 #ifndef CC_PP_ORDER
 #define CC_PP_ORDER 1
 #endif
+#ifndef CC_PP_PRIO_BASE  // experiment: wave priority of the whole GEMM (vs concurrent side-stream kernels)
+#define CC_PP_PRIO_BASE 0
+#endif
 
 CC_DEV int pp_h(int k) { return ((k >> 1) & 1) | ((k >> 2) & 2); }
 
@@ -210,6 +213,7 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
+  if (CC_PP_PRIO_BASE) __builtin_amdgcn_s_setprio(CC_PP_PRIO_BASE);
   int tm, tn;
   tile_of_block(bid, args.nbm, args.nbn, tm, tn);
   const int m0 = tm * BM, n0 = tn * 256;
@@ -399,7 +403,7 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
 #if CC_PP_PRIO
-      __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1 + CC_PP_PRIO_BASE);
 #endif
 #if CC_PP_ORDER == 0
 #pragma unroll
@@ -418,7 +422,7 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
           acc[ib + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii], acc[ib + ii][j], 0, 0, 0);
 #endif
 #if CC_PP_PRIO
-      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(CC_PP_PRIO_BASE);
 #endif
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();

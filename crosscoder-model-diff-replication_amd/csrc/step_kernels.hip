@@ -593,6 +593,68 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   }
 }
 
+// Decoder-half Adam over W_dec [h][K] (bf16) in 64 x 64 tiles that also emits what the next
+// step needs from the updated W_dec: W_dec^T [K][h] (LDS tile read back with ds_read_b64_tr_b16)
+// and the decoder norms' per-(row, 64-column block) squared sums in dec_norms_kernel's order
+// (8 sequential fma per lane, xor-1/2/4 butterfly) -- one HBM pass instead of Adam + a
+// transpose/norms pass.  Persistent grid over the tiles, rows fast; every element gets
+// adam_elem, so p / m / v are the bits cc_adam_step produces.
+__global__ __launch_bounds__(256) void adam_dec_tr_kernel(const AdamArgs a, int h, int K, char* __restrict__ wt,
+                                                          float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char tile[64 * 128];
+  const float coef = a.coef ? *a.coef : 1.f;
+  const int nr = (h + 63) / 64, nblk = K / 64, ntiles = nr * nblk;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g4 = lane >> 4, i = lane & 15, q4 = i >> 2, p4 = i & 3;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int r0 = (t % nr) * 64, c0 = (t / nr) * 64;
+    float p[2][8], g[2][8], m[2][8], v[2][8];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int idx = threadIdx.x + 256 * k, r = idx >> 3, ch = idx & 7;
+      if (r0 + r < h) {
+        const int64_t e = (int64_t)(r0 + r) * K + c0 + 8 * ch;
+        load8_nt<CC_BF16>(a.p, e, p[k]); load8_nt<CC_BF16>(a.g, e, g[k]);
+        load8_nt<CC_BF16>(a.m, e, m[k]); load8_nt<CC_BF16>(a.v, e, v[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int idx = threadIdx.x + 256 * k, r = idx >> 3, ch = idx & 7;
+      float qs = 0.f;
+      if (r0 + r < h) {
+        const int64_t e = (int64_t)(r0 + r) * K + c0 + 8 * ch;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) adam_elem<CC_BF16>(a, coef, p[k][j], g[k][j], m[k][j], v[k][j]);
+        store8_nt<CC_BF16>(a.p, e, p[k]); store8_nt<CC_BF16>(a.m, e, m[k]); store8_nt<CC_BF16>(a.v, e, v[k]);
+        bf16x8 b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          b[j] = (short)f2bf(p[k][j]);
+          qs = __fmaf_rn(p[k][j], p[k][j], qs);
+        }
+        *(bf16x8*)(tile + r * 128 + ((ch ^ (r & 7)) << 4)) = b;
+      }
+      qs = block8_sum(qs);
+      if (ch == 0 && r0 + r < h) part[(int64_t)(r0 + r) * nblk + (c0 >> 6)] = qs;
+    }
+    __syncthreads();
+    const int ca = 16 * w + 4 * p4, cch = ca >> 3, c = 16 * w + i;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int R = (4 * s2 + g4) * 8, l0 = R + q4, l1 = R + 4 + q4;
+      const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_bf16x4_s*)(tile + l0 * 128 + ((cch ^ (l0 & 7)) << 4) + (ca & 4) * 2));
+      const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_bf16x4_s*)(tile + l1 * 128 + ((cch ^ (l1 & 7)) << 4) + (ca & 4) * 2));
+      if (r0 + R < h)
+        *(bf16x8*)(wt + ((int64_t)(c0 + c) * h + r0 + R) * 2) =
+            bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    }
+    __syncthreads();
+  }
+}
+
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace cc
@@ -814,11 +876,10 @@ int cc_segment_sums(const float* sq, const int64_t* off, int nparams, int zero_m
   return CC_OK;
 }
 
-int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, double lr, double beta1,
-                 double beta2, double eps, int64_t step, int64_t max_blocks, int dtype, void* stream) {
-  if (!p || !g || !m || !v) return CC_ERR_NULL;
-  if (numel <= 0 || step <= 0) return CC_ERR_SHAPE;
-  if (!al16(p) || !al16(g) || !al16(m) || !al16(v)) return CC_ERR_ALIGN;
+}  // extern "C"
+
+static AdamArgs adam_args(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, double lr,
+                          double beta1, double beta2, double eps, int64_t step) {
   AdamArgs a = {};
   a.p = p; a.g = g; a.m = m; a.v = v; a.numel = numel; a.coef = coef;
   // host-side scalars in double, as torch computes them from python floats (adam.py)
@@ -830,6 +891,33 @@ int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const 
   double bc1 = 1.0 - pow(b1, (double)step), bc2 = 1.0 - pow(b2, (double)step);
   a.bc2s = (float)sqrt(bc2);
   a.neg_step = (float)(-((double)lr / bc1));
+  return a;
+}
+
+extern "C" {
+
+int cc_adam_dec_transposed(void* p, const void* g, void* m, void* v, int64_t h, int64_t K, const float* coef,
+                           double lr, double beta1, double beta2, double eps, int64_t step, int64_t max_blocks,
+                           void* W_dec_t, float* part, int dtype, void* stream) {
+  if (!p || !g || !m || !v || !W_dec_t || !part) return CC_ERR_NULL;
+  if (dtype != CC_BF16) return CC_ERR_DTYPE;
+  if (h <= 0 || K <= 0 || h % 8 || K % 64 || step <= 0 || h > (1 << 30)) return CC_ERR_SHAPE;
+  if (!al16(p) || !al16(g) || !al16(m) || !al16(v) || !al16(W_dec_t)) return CC_ERR_ALIGN;
+  const AdamArgs a = adam_args(p, g, m, v, h * K, coef, lr, beta1, beta2, eps, step);
+  const int64_t ntiles = ((h + 63) / 64) * (K / 64);
+  const int64_t blocks = max_blocks > 0 && max_blocks < ntiles ? max_blocks : ntiles;
+  hipLaunchKernelGGL(adam_dec_tr_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a, (int)h, (int)K,
+                     (char*)W_dec_t, part);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, double lr, double beta1,
+                 double beta2, double eps, int64_t step, int64_t max_blocks, int dtype, void* stream) {
+  if (!p || !g || !m || !v) return CC_ERR_NULL;
+  if (numel <= 0 || step <= 0) return CC_ERR_SHAPE;
+  if (!al16(p) || !al16(g) || !al16(m) || !al16(v)) return CC_ERR_ALIGN;
+  const AdamArgs a = adam_args(p, g, m, v, numel, coef, lr, beta1, beta2, eps, step);
   hipStream_t st = (hipStream_t)stream;
   if (max_blocks > 0) {  // capped grid-stride form: leaves most CUs to a concurrent GEMM
     int64_t work = (numel + 7) / 8;

@@ -291,6 +291,12 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False):
 
 # workgroups of the decoder-half Adam that runs beside the next step's G1 (0: uncapped one-pass)
 DEC_ADAM_BLOCKS = 256
+# decoder-half Adam in 64x64 tiles that also write W_dec^T and the norm partials (transposed mode,
+# d % 64 == 0), instead of the flat Adam + a separate W_dec^T / norms pass.  "serial": only when the
+# decoder half runs on torch's stream -- beside G1 the fused kernel's faster HBM stream slows G1 more
+# than it saves (tools/step_ab.py: 2.88 vs 2.79 ms/step side-stream; 2.81 serial).  True / False
+# force it on / off (A/B switch for tools/).
+FUSED_DEC_ADAM = "serial"
 
 
 def clip_and_adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, max_norm=1.0, side_stream=None):
@@ -302,28 +308,43 @@ def clip_and_adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, max_norm=1.0, sid
 
 def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None):
     """Adam with the clip coefficient in ws.clip_out[0].  side_stream: the decoder half's Adam (+ the
-    next step's decoder norms) runs there, so it overlaps the next step's encoder GEMM (G1 reads only
-    the encoder half, which Adam updates on torch's stream); P.pending orders every later
-    decoder-half use (forward() waits before the decoder norms; CrossCoder's methods wait;
-    Trainer.synchronize())."""
-    if side_stream is None:
+    next step's decoder norms / W_dec^T) runs there, so it overlaps the next step's encoder GEMM (G1
+    reads only the encoder half, which Adam updates on torch's stream); P.pending orders every later
+    decoder-half use (forward() waits before G2; CrossCoder's methods wait; Trainer.synchronize())."""
+    fused = ws.norm_part is not None and (FUSED_DEC_ADAM is True or (FUSED_DEC_ADAM == "serial" and side_stream is None))
+    if side_stream is None and not fused:
         with _span("adam"):
             ops.adam_step(P.data, G.data, M.data, V.data, ws.clip_out[0:1], lr, beta1, beta2, eps, step)
         return
-    main = torch.cuda.current_stream(P.data.device)
+    coef = ws.clip_out[0:1]
     with _span("adam"):
-        ops.adam_step(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), ws.clip_out[0:1], lr, beta1, beta2,
-                      eps, step)
-    # the decoder half starts after the encoder half (both are HBM-bound: run together they only
-    # share the bandwidth), i.e. beside the next step's prep / G1 on the main stream
-    enc_done = torch.cuda.Event()
-    enc_done.record(main)
-    with torch.cuda.stream(side_stream):
-        side_stream.wait_event(enc_done)
+        ops.adam_step(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), coef, lr, beta1, beta2, eps, step)
+    if side_stream is not None:
+        # the decoder half starts after the encoder half (both are HBM-bound: run together they only
+        # share the bandwidth), i.e. beside the next step's prep / G1 on the main stream
+        enc_done = torch.cuda.Event()
+        enc_done.record(torch.cuda.current_stream(P.data.device))
+        ctx = torch.cuda.stream(side_stream)
+    else:
+        ctx = contextlib.nullcontext()
+    with ctx:
+        if side_stream is not None:
+            side_stream.wait_event(enc_done)
         with _span("adam_dec"):
-            ops.adam_step(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), ws.clip_out[0:1], lr, beta1,
-                          beta2, eps, step, max_blocks=DEC_ADAM_BLOCKS)
+            if fused:
+                # W_dec in tiles that also emit W_dec^T + the norm partials; then b_dec; then the norms
+                ops.adam_dec_transposed(P.W_dec_hk, G.W_dec_hk, M.W_dec_hk, V.W_dec_hk, coef, lr, beta1, beta2, eps,
+                                        step, ws.W_dec_t, ws.norm_part,
+                                        max_blocks=DEC_ADAM_BLOCKS if side_stream is not None else 0)
+                ops.adam_step(P.b_dec_flat, G.b_dec_flat, M.b_dec_flat, V.b_dec_flat, coef, lr, beta1, beta2, eps,
+                              step)
+                ops.dec_norms_finalize(ws.norm_part, ws.h, ws.n, ws.d, ws.norms, ws.tn, ws.inv_norms)
+                ws.norms_token = _norms_token(P)
+            else:
+                ops.adam_step(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), coef, lr, beta1, beta2, eps,
+                              step, max_blocks=DEC_ADAM_BLOCKS)
         norms_for_next(ws, P)
-        done = torch.cuda.Event()
-        done.record(side_stream)
-    P.pending = done
+        if side_stream is not None:
+            done = torch.cuda.Event()
+            done.record(side_stream)
+            P.pending = done

@@ -254,6 +254,20 @@ def transpose_dec_norms(W_dec_hk, n, d, W_dec_t, part, norms, total, inv_norms=N
                                        _ptr(inv_norms), _stream(W_dec_hk)))
 
 
+def dec_norms_finalize(part, h, n, d, norms, total, inv_norms=None):
+    check(lib().cc_dec_norms_finalize(_ptr(part), h, n, d, _ptr(norms), _ptr(total), _ptr(inv_norms),
+                                      _stream(part)))
+
+
+def adam_dec_transposed(p, g, m, v, coef, lr, beta1, beta2, eps, step, W_dec_t, part, max_blocks=0):
+    """Adam over the decoder matrix p/g/m/v [h, K] (views into the arenas) + W_dec_t = p^T and the
+    decoder-norm partials from the same pass."""
+    h, K = p.shape
+    check(lib().cc_adam_dec_transposed(_ptr(p), _ptr(g), _ptr(m), _ptr(v), h, K, _ptr(coef), lr, beta1, beta2, eps,
+                                       int(step), int(max_blocks), _ptr(W_dec_t), _ptr(part), dtype_code(p.dtype),
+                                       _stream(p)))
+
+
 def wgrad_dec(acts, g_recon, W_dec_hk, norms, colsum_acts, l1_scale, grad, sq_part, n, d):
     B, h = acts.shape
     check(lib().cc_wgrad_dec(_ptr(acts), _ptr(g_recon), _ptr(W_dec_hk), _ptr(norms), _ptr(colsum_acts), l1_scale,

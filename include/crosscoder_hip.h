@@ -244,6 +244,18 @@ int64_t cc_dec_norms_part_floats(int64_t h, int64_t n, int64_t d);
 int cc_transpose_dec_norms(const void* W_dec, int64_t h, int64_t n, int64_t d, void* W_dec_t, float* part,
                            float* norms, float* total, float* inv_norms, void* stream);
 
+/* The rest of cc_dec_norms from per-(row, 64-column block) squared sums (cc_adam_dec_transposed). */
+int cc_dec_norms_finalize(const float* part, int64_t h, int64_t n, int64_t d, float* norms, float* total,
+                          float* inv_norms, void* stream);
+
+/* cc_adam_step over the decoder matrix W_dec [h][K] only (p/g/m/v point at W_dec in each arena; same
+ * bits as cc_adam_step), in 64 x 64 tiles that also write W_dec_t = the updated W_dec^T and `part`
+ * (cc_dec_norms_part_floats floats) for cc_dec_norms_finalize: the next step's decoder norms and G2
+ * operand from the same HBM pass.  bf16, K % 64 == 0, h % 8 == 0; max_blocks caps the grid. */
+int cc_adam_dec_transposed(void* p, const void* g, void* m, void* v, int64_t h, int64_t K, const float* coef,
+                           double lr, double beta1, double beta2, double eps, int64_t step, int64_t max_blocks,
+                           void* W_dec_t, float* part, int dtype, void* stream);
+
 int cc_gather_rows(const void* src, int64_t src_rows, const int64_t* perm, void* dst, int64_t rows,
                    int64_t row_bytes, void* stream);
 

@@ -563,6 +563,35 @@ def test_transposed_epilogue_outputs(gpu, B, K, h):
     assert torch.equal(g_pre_t2[:, r0:], g_pre[r0:].t()) and not bool(g_pre_t2[:, :r0].any())
 
 
+@pytest.mark.parametrize("h", [2048, 200])
+def test_fused_decoder_adam_matches_flat(gpu, h, monkeypatch):
+    """The side-stream decoder Adam in 64x64 tiles that also writes W_dec^T and the norm partials
+    (cc_adam_dec_transposed) takes bit-identical Trainer steps to the flat Adam + separate
+    W_dec^T / norms pass, and its W_dec^T / norms are those of the updated W_dec."""
+    B, n, d = 1024, 2, 256
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+               num_tokens=B * 20, device=str(gpu))
+    out = []
+    for fused in (True, False):
+        monkeypatch.setattr(engine, "FUSED_DEC_ADAM", fused)  # (beside G1 when True)
+        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=1), crosscoder=ca.CrossCoder(cfg))
+        losses = [tr.step() for _ in range(3)]
+        tr.synchronize()
+        torch.cuda.synchronize()
+        ws, P = tr.crosscoder._ws, tr.crosscoder.arena()
+        assert ws.norm_part is not None
+        assert torch.equal(ws.W_dec_t, P.W_dec_hk.t())
+        nm = torch.empty(h, n, device=gpu)
+        ops.dec_norms(P.W_dec_hk, h, n, d, norms=nm, total=torch.empty(h, device=gpu))
+        torch.cuda.synchronize()
+        assert torch.equal(ws.norms, nm)
+        opt = tr.optimizer
+        out.append((losses, P.data.clone(), opt.exp_avg.data.clone(), opt.exp_avg_sq.data.clone()))
+    assert out[0][0] == out[1][0]
+    for a, b in zip(out[0][1:], out[1][1:]):
+        assert torch.equal(a, b)
+
+
 def test_sharded_trainer_world1_matches_trainer(gpu):
     """ShardedTrainer over a 1-rank RCCL group (the sliced async all-reduce path, 4 slices) takes
     the same steps as the single-GPU Trainer."""

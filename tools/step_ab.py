@@ -27,9 +27,10 @@ def main():
 
     defaults = (tr.mapped_losses, tr.overlap_decoder_adam, engine.DEC_ADAM_BLOCKS)
 
-    def setup(ws, mapped=defaults[0], fused=True, side=defaults[1], blocks=defaults[2]):
+    def setup(ws, mapped=defaults[0], fused=True, side=defaults[1], blocks=defaults[2], fused_adam="serial"):
         def f():
             cc._ws = ws
+            engine.FUSED_DEC_ADAM = fused_adam
             tr.mapped_losses = mapped
             tr.overlap_decoder_adam = side
             engine.DEC_ADAM_BLOCKS = blocks
@@ -37,10 +38,13 @@ def main():
             ws.norms_token = None
         return f
 
-    variants = {"default": setup(ws_t), "mapped losses on": setup(ws_t, mapped=True),
-                "no fused W_dec^T+norms": setup(ws_t, fused=False), "decoder Adam serial": setup(ws_t, side=False),
-                "side Adam 512 blocks": setup(ws_t, blocks=512), "side Adam uncapped": setup(ws_t, blocks=0),
-                "batch-major wgrad": setup(ws_b)}
+    variants = {"default": setup(ws_t), "fused dec Adam beside G1": setup(ws_t, fused_adam=True),
+                "fused dec Adam serial": setup(ws_t, side=False), "flat dec Adam serial": setup(ws_t, side=False,
+                                                                                             fused_adam=False),
+                "side Adam 384 blocks": setup(ws_t, blocks=384), "batch-major wgrad": setup(ws_b)}
+    only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--only=")]
+    if only:
+        variants = {k: v for k, v in variants.items() if k in only[0].split(",")}
     spans = "--spans" in sys.argv
     timers = {k: bench.EventTimer() for k in variants} if spans else {}
     for t in timers.values():
