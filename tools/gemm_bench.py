@@ -78,6 +78,9 @@ def main():
             "G4G5_both_T_x0.5": lambda: L.cc_wgrad_both_t(P(actsT), P(grT), P(W2), P(norms), P(colsum), 1e-4, P(gW),
                                                           P(parts), P(gpT), P(xT), P(gW2), P(parts2), B, h, n, d, 1,
                                                           st),
+            "G4G5_both_T_noL1_x0.5": lambda: L.cc_wgrad_both_t(P(actsT), P(grT), P(W2), P(norms), P(colsum), 0.0,
+                                                               P(gW), P(parts), P(gpT), P(xT), P(gW2), P(parts2), B,
+                                                               h, n, d, 1, st),
             "G5_on_G4_data": lambda: L.cc_wgrad_enc(P(acts), P(g_recon), P(gW), P(parts), B, h, K, 1, st),
         }
 
