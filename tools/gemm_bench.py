@@ -53,6 +53,8 @@ def main():
     g_pre.copy_((torch.randn(B, h, device=dev, generator=g) * 1e-3).to(bf))
     actsT, grT, gpT, xT = acts.t().contiguous(), g_recon.t().contiguous(), g_pre.t().contiguous(), x.t().contiguous()
     W2T = W2.t().contiguous()
+    actsT2 = torch.empty(h, B, device=dev, dtype=bf)
+    gpT2 = torch.empty(h, B, device=dev, dtype=bf)
     nws = libs[0][1].cc_decode_ws_floats(B, h, K, 1) if hasattr(libs[0][1], "cc_decode_ws_floats") else 0
     dws = torch.empty(max(nws, 1), device=dev)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
@@ -63,9 +65,13 @@ def main():
         return {
             "G1_encode": lambda: L.cc_encode_fwd(P(x), P(W), P(b_enc), P(tn), P(acts), 1, P(parts), P(parts), P(parts),
                                                  B, K, h, 1, st),
+            "G1_encode_T": lambda: L.cc_encode_fwd_t(P(x), P(W), P(b_enc), P(tn), P(acts), P(actsT2), 1, P(parts),
+                                                     P(parts), P(parts), B, K, h, 1, st),
             "G2_decode": lambda: L.cc_decode_fwd(P(acts), P(W2), N0, P(recon), N0, B, h, K, 1, st),
             "G2_decode_ws": lambda: L.cc_decode_fwd_ws(P(acts), P(W2), P(recon), P(dws), nws, B, h, K, 1, st),
             "G2_decode_ws_T": lambda: L.cc_decode_fwd_ws_t(P(acts), P(W2T), P(recon), P(dws), nws, B, h, K, 1, st),
+            "G3_dacts_T": lambda: L.cc_dacts_bwd_t(P(g_recon), P(W2), P(acts), P(tn), 1e-4, P(gpT2), B, P(parts), B, K,
+                                                   h, 1, st),
             "G3_dacts": lambda: L.cc_dacts_bwd(P(g_recon), P(W2), P(acts), P(tn), 1e-4, P(g_pre), P(parts), B, K, h, 1,
                                                st),
             "G4_wgrad_dec": lambda: L.cc_wgrad_dec(P(acts), P(g_recon), P(W2), P(norms), P(colsum), 1e-4, P(gW),
