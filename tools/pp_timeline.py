@@ -100,6 +100,10 @@ def main():
     ws = torch.empty(max(1, nws), device=dev)
     cases["G2 split-K leftover pass"] = (lambda: L.cc_decode_fwd_ws(P(acts), P(W2), P(rec), P(ws), nws, B, h, K, 1, st),
                                          None)
+    aT, grT, gpT, xT = acts.t().contiguous(), g_recon.t().contiguous(), g_pre.t().contiguous(), x.t().contiguous()
+    cases["G4+G5 dual (KC/KC, batch-contiguous operands)"] = (
+        lambda: L.cc_wgrad_both_t(P(aT), P(grT), P(W), P(norms), P(colsum), 1e-4, P(gW), P(parts), P(gpT), P(xT),
+                                  P(gW2), P(parts2), B, h, n, d, 1, st), (h // 256) * (K // 256))
     for name, (fn, nb0) in cases.items():
         for _ in range(20):  # warm clocks
             assert fn() == 0
