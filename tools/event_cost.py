@@ -10,7 +10,8 @@ import torch
 
 PATTERNS = ["none", "event record", "wait (done event, other stream)", "aux.wait_stream(main)",
             "record + host query", "pinned copy + record", "device-scope record", "device-scope wait_stream",
-            "device-scope ping-pong (aux waits main, main waits aux)"]
+            "device-scope ping-pong (aux waits main, main waits aux)", "two event records",
+            "pinned copy + record + record"]
 
 
 def run():
@@ -52,6 +53,13 @@ def run():
                     with torch.cuda.stream(aux):
                         k()
                     H.wait_stream(torch.cuda.current_stream(), aux)
+                elif p == "two event records":
+                    torch.cuda.Event().record()
+                    torch.cuda.Event().record()
+                elif p == "pinned copy + record + record":
+                    host.copy_(small, non_blocking=True)
+                    torch.cuda.Event().record()
+                    torch.cuda.Event().record()
                 elif p.startswith("pinned"):
                     host.copy_(small, non_blocking=True)
                     torch.cuda.Event().record()
