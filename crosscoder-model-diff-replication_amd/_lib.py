@@ -58,6 +58,10 @@ SIGNATURES = {
     "cc_wgrad_both_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_both": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_clip_finalize": (_i, [_p, ctypes.POINTER(_i64), _i, _f, _i, _p, _p]),
+    "cc_grad_tail": (_i, [_p, _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _i, _p, ctypes.POINTER(_i64), _i, _f, _i, _p,
+                          _p, _p]),
+    "cc_loss_tail": (_i, [_p, _i64, _i64, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _i64,
+                          _i64, _i64, _p, _p]),
     "cc_transposed_ok": (_i, [_i64, _i64, _i64, _i]),
     "cc_encode_fwd_t": (_i, [_p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_dacts_bwd_t": (_i, [_p, _p, _p, _p, _f, _p, _i64, _p, _i64, _i64, _i64, _i, _p]),
@@ -97,6 +101,8 @@ def load(path=LIB_PATH):
     # tuning hook outside the public ABI: which bf16 layouts run the ping-pong GEMM loop
     lib.cc_debug_set_pp_mask.restype = None
     lib.cc_debug_set_pp_mask.argtypes = [ctypes.c_int]
+    lib.cc_debug_set_tail_fence.restype = None
+    lib.cc_debug_set_tail_fence.argtypes = [ctypes.c_int]
     _lib = lib
     return lib
 

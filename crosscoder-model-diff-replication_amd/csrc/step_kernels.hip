@@ -124,48 +124,68 @@ __global__ __launch_bounds__(256) void prep_kernel(const void* __restrict__ x_in
 // Block = 64 columns x 4 waves; wave w sums rows w, w+4, ... (independent loads in flight),
 // then a fixed-order combine of the 4 wave partials.  One sq / dot partial per block.
 constexpr int RED_COLS = 64;
-template <int DT>
-__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ part, int R, int C, int64_t ld,
-                                                          float scale, float* __restrict__ out_f32,
-                                                          void* __restrict__ out_t, float* __restrict__ sq_part,
-                                                          const float* __restrict__ dot_w, float* __restrict__ dot_part) {
-  __shared__ float red[4][RED_COLS];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int j = blockIdx.x * RED_COLS + lane;
+// Phase 1 (all 4 waves of a 256-thread group, t = thread in the group): column sums into red;
+// phase 2 (after a barrier, wave 0 of the group): outputs + the group's sq / dot partial.  The
+// stand-alone kernel and the fused tail kernels (grad_tail / loss_tail) run the same two phases.
+struct RedSeg {
+  const float* part;
+  int R, C;
+  int64_t ld;
+  float scale;
+  float* out_f32;
+  void* out_t;
+  float* sq_part;
+  const float* dot_w;
+  float* dot_part;
+};
+CC_DEV void reduce_rows_phase1(const RedSeg& a, int blk, int t, float (*red)[RED_COLS]) {
+  const int lane = t & 63, wave = t >> 6;
+  const int j = blk * RED_COLS + lane;
   float s = 0.f;
-  if (j < C) {
-    float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (j < a.C) {
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
     int i = wave;
-    for (; i + 12 < R; i += 16) {
+    for (; i + 12 < a.R; i += 16) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) a[u] += part[(int64_t)(i + 4 * u) * ld + j];
+      for (int u = 0; u < 4; ++u) v[u] += a.part[(int64_t)(i + 4 * u) * a.ld + j];
     }
-    for (; i < R; i += 4) a[0] += part[(int64_t)i * ld + j];
-    s = (a[0] + a[1]) + (a[2] + a[3]);
+    for (; i < a.R; i += 4) v[0] += a.part[(int64_t)i * a.ld + j];
+    s = (v[0] + v[1]) + (v[2] + v[3]);
   }
   red[wave][lane] = s;
-  __syncthreads();
-  if (wave != 0) return;
+}
+template <int DT>
+CC_DEV void reduce_rows_phase2(const RedSeg& a, int blk, int t, float (*red)[RED_COLS]) {
+  if ((t >> 6) != 0) return;
+  const int lane = t & 63;
+  const int j = blk * RED_COLS + lane;
   float sq = 0.f, dot = 0.f;
-  if (j < C) {
-    s = (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]) * scale;
-    if (out_f32) out_f32[j] = s;
-    if (out_t) {
+  if (j < a.C) {
+    float s = (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]) * a.scale;
+    if (a.out_f32) a.out_f32[j] = s;
+    if (a.out_t) {
       typename Elem<DT>::T q = Elem<DT>::from_f(s);
-      ((typename Elem<DT>::T*)out_t)[j] = q;
+      ((typename Elem<DT>::T*)a.out_t)[j] = q;
       float vq = Elem<DT>::to_f(q);
       sq = vq * vq;
     }
-    if (dot_part) dot = s * dot_w[j];
+    if (a.dot_part) dot = s * a.dot_w[j];
   }
-  if (sq_part) {
+  if (a.sq_part) {
     sq = wave_sum(sq);
-    if (lane == 0) sq_part[blockIdx.x] = sq;
+    if (lane == 0) a.sq_part[blk] = sq;
   }
-  if (dot_part) {
+  if (a.dot_part) {
     dot = wave_sum(dot);
-    if (lane == 0) dot_part[blockIdx.x] = dot;
+    if (lane == 0) a.dot_part[blk] = dot;
   }
+}
+template <int DT>
+__global__ __launch_bounds__(256) void reduce_rows_kernel(const RedSeg a) {
+  __shared__ float red[4][RED_COLS];
+  reduce_rows_phase1(a, blockIdx.x, threadIdx.x, red);
+  __syncthreads();
+  reduce_rows_phase2<DT>(a, blockIdx.x, threadIdx.x, red);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -300,54 +320,87 @@ __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ rec
 
 // Per-row explained variances (crosscoder.py:110-121) + per-block partial sums of the row terms.
 // grid ceil(B/256), block 256. part_out[blk][4] = {sum l2_row, sum ev, sum ev_a, sum ev_b}.
-__global__ __launch_bounds__(256) void ev_kernel(const float* __restrict__ row_part, int B, int n, int ncb,
-                                                 float* __restrict__ ev, float* __restrict__ ev_a,
-                                                 float* __restrict__ ev_b, float* __restrict__ part_out) {
-  __shared__ float red[4][4];
-  const int r = blockIdx.x * 256 + threadIdx.x;
+struct EvSeg {
+  const float* row_part;
+  int B, n, ncb;
+  float* ev;
+  float* ev_a;
+  float* ev_b;
+  float* part_out;
+};
+CC_DEV void ev_phase1(const EvSeg& a, int blk, int t, float (*red)[4]) {
+  const int r = blk * 256 + t;
   float v[4] = {0, 0, 0, 0};
-  if (r < B) {
+  if (r < a.B) {
+    const int B = a.B, n = a.n, ncb = a.ncb;
     const int64_t plane = (int64_t)n * ncb * B;
     const float eps = 1e-8f;
     float l2 = 0.f, tv = 0.f, l2m[2] = {0, 0}, tvm[2] = {0, 0};
     for (int m = 0; m < n; ++m) {
-      float a = 0.f, t = 0.f;
+      float s = 0.f, u = 0.f;
       for (int cb = 0; cb < ncb; ++cb) {
-        a += row_part[(int64_t)(m * ncb + cb) * B + r];
-        t += row_part[plane + (int64_t)(m * ncb + cb) * B + r];
+        s += a.row_part[(int64_t)(m * ncb + cb) * B + r];
+        u += a.row_part[plane + (int64_t)(m * ncb + cb) * B + r];
       }
-      l2 += a;
-      tv += t;
-      if (m < 2) { l2m[m] = a; tvm[m] = t; }
+      l2 += s;
+      tv += u;
+      if (m < 2) { l2m[m] = s; tvm[m] = u; }
     }
     float e = 1.f - l2 / (tv + eps);
     float ea = 1.f - l2m[0] / (tvm[0] + eps);
     float eb = n > 1 ? 1.f - l2m[1] / (tvm[1] + eps) : 0.f;
-    if (ev) ev[r] = e;
-    if (ev_a) ev_a[r] = ea;
-    if (ev_b) ev_b[r] = eb;
+    if (a.ev) a.ev[r] = e;
+    if (a.ev_a) a.ev_a[r] = ea;
+    if (a.ev_b) a.ev_b[r] = eb;
     v[0] = l2; v[1] = e; v[2] = ea; v[3] = eb;
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     float s = wave_sum(v[q]);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = s;
+    if ((t & 63) == 0) red[t >> 6][q] = s;
   }
+}
+CC_DEV void ev_phase2(const EvSeg& a, int blk, int t, float (*red)[4]) {
+  if (t < 4) {
+    int q = t;
+    a.part_out[blk * 4 + q] = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
+  }
+}
+__global__ __launch_bounds__(256) void ev_kernel(const EvSeg a) {
+  __shared__ float red[4][4];
+  ev_phase1(a, blockIdx.x, threadIdx.x, red);
   __syncthreads();
-  if (threadIdx.x < 4) {
-    int q = threadIdx.x;
-    part_out[blockIdx.x * 4 + q] = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
-  }
+  ev_phase2(a, blockIdx.x, threadIdx.x, red);
 }
 
 // Single block: scalars = {l2, l1, l0, mean ev, mean ev_a, mean ev_b}.
 constexpr int SCAL_THREADS = 1024;
-__global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const float* __restrict__ ev_part, int nblk,
-                                                                    const float* __restrict__ l1_part, int64_t n_l1,
-                                                                    const float* __restrict__ l0_part, int64_t n_wave,
-                                                                    int B, float* __restrict__ scalars,
-                                                                    float* __restrict__ l1l0_out,
-                                                                    float* __restrict__ host_out, unsigned seq) {
+struct ScalArgs {
+  const float* ev_part;
+  int nblk;
+  const float* l1_part;
+  int64_t n_l1;
+  const float* l0_part;
+  int64_t n_wave;
+  int B;
+  float* scalars;
+  float* l1l0_out;
+  float* host_out;
+  unsigned seq;
+};
+// 1024 threads (SCAL_THREADS), one block
+CC_DEV void loss_scalars_body(const ScalArgs& sa) {
+  const float* __restrict__ ev_part = sa.ev_part;
+  const int nblk = sa.nblk;
+  const float* __restrict__ l1_part = sa.l1_part;
+  const int64_t n_l1 = sa.n_l1;
+  const float* __restrict__ l0_part = sa.l0_part;
+  const int64_t n_wave = sa.n_wave;
+  const int B = sa.B;
+  float* __restrict__ scalars = sa.scalars;
+  float* __restrict__ l1l0_out = sa.l1l0_out;
+  float* __restrict__ host_out = sa.host_out;
+  const unsigned seq = sa.seq;
   constexpr int NW = SCAL_THREADS / 64;
   __shared__ double red[NW][6];
   double acc[6] = {0, 0, 0, 0, 0, 0};
@@ -400,6 +453,8 @@ __global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const float*
   }
 }
 
+__global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const ScalArgs a) { loss_scalars_body(a); }
+
 // ---------------------------------------------------------------------------------------
 CC_DEV float bf16r(float f) { return bf2f(f2bf(f)); }
 
@@ -413,7 +468,8 @@ struct ClipArgs {
   int sums_only;   // cc_segment_sums: out[p] = the raw per-parameter sum (0 where zero_mask has bit p)
   int zero_mask;
 };
-__global__ __launch_bounds__(SCAL_THREADS) void clip_kernel(const ClipArgs a) {
+// 1024 threads (SCAL_THREADS), one block
+CC_DEV void clip_body(const ClipArgs& a) {
   constexpr int NW = SCAL_THREADS / 64;
   __shared__ double red[8][NW];
   __shared__ float norms[8];
@@ -477,6 +533,70 @@ __global__ __launch_bounds__(SCAL_THREADS) void clip_kernel(const ClipArgs a) {
     a.out[1] = total;
     for (int p = 0; p < a.nparams; ++p) a.out[2 + p] = norms[p];
   }
+}
+
+__global__ __launch_bounds__(SCAL_THREADS) void clip_kernel(const ClipArgs a) { clip_body(a); }
+
+// ---------------------------------------------------------------------------------------
+// Fused step tails: one launch of 1024-thread blocks = 4 independent 256-thread groups, each
+// running one block of a column reduction (RedSeg) or of ev_kernel (EvSeg) -- the same two phases
+// as the stand-alone kernels, so the same bits -- then the last block to finish (device-scope
+// arrival counter, reset by that block for the next launch) runs the single-block finaliser
+// (clip_body or loss_scalars_body) over the partials the whole grid wrote.  Saves the finaliser's
+// launch (and, for the loss tail, one reduction launch) per step.
+//   grad tail: b_enc.grad, b_dec.grad column sums + their sq partials -> clip coefficient
+//   loss tail: sum_b acts + l1 partials, per-row EV + partials -> the loss scalars
+struct TailArgs {
+  RedSeg red[2];
+  int red_blocks[2];  // 256-thread groups per reduction (0: unused)
+  EvSeg ev;
+  int ev_blocks;      // 0: no EV segment
+  int finalize;       // 0: clip_body(clip), 1: loss_scalars_body(scal)
+  ClipArgs clip;
+  ScalArgs scal;
+  unsigned* counter;
+  int fence_all;
+};
+static int g_tail_fence_all = 0;  // cc_debug_set_tail_fence (A/B tooling, not part of the ABI)
+template <int DT>
+__global__ __launch_bounds__(SCAL_THREADS) void tail_kernel(const TailArgs a) {
+  __shared__ float red[4][4][RED_COLS];
+  __shared__ float evred[4][4][4];
+  __shared__ int last;
+  const int grp = threadIdx.x >> 8, t = threadIdx.x & 255;
+  int b = blockIdx.x * 4 + grp;
+  // role of this group: reduction 0, reduction 1, EV block or idle (uniform per group)
+  int role = 3;
+  if (b < a.red_blocks[0]) {
+    role = 0;
+  } else if ((b -= a.red_blocks[0]) < a.red_blocks[1]) {
+    role = 1;
+  } else if ((b -= a.red_blocks[1]) < a.ev_blocks) {
+    role = 2;
+  }
+  if (role < 2) reduce_rows_phase1(a.red[role], b, t, red[grp]);
+  else if (role == 2) ev_phase1(a.ev, b, t, evred[grp]);
+  __syncthreads();
+  if (role < 2) reduce_rows_phase2<DT>(a.red[role], b, t, red[grp]);
+  else if (role == 2) ev_phase2(a.ev, b, t, evred[grp]);
+  // publish this block's partials, then count arrivals.  The barrier's workgroup-scope release
+  // waits for every wave's stores to reach this XCD's L2; ONE agent-scope release (an L2
+  // write-back) then publishes them all before the arrival count.  (fence_all: every thread fences,
+  // seq_cst -- an L2 write-back + invalidate per wave; measured slower, A/B switch.)
+  if (a.fence_all) __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const bool is_last = atomicAdd(a.counter, 1u) == gridDim.x - 1;
+    if (is_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // drop stale lines before the reads
+    last = is_last;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (a.fence_all) __threadfence();
+  if (a.finalize == 0) clip_body(a.clip);
+  else loss_scalars_body(a.scal);
+  if (threadIdx.x == 0) atomicExch(a.counter, 0u);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -750,12 +870,11 @@ int cc_reduce_rows(const float* part, int64_t R, int64_t C, int64_t ld, float sc
   if (dot_part && !dot_w) return CC_ERR_NULL;
   dim3 grid((unsigned)((C + RED_COLS - 1) / RED_COLS));
   hipStream_t st = (hipStream_t)stream;
+  const RedSeg a = {part, (int)R, (int)C, ld, scale, out_f32, out_t, sq_part, dot_w, dot_part};
   if (out_t) {
-    DISPATCH_DT(dtype, hipLaunchKernelGGL((reduce_rows_kernel<DT_>), grid, dim3(256), 0, st, part, (int)R, (int)C, ld,
-                                          scale, out_f32, out_t, sq_part, dot_w, dot_part));
+    DISPATCH_DT(dtype, hipLaunchKernelGGL((reduce_rows_kernel<DT_>), grid, dim3(256), 0, st, a));
   } else {
-    hipLaunchKernelGGL((reduce_rows_kernel<CC_F32>), grid, dim3(256), 0, st, part, (int)R, (int)C, ld, scale, out_f32,
-                       nullptr, nullptr, dot_w, dot_part);
+    hipLaunchKernelGGL((reduce_rows_kernel<CC_F32>), grid, dim3(256), 0, st, a);
   }
   CC_LAUNCH_CHECK();
   return CC_OK;
@@ -838,9 +957,10 @@ int cc_loss_finalize_mapped(const float* row_part, const float* l1_part, int64_t
   int nblk = (int)((B + 255) / 256);
   float* ev_part = scalars + 8;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(ev_kernel, dim3(nblk), dim3(256), 0, st, row_part, (int)B, (int)n, ncb, ev, ev_a, ev_b, ev_part);
-  hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(SCAL_THREADS), 0, st, ev_part, nblk, l1_part, n_l1, l0_part,
-                     n_l0, (int)B, scalars, l1l0_out, host_out, (unsigned)seq);
+  const EvSeg e = {row_part, (int)B, (int)n, ncb, ev, ev_a, ev_b, ev_part};
+  hipLaunchKernelGGL(ev_kernel, dim3(nblk), dim3(256), 0, st, e);
+  const ScalArgs s = {ev_part, nblk, l1_part, n_l1, l0_part, n_l0, (int)B, scalars, l1l0_out, host_out, (unsigned)seq};
+  hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(SCAL_THREADS), 0, st, s);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }
@@ -951,6 +1071,63 @@ int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const 
   DISPATCH_DT(dtype, hipLaunchKernelGGL((adam_kernel<DT_>), dim3((unsigned)blocks), dim3(256), 0, st, a));
   CC_LAUNCH_CHECK();
 #endif
+  return CC_OK;
+}
+
+
+void cc_debug_set_tail_fence(int all) { g_tail_fence_all = all; }
+
+int cc_grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,
+                 const float* loss_colpart, int64_t R_dec, int64_t K, void* g_b_dec, float* sq_b_dec, int dtype,
+                 const float* sq, const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
+                 uint32_t* counter, void* stream) {
+  if (!gpre_colpart || !g_b_enc || !sq_b_enc || !loss_colpart || !g_b_dec || !sq_b_dec || !sq || !off || !clip_out ||
+      !counter)
+    return CC_ERR_NULL;
+  if (R_enc <= 0 || R_dec <= 0 || h <= 0 || K <= 0) return CC_ERR_SHAPE;
+  if (nparams <= 0 || nparams > 8) return CC_ERR_SHAPE;
+  TailArgs a = {};
+  a.red[0] = {gpre_colpart, (int)R_enc, (int)h, h, 1.f, nullptr, g_b_enc, sq_b_enc, nullptr, nullptr};
+  a.red[1] = {loss_colpart, (int)R_dec, (int)K, K, 1.f, nullptr, g_b_dec, sq_b_dec, nullptr, nullptr};
+  a.red_blocks[0] = (int)((h + RED_COLS - 1) / RED_COLS);
+  a.red_blocks[1] = (int)((K + RED_COLS - 1) / RED_COLS);
+  a.finalize = 0;
+  a.clip.sq = sq;
+  for (int i = 0; i <= nparams; ++i) a.clip.off[i] = off[i];
+  a.clip.nparams = nparams;
+  a.clip.max_norm = max_norm;
+  a.clip.emulate_bf16 = emulate_bf16;
+  a.clip.out = clip_out;
+  a.counter = counter;
+  a.fence_all = g_tail_fence_all;
+  dim3 grid((unsigned)((a.red_blocks[0] + a.red_blocks[1] + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_DT(dtype, hipLaunchKernelGGL((tail_kernel<DT_>), grid, dim3(SCAL_THREADS), 0, st, a));
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+int cc_loss_tail(const float* acts_colpart, int64_t R, int64_t h, float* colsum_acts, const float* tn,
+                 float* l1_part, const float* row_part, const float* l0_part, int64_t n_l0, float* ev, float* ev_a,
+                 float* ev_b, float* scalars, float* l1l0_out, float* host_out, uint32_t seq, int64_t B, int64_t n,
+                 int64_t d, uint32_t* counter, void* stream) {
+  if (!acts_colpart || !colsum_acts || !tn || !l1_part || !row_part || !scalars || !counter) return CC_ERR_NULL;
+  if (R <= 0 || h <= 0 || B <= 0 || n <= 0 || d <= 0) return CC_ERR_SHAPE;
+  TailArgs a = {};
+  const int nred = (int)((h + RED_COLS - 1) / RED_COLS);
+  const int nblk = (int)((B + 255) / 256);
+  float* ev_part = scalars + 8;  // as cc_loss_finalize (cc_loss_scalars_len)
+  a.red[0] = {acts_colpart, (int)R, (int)h, h, 1.f, colsum_acts, nullptr, nullptr, tn, l1_part};
+  a.red_blocks[0] = nred;
+  a.ev = {row_part, (int)B, (int)n, (int)cc_loss_col_blocks(d), ev, ev_a, ev_b, ev_part};
+  a.ev_blocks = nblk;
+  a.finalize = 1;
+  a.scal = {ev_part, nblk, l1_part, nred, l0_part, n_l0, (int)B, scalars, l1l0_out, host_out, (unsigned)seq};
+  a.counter = counter;
+  a.fence_all = g_tail_fence_all;
+  dim3 grid((unsigned)((nred + nblk + 3) / 4));
+  hipLaunchKernelGGL((tail_kernel<CC_F32>), grid, dim3(SCAL_THREADS), 0, (hipStream_t)stream, a);
+  CC_LAUNCH_CHECK();
   return CC_OK;
 }
 

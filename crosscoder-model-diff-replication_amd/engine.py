@@ -149,6 +149,9 @@ class StepWorkspace:
             self.sq_off.append(self.sq_off[-1] + s)
         self.sq = E(self.sq_off[-1])
         self.clip_out = E(8)
+        self.clip_ready = False  # backward(clip=...) already wrote clip_out (fused grad tail)
+        # arrival counters of the fused tail launches (loss tail, grad tail); each launch leaves 0
+        self.tail_ctr = torch.zeros(2, dtype=torch.int32, device=device)
         self.norms_token = None
         self.host = None  # _hip.MappedHostBuffer for the loss scalars (Trainer), or None
         self.host_seq = 0
@@ -222,6 +225,11 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
             ops.decode_partial_t(ws.acts, ws.W_dec_t, ws.recon, ws.dec_ws)
         else:
             ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
+    if loss and FUSED_TAILS:
+        # loss rows + g_recon, then ONE launch: the activation column sums + l1 partials, EV, scalars
+        loss_rows(ws, P, 0, B, grad_scale)
+        loss_tail(ws)
+        return
     # sum_b acts (for dL1/dW_dec) and B * l1 = sum_h colsum_acts[h] * tn[h] (crosscoder.py:126)
     ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts, dot_w=ws.tn,
                     dot_part=ws.l1_part)
@@ -243,6 +251,14 @@ def loss_finalize(ws, l1l0_out=None):
         ws.host_seq = (ws.host_seq + 1) & 0xFFFFFFFF or 1
     ops.loss_finalize(ws.row_part, ws.l1_part, ws.n_l1, ws.l0_part, ws.n_wave, ws.ev, ws.ev_a, ws.ev_b, ws.scalars,
                       ws.B, ws.n, ws.d, l1l0_out=l1l0_out, host=ws.host, seq=ws.host_seq)
+
+
+def loss_tail(ws):
+    """= reduce_rows(acts column sums, dot_w=tn -> l1 partials) + loss_finalize, one launch."""
+    if ws.host is not None:
+        ws.host_seq = (ws.host_seq + 1) & 0xFFFFFFFF or 1
+    ops.loss_tail(ws.acts_colpart, ws.h, ws.colsum_acts, ws.tn, ws.l1_part, ws.row_part, ws.l0_part, ws.n_wave, ws.ev,
+                  ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], host=ws.host, seq=ws.host_seq)
 
 
 def loss_from_recon(ws, P, grad_scale=None):
@@ -271,9 +287,11 @@ def dacts_rows(ws, P, l1_coeff, r0, r1, l1_grad_weight=1.0):
                           colsum_part=ws.gpre_colpart[c0:c1])
 
 
-def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False):
+def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None):
     """Gradients of l2 + l1_coeff * l1 into the grads Arena G (+ squared-sum partials).
-    dacts_done: G3 already ran per batch slice (dacts_rows)."""
+    dacts_done: G3 already ran per batch slice (dacts_rows).  clip (max_norm, single-GPU step): the
+    bias-gradient sums and clip_grad_norm_'s coefficient in one launch (clip_and_adam then skips
+    its clip_finalize)."""
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
     l1_scale = float(l1_coeff) * l1_grad_weight / B
     if not dacts_done:
@@ -285,9 +303,18 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False):
         else:
             ops.wgrad_both(ws.acts, ws.g_recon, P.W_dec_hk, ws.inv_norms, ws.colsum_acts, l1_scale, G.W_dec_hk,
                            ws.sq_slice(1), ws.g_pre, ws.x, G.W_enc_hk, ws.sq_slice(0), n, d)
+    if clip is not None and FUSED_TAILS:
+        ops.grad_tail(ws.gpre_colpart, G.b_enc, ws.sq_slice(2), ws.loss_colpart, G.b_dec_flat, ws.sq_slice(3), ws.sq,
+                      ws.sq_off, clip, ws.dtype == torch.bfloat16, ws.clip_out, ws.tail_ctr[1:2])
+        ws.clip_ready = True
+        return
     ops.reduce_rows(ws.gpre_colpart, ws.gpre_colpart.shape[0], h, out_t=G.b_enc, sq_part=ws.sq_slice(2))
     ops.reduce_rows(ws.loss_colpart, ws.loss_colpart.shape[0], K, out_t=G.b_dec_flat, sq_part=ws.sq_slice(3))
 
+
+# the forward's / backward's small reductions + finalisers as single launches (loss_tail, grad_tail;
+# bit-identical to the separate launches -- A/B switch for tools/ and tests)
+FUSED_TAILS = True
 
 # workgroups of the decoder-half Adam that runs beside the next step's G1 (0: uncapped one-pass)
 DEC_ADAM_BLOCKS = 256
@@ -302,7 +329,9 @@ FUSED_DEC_ADAM = "serial"
 def clip_and_adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, max_norm=1.0, side_stream=None):
     """clip_grad_norm_ (from the squared-sum slabs of the backward) + Adam (see adam())."""
     emulate = ws.dtype == torch.bfloat16
-    ops.clip_finalize(ws.sq, ws.sq_off, max_norm, emulate, ws.clip_out)
+    if not ws.clip_ready:
+        ops.clip_finalize(ws.sq, ws.sq_off, max_norm, emulate, ws.clip_out)
+    ws.clip_ready = False
     adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream)
 
 

@@ -205,6 +205,25 @@ def loss_finalize(row_part, l1_part, n_l1, l0_part, n_l0, ev, ev_a, ev_b, scalar
                                  _ptr(ev_b), _ptr(scalars), _ptr(l1l0_out), B, n, d, _stream(row_part)))
 
 
+def loss_tail(acts_colpart, h, colsum_acts, tn, l1_part, row_part, l0_part, n_l0, ev, ev_a, ev_b, scalars, B, n, d,
+              counter, l1l0_out=None, host=None, seq=0):
+    """reduce_rows(acts_colpart, dot_w=tn, dot_part=l1_part) + loss_finalize as one launch (same bits)."""
+    check(lib().cc_loss_tail(_ptr(acts_colpart), acts_colpart.shape[0], h, _ptr(colsum_acts), _ptr(tn), _ptr(l1_part),
+                             _ptr(row_part), _ptr(l0_part), n_l0, _ptr(ev), _ptr(ev_a), _ptr(ev_b), _ptr(scalars),
+                             _ptr(l1l0_out), host.device_ptr if host is not None else None, seq, B, n, d,
+                             _ptr(counter), _stream(acts_colpart)))
+
+
+def grad_tail(gpre_colpart, g_b_enc, sq_b_enc, loss_colpart, g_b_dec, sq_b_dec, sq, offsets, max_norm, emulate_bf16,
+              out, counter):
+    """The two bias-gradient reduce_rows (+ sq partials) + clip_finalize as one launch (same bits)."""
+    arr = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
+    check(lib().cc_grad_tail(_ptr(gpre_colpart), gpre_colpart.shape[0], gpre_colpart.shape[1], _ptr(g_b_enc),
+                             _ptr(sq_b_enc), _ptr(loss_colpart), loss_colpart.shape[0], loss_colpart.shape[1],
+                             _ptr(g_b_dec), _ptr(sq_b_dec), dtype_code(g_b_enc.dtype), _ptr(sq), arr, len(offsets) - 1,
+                             max_norm, int(emulate_bf16), _ptr(out), _ptr(counter), _stream(sq)))
+
+
 def segment_sums(sq, offsets, out, zero_mask=0):
     """out[p] = sum(sq[offsets[p]:offsets[p+1]]) (0 where bit p of zero_mask is set)."""
     arr = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])

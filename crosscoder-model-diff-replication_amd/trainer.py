@@ -107,7 +107,7 @@ class Trainer:
         if on_losses is not None:
             on_losses(ws.scalars)
         l1c = self.get_l1_coeff()
-        engine.backward(ws, P, opt.grads, l1c)
+        engine.backward(ws, P, opt.grads, l1c, clip=1.0)  # clip_grad_norm_(max_norm=1.0), trainer.py:46
         g = opt.param_groups[0]
         opt.t += 1
         b1, b2 = g["betas"]

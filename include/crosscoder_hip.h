@@ -166,6 +166,18 @@ int cc_loss_finalize_mapped(const float* row_part, const float* l1_part, int64_t
                             int64_t n_l0, float* ev, float* ev_a, float* ev_b, float* scalars, float* l1l0_out,
                             float* host_out, uint32_t seq, int64_t B, int64_t n, int64_t d, void* stream);
 
+/* One launch for the forward's tail (crosscoder.py:106-128): cc_reduce_rows of the activation
+ * column-sum partials acts_colpart [R x h] into colsum_acts [h] (= sum_b acts) with the L1 dot
+ * partials l1_part [cc_reduce_parts(h)] against tn [h], the per-row EV terms, and the loss scalars
+ * -- bit-identical to cc_reduce_rows(.., dot_w = tn, dot_part = l1_part) followed by
+ * cc_loss_finalize[_mapped](.., n_l1 = cc_reduce_parts(h), ..).  The last block to finish runs the
+ * scalar finaliser; `counter` is one device uint32, zero before the first call, left zero by
+ * every call (launches sharing a counter must be ordered, e.g. one stream).  host_out may be NULL. */
+int cc_loss_tail(const float* acts_colpart, int64_t R, int64_t h, float* colsum_acts, const float* tn,
+                 float* l1_part, const float* row_part, const float* l0_part, int64_t n_l0, float* ev, float* ev_a,
+                 float* ev_b, float* scalars, float* l1l0_out, float* host_out, uint32_t seq, int64_t B, int64_t n,
+                 int64_t d, uint32_t* counter, void* stream);
+
 /* Backward through decode + L1 + ReLU (autograd of crosscoder.py:77,84-89,126):
  * g_pre[B,h] = (g_recon . W_dec^T + l1_scale * tn[h]) * (acts > 0),  l1_scale = l1_coeff / B.
  * colsum_part [cc_col_part_rows(B) x h]: column sums of g_pre (-> b_enc.grad). */
@@ -212,6 +224,16 @@ int cc_wgrad_both_t(const void* actsT, const void* g_reconT, const void* W_dec, 
  * out[0] = coef, out[1] = total norm, out[2 + i] = norm_i  (fp32, device). */
 int cc_clip_finalize(const float* sq, const int64_t* off, int nparams, float max_norm, int emulate_bf16,
                      float* out, void* stream);
+
+/* One launch for the backward's tail (trainer.py:45-46): the bias gradients
+ * g_b_enc [h] = sum of gpre_colpart [R_enc x h], g_b_dec [K] = sum of loss_colpart [R_dec x K] (param
+ * dtype) with their squared-sum partials sq_b_enc / sq_b_dec [cc_reduce_parts(.)] (which must be the
+ * segments 2 and 3 of sq), then cc_clip_finalize over sq -- bit-identical to the two cc_reduce_rows
+ * launches + cc_clip_finalize.  counter: as cc_loss_tail. */
+int cc_grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,
+                 const float* loss_colpart, int64_t R_dec, int64_t K, void* g_b_dec, float* sq_b_dec, int dtype,
+                 const float* sq, const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
+                 uint32_t* counter, void* stream);
 
 /* Per-parameter sums of the squared-gradient partials, sq[off[p] .. off[p+1]) (nparams <= 8, off on
  * the HOST), for the latent-sharded step's all-reduce: out[p] = the sum (fp32), or 0 where bit p of

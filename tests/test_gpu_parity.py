@@ -812,3 +812,28 @@ def test_baseline_config_shapes_spot_check(gpu, B, n, d, h):
     # bias gradients
     assert rel(D(G.b_enc), gpre.sum(0)) < 1e-2
     assert rel(D(G.b_dec_flat), grec.sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("enc_dtype,B,n,d,h", [("bf16", 1024, 2, 256, 2048), ("fp32", 96, 2, 40, 200),
+                                               ("bf16", 512, 4, 64, 384), ("fp32", 256, 2, 64, 1000)])
+def test_fused_tails_match_separate_launches(gpu, enc_dtype, B, n, d, h, monkeypatch):
+    """The one-launch loss tail (acts column sums + l1 partials + EV + loss scalars, cc_loss_tail) and
+    grad tail (bias-gradient sums + clip coefficient, cc_grad_tail) take bit-identical Trainer steps
+    to the separate reduce_rows / loss_finalize / clip_finalize launches, and leave their arrival
+    counters at zero."""
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype=enc_dtype,
+               num_tokens=B * 20, device=str(gpu))
+    out = []
+    for fused in (True, False):
+        monkeypatch.setattr(engine, "FUSED_TAILS", fused)
+        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=1), crosscoder=ca.CrossCoder(cfg))
+        losses = [tr.step() for _ in range(3)]
+        tr.synchronize()
+        torch.cuda.synchronize()
+        ws, P, opt = tr.crosscoder._ws, tr.crosscoder.arena(), tr.optimizer
+        assert not bool(ws.tail_ctr.any())
+        out.append((losses, P.data.clone(), opt.exp_avg.data.clone(), opt.exp_avg_sq.data.clone(), opt.grads.data.clone(),
+                    ws.clip_out[:6].clone(), ws.ev.clone(), ws.ev_a.clone(), ws.colsum_acts.clone(), ws.l1_part.clone()))
+    assert out[0][0] == out[1][0]
+    for a, b in zip(out[0][1:], out[1][1:]):
+        assert torch.equal(a, b)

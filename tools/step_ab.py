@@ -27,9 +27,12 @@ def main():
 
     defaults = (tr.mapped_losses, tr.overlap_decoder_adam, engine.DEC_ADAM_BLOCKS)
 
-    def setup(ws, mapped=defaults[0], fused=True, side=defaults[1], blocks=defaults[2], fused_adam="serial"):
+    def setup(ws, mapped=defaults[0], fused=True, side=defaults[1], blocks=defaults[2], fused_adam="serial",
+              tails=True, fence_all=0):
         def f():
             cc._ws = ws
+            engine.FUSED_TAILS = tails
+            ca._lib.load().cc_debug_set_tail_fence(fence_all)
             engine.FUSED_DEC_ADAM = fused_adam
             tr.mapped_losses = mapped
             tr.overlap_decoder_adam = side
@@ -41,7 +44,8 @@ def main():
     variants = {"default": setup(ws_t), "fused dec Adam beside G1": setup(ws_t, fused_adam=True),
                 "fused dec Adam serial": setup(ws_t, side=False), "flat dec Adam serial": setup(ws_t, side=False,
                                                                                              fused_adam=False),
-                "side Adam 384 blocks": setup(ws_t, blocks=384), "batch-major wgrad": setup(ws_b)}
+                "side Adam 384 blocks": setup(ws_t, blocks=384), "batch-major wgrad": setup(ws_b),
+                "separate tails": setup(ws_t, tails=False), "tails fence all": setup(ws_t, fence_all=1)}
     only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--only=")]
     if only:
         variants = {k: v for k, v in variants.items() if k in only[0].split(",")}
