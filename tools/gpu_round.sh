@@ -2,7 +2,7 @@
 # One GPU-box session: parity tests, the bench line, a rocprofv3 kernel-trace summary of the same
 # bench command, and the GEMM / Adam A/B timers.  Every GPU step has its own time limit; the script
 # stops at the first fault, abort, segfault or timeout (test FAILURES -- exit 1 -- do not stop it).
-# Usage (repo root on the box): tools/gpu_round.sh [OUT] [steps...]   steps: test bench prof gemm ab stepab adam pmc
+# Usage (repo root on the box): tools/gpu_round.sh [OUT] [steps...]   steps: test bench prof gemm ab stepab small adam pmc
 OUT=${1:-gpurun_out/round}
 shift
 STEPS=${*:-test bench prof gemm adam}
@@ -35,6 +35,8 @@ for s in $STEPS; do
     ab) run gemm_ab 400 python tools/gemm_bench.py crosscoder-model-diff-replication_amd/exp/base.so \
           crosscoder-model-diff-replication_amd/libcrosscoder_hip.so ;;
     stepab) run step_ab 400 python tools/step_ab.py "--only=${STEPAB_ONLY:-default,separate tails}" ;;
+    small) run small_bench 200 python tools/small_bench.py crosscoder-model-diff-replication_amd/exp/base.so \
+             crosscoder-model-diff-replication_amd/libcrosscoder_hip.so ;;
     adam) run adam_bench 200 python tools/adam_bench.py crosscoder-model-diff-replication_amd/libcrosscoder_hip.so ;;
     pmc)
       run pmc_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc/p1" -o pmc -- \
