@@ -62,33 +62,26 @@ __global__ __launch_bounds__(256) void prep_kernel(const void* __restrict__ x_in
   float f = 1.f;
   if (factor && col < K) f = Elem<DF>::load((const typename Elem<DF>::T*)factor + col / d);
   if constexpr (TR) {
-    // both halves' rows (r0 + 32 * half + wave + 4k) in flight at once; the column sums still add
-    // rows in the order r0+w, r0+w+4, ...
-    float v[2][8][8];
-    if (col < K) {
-#pragma unroll
-      for (int half = 0; half < 2; ++half)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int r = r0 + 32 * half + wave + 4 * k;
-          if (r < B) load8<DIN>(x_in, (int64_t)r * K + col, v[half][k]);
-        }
-    }
-#pragma unroll
     for (int half = 0; half < 2; ++half) {
       const int base = r0 + 32 * half;
       if (base >= B) break;  // block-uniform
       if (col < K) {
+        // the wave's 8 rows of this half (base + w + 4k): all loads in flight; the column sums
+        // still add rows in the order r0+w, r0+w+4, ...
+        float v[8][8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (base + wave + 4 * k < B) load8<DIN>(x_in, (int64_t)(base + wave + 4 * k) * K + col, v[k]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const int r = base + wave + 4 * k;
           if (r >= B) break;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[half][k][j] = Elem<DT>::round(v[half][k][j] * f);
-          store8<DT>(x_out, (int64_t)r * K + col, v[half][k]);
-          tile_put8(lds, r - base, lane, v[half][k]);
+          for (int j = 0; j < 8; ++j) v[k][j] = Elem<DT>::round(v[k][j] * f);
+          store8<DT>(x_out, (int64_t)r * K + col, v[k]);
+          tile_put8(lds, r - base, lane, v[k]);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) cs[j] += v[half][k][j];
+          for (int j = 0; j < 8; ++j) cs[j] += v[k][j];
         }
       }
       __syncthreads();
@@ -267,51 +260,45 @@ __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ rec
     if (x_mean) load8f(x_mean, col, mu);
   }
   const int64_t plane = (int64_t)n * ncb * B;  // row_part [2][n*ncb][B]
-  // the wave's rows r0 + wave + 4i in batches of NR rows whose loads are all in flight together,
-  // each batch processed in row order
-#ifndef CC_LOSS_INFLIGHT
-#define CC_LOSS_INFLIGHT 2  // 2: 34.5 us at config 2, 4: 35.3, 8: 41.8 (tools/small_bench.py)
-#endif
-  constexpr int NR = CC_LOSS_INFLIGHT;
-  for (int i0 = 0; i0 < LOSS_ROWS / 4; i0 += NR) {
-  if (r0 + wave + 4 * i0 >= row_end) break;  // wave-uniform
-  float rv[NR][8], xv[NR][8];
-  if (cv) {
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int r = r0 + wave + 4 * (i0 + i);
-      if (r < row_end) {
-        load8f(recon, (int64_t)r * K + col, rv[i]);
-        load8<DT>(x, (int64_t)r * K + col, xv[i]);
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    const int r = r0 + wave + 4 * (i0 + i);
-    if (r >= row_end) break;  // wave-uniform
-    float l2 = 0.f, tv = 0.f;
+  // two rows per trip (r, r + 4): both rows' loads are in flight together
+  for (int i = 0; i < LOSS_ROWS / 4; i += 2) {
+    const int ra = r0 + wave + 4 * i;
+    if (ra >= row_end) break;  // wave-uniform
+    float rv[2][8], xv[2][8];
     if (cv) {
-      float g[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float diff = (rv[i][j] + bd[j]) - xv[i][j];
-        l2 += diff * diff;
-        float c = xv[i][j] - mu[j];
-        tv += c * c;
-        g[j] = E::round(grad_scale * diff);
-        cs[j] += g[j];
+      for (int u = 0; u < 2; ++u)
+        if (ra + 4 * u < row_end) {
+          load8f(recon, (int64_t)(ra + 4 * u) * K + col, rv[u]);
+          load8<DT>(x, (int64_t)(ra + 4 * u) * K + col, xv[u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = ra + 4 * u;
+      if (r >= row_end) break;
+      float l2 = 0.f, tv = 0.f;
+      if (cv) {
+        float g[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float diff = (rv[u][j] + bd[j]) - xv[u][j];
+          l2 += diff * diff;
+          float c = xv[u][j] - mu[j];
+          tv += c * c;
+          g[j] = E::round(grad_scale * diff);
+          cs[j] += g[j];
+        }
+        store8<DT>(g_recon, (int64_t)r * K + col, g);
+        if constexpr (TR) tile_put8(tile, r - r0, lane, g);
       }
-      store8<DT>(g_recon, (int64_t)r * K + col, g);
-      if constexpr (TR) tile_put8(tile, r - r0, lane, g);
+      l2 = wave_sum(l2);
+      tv = wave_sum(tv);
+      if (lane == 0) {
+        row_part[(int64_t)blockIdx.x * B + r] = l2;
+        row_part[plane + (int64_t)blockIdx.x * B + r] = tv;
+      }
     }
-    l2 = wave_sum(l2);
-    tv = wave_sum(tv);
-    if (lane == 0) {
-      row_part[(int64_t)blockIdx.x * B + r] = l2;
-      row_part[plane + (int64_t)blockIdx.x * B + r] = tv;
-    }
-  }
   }
   if constexpr (TR) {
     __syncthreads();

@@ -150,6 +150,7 @@ class StepWorkspace:
         self.sq = E(self.sq_off[-1])
         self.clip_out = E(8)
         self.clip_ready = False  # backward(clip=...) already wrote clip_out (fused grad tail)
+        self.acts_pending = False  # forward deferred the activation column sums to loss_finalize
         # arrival counters of the fused tail launches (loss tail, grad tail); each launch leaves 0
         self.tail_ctr = torch.zeros(2, dtype=torch.int32, device=device)
         self.norms_token = None
@@ -225,14 +226,13 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
             ops.decode_partial_t(ws.acts, ws.W_dec_t, ws.recon, ws.dec_ws)
         else:
             ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
-    if loss and FUSED_TAILS:
-        # loss rows + g_recon, then ONE launch: the activation column sums + l1 partials, EV, scalars
-        loss_rows(ws, P, 0, B, grad_scale)
-        loss_tail(ws)
-        return
-    # sum_b acts (for dL1/dW_dec) and B * l1 = sum_h colsum_acts[h] * tn[h] (crosscoder.py:126)
-    ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts, dot_w=ws.tn,
-                    dot_part=ws.l1_part)
+    if FUSED_TAILS:
+        # the activation column sums + l1 partials ride in the loss finaliser's launch (loss_tail)
+        ws.acts_pending = True
+    else:
+        # sum_b acts (for dL1/dW_dec) and B * l1 = sum_h colsum_acts[h] * tn[h] (crosscoder.py:126)
+        ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts, dot_w=ws.tn,
+                        dot_part=ws.l1_part)
     if loss:
         loss_from_recon(ws, P, grad_scale)
 
@@ -246,19 +246,25 @@ def loss_rows(ws, P, r0, r1, grad_scale=None):
 
 def loss_finalize(ws, l1l0_out=None):
     """Loss scalars / EV vectors; with ws.host (a mapped host buffer, set by the Trainer) the
-    scalars also land in host memory followed by the sequence word ws.host_seq."""
+    scalars also land in host memory followed by the sequence word ws.host_seq.  After a forward
+    that deferred the activation column sums (FUSED_TAILS), one launch does both (loss_tail)."""
+    if ws.acts_pending:
+        loss_tail(ws, l1l0_out)
+        return
     if ws.host is not None:
         ws.host_seq = (ws.host_seq + 1) & 0xFFFFFFFF or 1
     ops.loss_finalize(ws.row_part, ws.l1_part, ws.n_l1, ws.l0_part, ws.n_wave, ws.ev, ws.ev_a, ws.ev_b, ws.scalars,
                       ws.B, ws.n, ws.d, l1l0_out=l1l0_out, host=ws.host, seq=ws.host_seq)
 
 
-def loss_tail(ws):
+def loss_tail(ws, l1l0_out=None):
     """= reduce_rows(acts column sums, dot_w=tn -> l1 partials) + loss_finalize, one launch."""
     if ws.host is not None:
         ws.host_seq = (ws.host_seq + 1) & 0xFFFFFFFF or 1
     ops.loss_tail(ws.acts_colpart, ws.h, ws.colsum_acts, ws.tn, ws.l1_part, ws.row_part, ws.l0_part, ws.n_wave, ws.ev,
-                  ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], host=ws.host, seq=ws.host_seq)
+                  ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], l1l0_out=l1l0_out, host=ws.host,
+                  seq=ws.host_seq)
+    ws.acts_pending = False
 
 
 def loss_from_recon(ws, P, grad_scale=None):

@@ -45,7 +45,8 @@ def main():
                 "fused dec Adam serial": setup(ws_t, side=False), "flat dec Adam serial": setup(ws_t, side=False,
                                                                                              fused_adam=False),
                 "side Adam 384 blocks": setup(ws_t, blocks=384), "batch-major wgrad": setup(ws_b),
-                "separate tails": setup(ws_t, tails=False), "tails fence all": setup(ws_t, fence_all=1)}
+                "separate tails": setup(ws_t, tails=False), "tails fence all": setup(ws_t, fence_all=1),
+                "mapped losses": setup(ws_t, mapped=True)}
     only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--only=")]
     if only:
         variants = {k: v for k, v in variants.items() if k in only[0].split(",")}
