@@ -322,6 +322,9 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
 # bit-identical to the separate launches -- A/B switch for tools/ and tests)
 FUSED_TAILS = True
 
+# the side-stream decoder-half Adam starts after the encoder half (True) or beside it (False)
+SIDE_AFTER_ENC = True
+
 # workgroups of the decoder-half Adam that runs beside the next step's G1 (0: uncapped one-pass)
 DEC_ADAM_BLOCKS = 256
 # decoder-half Adam in 64x64 tiles that also write W_dec^T and the norm partials (transposed mode,
@@ -352,13 +355,20 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None):
             ops.adam_step(P.data, G.data, M.data, V.data, ws.clip_out[0:1], lr, beta1, beta2, eps, step)
         return
     coef = ws.clip_out[0:1]
-    with _span("adam"):
-        ops.adam_step(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), coef, lr, beta1, beta2, eps, step)
+    if side_stream is None:
+        with _span("adam"):
+            ops.adam_step(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), coef, lr, beta1, beta2, eps, step)
     if side_stream is not None:
         # the decoder half starts after the encoder half (both are HBM-bound: run together they only
         # share the bandwidth), i.e. beside the next step's prep / G1 on the main stream
+        # (SIDE_AFTER_ENC False: it waits for the clip coefficient only -- A/B switch for tools/)
         enc_done = torch.cuda.Event()
-        enc_done.record(torch.cuda.current_stream(P.data.device))
+        if not SIDE_AFTER_ENC:
+            enc_done.record(torch.cuda.current_stream(P.data.device))
+        with _span("adam"):
+            ops.adam_step(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), coef, lr, beta1, beta2, eps, step)
+        if SIDE_AFTER_ENC:
+            enc_done.record(torch.cuda.current_stream(P.data.device))
         ctx = torch.cuda.stream(side_stream)
     else:
         ctx = contextlib.nullcontext()

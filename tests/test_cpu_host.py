@@ -53,6 +53,20 @@ def test_argument_validation_without_gpu():
     assert lib.cc_wgrad_parts(16384, 4608, 2) == 8 * 64 * 18  # fp32: 256 x 256 tiles
     assert lib.cc_wgrad_parts(16384, 4608, 2) == 8 * 64 * 18  # fp32: 256 x 256
     assert lib.cc_loss_col_blocks(2304) == 5
+    # fused step tails (cc_grad_tail / cc_loss_tail): NULL and shape checks come before any launch
+    off = (ctypes.c_int64 * 5)(0, 1, 2, 3, 4)
+    assert lib.cc_grad_tail(null, 16, 256, fake, fake, fake, 128, 64, fake, fake, 1, fake, off, 4, 1.0, 1, fake, fake,
+                            null) == 1
+    assert lib.cc_grad_tail(fake, 16, 256, fake, fake, fake, 128, 64, fake, fake, 1, fake, off, 4, 1.0, 1, fake, null,
+                            null) == 1                                                           # no counter
+    assert lib.cc_grad_tail(fake, 0, 256, fake, fake, fake, 128, 64, fake, fake, 1, fake, off, 4, 1.0, 1, fake, fake,
+                            null) == 3                                                           # R_enc = 0
+    assert lib.cc_grad_tail(fake, 16, 256, fake, fake, fake, 128, 64, fake, fake, 1, fake, off, 9, 1.0, 1, fake, fake,
+                            null) == 3                                                           # nparams > 8
+    assert lib.cc_loss_tail(fake, 16, 256, fake, fake, fake, fake, fake, 8, fake, fake, fake, fake, null, null, 0, 64,
+                            2, 32, null, null) == 1                                              # no counter
+    assert lib.cc_loss_tail(fake, 16, 256, fake, fake, fake, fake, fake, 8, fake, fake, fake, fake, null, null, 0, 0,
+                            2, 32, fake, null) == 3                                              # empty batch
 
 
 def _cfg(dtype="bf16", h=256, d=32, device="cpu"):
