@@ -72,10 +72,17 @@ class ShardedStep:
             b.rows_ready(r0, r1, l1c)                # loss rows + g_recon + d_acts rows of the slice
         red = b.reduce_buffer()                      # [6]: 4 clip sums + l1, l0 (latent-local)
         scalars = b.loss_finalize(red)               # [l2, l1, l0, ev, ev_a, ev_b, ...]; red[4:6] = local l1, l0
-        b.backward(l1c, red, self.rank)              # red[0:4] = local squared sums (b_dec on rank 0 only)
-        dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
+        # l1 / l0 over all ranks first (8 bytes, async on the collective stream): the losses are final
+        # before the backward runs, so the host can read them (on_losses) and enqueue the next step
+        # while this step's backward / clip / Adam still run.  The collective stream is in order, so
+        # the compute stream's wait for the clip sums below also orders it after this one.
+        lw = dist.all_reduce(red[4:6], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         if on_losses is not None:
-            on_losses(scalars, red)
+            on_losses(scalars, red, lw)
+        b.backward(l1c, red, self.rank)              # red[0:4] = local squared sums (b_dec on rank 0 only)
+        dist.all_reduce(red[0:4], op=dist.ReduceOp.SUM, group=self.group)
+        if on_losses is None:
+            lw.wait()
         b.clip_and_adam_from_sums(red[0:4], lr, betas, eps, t, max_norm)
         return scalars, red
 
@@ -165,15 +172,21 @@ class ShardedTrainer:
             return self.cfg["l1_coeff"] * self.step_counter / (0.05 * self.total_steps)
         return self.cfg["l1_coeff"]
 
-    def _copy_losses(self, scalars, red):
-        # pinned landing buffers: the host waits for the losses only, not for clip / Adam
+    def _copy_losses(self, scalars, red, l1l0_work):
+        # pinned landing buffers, filled on a copy stream that waits for the forward (compute stream)
+        # and for the l1 / l0 all-reduce: the host waits for the losses only, and the compute stream
+        # never waits for the copy
         if self._host is None:
             self._host = torch.empty(8, dtype=torch.float32, pin_memory=True)
             self._host_red = torch.empty(6, dtype=torch.float32, pin_memory=True)
             self._copied = torch.cuda.Event()
-        self._host.copy_(scalars[:8], non_blocking=True)
-        self._host_red.copy_(red[:6], non_blocking=True)
-        self._copied.record()
+            self._copy_stream = torch.cuda.Stream(device=scalars.device)
+        self._copy_stream.wait_stream(torch.cuda.current_stream(scalars.device))
+        with torch.cuda.stream(self._copy_stream):
+            l1l0_work.wait()  # (the copy stream waits for the collective stream)
+            self._host.copy_(scalars[:8], non_blocking=True)
+            self._host_red.copy_(red[:6], non_blocking=True)
+            self._copied.record(self._copy_stream)
 
     def synchronize(self):
         """Order torch's current stream after the last step's side-stream (decoder-half) Adam."""
