@@ -103,6 +103,8 @@ def load(path=LIB_PATH):
     lib.cc_debug_set_pp_mask.argtypes = [ctypes.c_int]
     lib.cc_debug_set_tail_fence.restype = None
     lib.cc_debug_set_tail_fence.argtypes = [ctypes.c_int]
+    lib.cc_debug_set_dec_one_launch.restype = None
+    lib.cc_debug_set_dec_one_launch.argtypes = [ctypes.c_int]
     _lib = lib
     return lib
 

@@ -866,6 +866,13 @@ int64_t cc_decode_ws_floats(int64_t B, int64_t h, int64_t K, int dtype) {
 
 }  // extern "C"
 
+// G2's main tiles and split-K units as one launch (1) or two (0): cc_debug_set_dec_one_launch (A/B)
+#ifndef CC_DEC_ONE_LAUNCH
+#define CC_DEC_ONE_LAUNCH 1
+#endif
+static int g_dec_one_launch = CC_DEC_ONE_LAUNCH;
+extern "C" void cc_debug_set_dec_one_launch(int on) { g_dec_one_launch = on; }
+
 // BKC: W_dec given transposed, W_dec_t [K][h] (both operands contract over h contiguously)
 template <bool BKC>
 static int decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, float* ws, int64_t ws_floats,
@@ -896,8 +903,6 @@ static int decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, 
 #ifdef CC_PP_STAMPS
   if (g_split_stamps_only) a.dbg = nullptr;
 #endif
-  rc = launch_pp<true, BKC, EPI_DEC>(a, st);  // whole waves
-  if (rc) return rc;
   GemmArgs t = {};
   t.A = acts; t.lda = h; t.B = (const bf16_t*)W_dec + (int64_t)p.nbn_main * 256 * (BKC ? h : 1); t.ldb = ldb;
   t.M = (int)B; t.N = p.tail_cols; t.K = (int)h;
@@ -907,9 +912,21 @@ static int decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, 
 #ifdef CC_PP_STAMPS
   t.dbg = g_stamp_buf;
 #endif
-  hipLaunchKernelGGL((gemm_pp_splitk_kernel<true, BKC>), dim3(p.nsplit * t.nbm * t.nbn), dim3(NTHR), 0, st, t,
-                     p.steps_per, p.nk, split_stride);
-  CC_LAUNCH_CHECK();
+  if (g_dec_one_launch) {
+    // main tiles and split units in one grid (gemm_pp_main_splitk_kernel)
+    a.nbm = (a.M + BM - 1) / BM;
+    a.nbn = (a.N + 255) / 256;
+    hipLaunchKernelGGL((gemm_pp_main_splitk_kernel<true, BKC, EPI_DEC>),
+                       dim3(a.nbm * a.nbn + p.nsplit * t.nbm * t.nbn), dim3(NTHR), 0, st, a, t, p.steps_per, p.nk,
+                       split_stride);
+    CC_LAUNCH_CHECK();
+  } else {
+    rc = launch_pp<true, BKC, EPI_DEC>(a, st);  // whole waves
+    if (rc) return rc;
+    hipLaunchKernelGGL((gemm_pp_splitk_kernel<true, BKC>), dim3(p.nsplit * t.nbm * t.nbn), dim3(NTHR), 0, st, t,
+                       p.steps_per, p.nk, split_stride);
+    CC_LAUNCH_CHECK();
+  }
   const int64_t threads = (int64_t)t.nbm * t.nbn * 8 * 32 * 64;
   hipLaunchKernelGGL(reduce_splits_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, ws, p.nsplit,
                      split_stride, t.M, t.N, t.nbm, t.nbn, recon_f32 + (int64_t)p.nbn_main * 256, (int64_t)K);

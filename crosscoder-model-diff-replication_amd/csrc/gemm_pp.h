@@ -499,6 +499,31 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_kernel(const GemmArgs a0
 #endif
 }
 
+// G2 as ONE launch: blocks [0, nb0) are the whole-wave main tiles (a0, epilogue EPI), the rest the
+// split-K units of the leftover tiles (t, as gemm_pp_splitk_kernel).  The split units are dispatched
+// as the first main tiles finish, instead of after the slowest one (the two-launch form waits for
+// the whole main wave to drain at the kernel boundary).
+template <bool AKC, bool BKC, int EPI>
+__global__ __launch_bounds__(NTHR, 1) void gemm_pp_main_splitk_kernel(const GemmArgs a0, const GemmArgs t,
+                                                                    int steps_per, int nk_total,
+                                                                    int64_t split_stride) {
+  __shared__ __attribute__((aligned(16))) char smem[PP_LDS];
+  const int nb0 = a0.nbm * a0.nbn;
+  if ((int)blockIdx.x < nb0) {
+    pp_tile<AKC, BKC, EPI>(a0, smem, blockIdx.x);
+    return;
+  }
+  const int b = blockIdx.x - nb0;
+  const int s = b / (t.nbm * t.nbn);
+  const int tb = b - s * t.nbm * t.nbn;
+  GemmArgs a = t;
+  a.k_step0 = s * steps_per;
+  a.k_steps = nk_total - a.k_step0 < steps_per ? nk_total - a.k_step0 : steps_per;
+  a.out = (float*)t.out + s * split_stride;
+  a.stamp_base = 4 * s * t.nbm * t.nbn;
+  pp_tile<AKC, BKC, EPI_SPLIT>(a, smem, tb);
+}
+
 // Split-K pass (fp32 partial tiles, no epilogue work): block b runs contraction slice
 // s = b / ntiles (steps [s * steps_per, ...)) of tile b % ntiles and stores its fp32 partial tile
 // (accumulator-fragment order, EPI_SPLIT) at out + s * split_stride.  Used for the tiles left over after the whole 256-tile waves of a

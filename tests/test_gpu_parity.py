@@ -652,8 +652,18 @@ def test_decode_split_schedule(gpu, shape):
     ops.decode_fwd(acts, W, None, recon_f32=r_one)
     r_t = torch.empty(B, K, device=gpu)
     ops.decode_partial_t(acts, W.t().contiguous(), r_t, ws)  # W_dec^T operand: same schedule, same bits
+    # main tiles + split units as two launches instead of one: same bits
+    lib = ops.lib()
+    r_two, r_two_t = torch.empty(B, K, device=gpu), torch.empty(B, K, device=gpu)
+    lib.cc_debug_set_dec_one_launch(0)
+    try:
+        ops.decode_partial(acts, W, r_two, ws)
+        ops.decode_partial_t(acts, W.t().contiguous(), r_two_t, ws)
+    finally:
+        lib.cc_debug_set_dec_one_launch(1)
     torch.cuda.synchronize()
     assert torch.equal(r_t, r_split)
+    assert torch.equal(r_two, r_split) and torch.equal(r_two_t, r_split)
     if (B, h, K) == (4096, 16384, 4608):
         assert nws == 8 * 4096 * 512  # 32 leftover tiles of 288 -> 8-way split
     ref = acts.double().cpu() @ W.double().cpu()
