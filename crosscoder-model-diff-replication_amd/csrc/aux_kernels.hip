@@ -166,17 +166,27 @@ __global__ __launch_bounds__(256) void transpose_b16_kernel(const char* __restri
 }
 
 // norms[r][m] = sqrt(sum of part[r][m*bpm .. (m+1)*bpm) in ascending order), total, inverses:
-// the rest of dec_norms_kernel from the per-block partials.  One thread per row.
-__global__ __launch_bounds__(256) void norms_finalize_kernel(const float* __restrict__ part, int h, int n, int bpm,
-                                                             float* __restrict__ norms, float* __restrict__ total,
-                                                             float* __restrict__ inv_norms) {
-  const int row = blockIdx.x * 256 + threadIdx.x;
+// the rest of dec_norms_kernel from the per-block partials.  One thread per row, one wave per
+// block (h/64 blocks spread over the CUs); each lane issues NORM_LOADS independent loads before
+// adding them in order (the sum is latency-bound: one dependent load per add took 15 us at config 2).
+constexpr int NORM_LOADS = 12;
+__global__ __launch_bounds__(64) void norms_finalize_kernel(const float* __restrict__ part, int h, int n, int bpm,
+                                                            float* __restrict__ norms, float* __restrict__ total,
+                                                            float* __restrict__ inv_norms) {
+  const int row = blockIdx.x * 64 + threadIdx.x;
   if (row >= h) return;
   const float* p = part + (int64_t)row * n * bpm;
   float tot = 0.f;
   for (int m = 0; m < n; ++m) {
     float s = 0.f;
-    for (int b = 0; b < bpm; ++b) s += p[m * bpm + b];
+    for (int b0 = 0; b0 < bpm; b0 += NORM_LOADS) {
+      float v[NORM_LOADS];
+#pragma unroll
+      for (int u = 0; u < NORM_LOADS; ++u) v[u] = b0 + u < bpm ? p[m * bpm + b0 + u] : 0.f;
+#pragma unroll
+      for (int u = 0; u < NORM_LOADS; ++u)
+        if (b0 + u < bpm) s += v[u];
+    }
     const float nr = sqrtf(s);
     norms[(int64_t)row * n + m] = nr;
     if (inv_norms) inv_norms[(int64_t)row * n + m] = nr > 0.f ? 1.f / nr : 0.f;
@@ -232,7 +242,7 @@ int cc_dec_norms_finalize(const float* part, int64_t h, int64_t n, int64_t d, fl
                           float* inv_norms, void* stream) {
   if (!part || !norms || !total) return CC_ERR_NULL;
   if (h <= 0 || n <= 0 || d <= 0 || d % 64) return CC_ERR_SHAPE;
-  hipLaunchKernelGGL(norms_finalize_kernel, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, (hipStream_t)stream, part,
+  hipLaunchKernelGGL(norms_finalize_kernel, dim3((unsigned)((h + 63) / 64)), dim3(64), 0, (hipStream_t)stream, part,
                      (int)h, (int)n, (int)(d / 64), norms, total, inv_norms);
   CC_LAUNCH_CHECK();
   return CC_OK;
@@ -249,7 +259,7 @@ int cc_transpose_dec_norms(const void* W_dec, int64_t h, int64_t n, int64_t d, v
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(transpose_b16_kernel<true>, rf ? dim3(nr, nc) : dim3(nc, nr), dim3(256), 0, st,
                      (const char*)W_dec, (int)h, (int)K, K, (char*)W_dec_t, h, rf, part, (int)(K / 64));
-  hipLaunchKernelGGL(norms_finalize_kernel, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, st, part, (int)h, (int)n,
+  hipLaunchKernelGGL(norms_finalize_kernel, dim3((unsigned)((h + 63) / 64)), dim3(64), 0, st, part, (int)h, (int)n,
                      (int)(d / 64), norms, total, inv_norms);
   CC_LAUNCH_CHECK();
   return CC_OK;
