@@ -98,9 +98,19 @@ def _worker(rank, world, port, q):
         backend = CpuShardBackend(Ps)
         step = sharded.ShardedStep(backend)
         outs = []
+        seen = []
+
+        def on_losses(scalars, red, l1l0_work):
+            # called before the backward: after the l1 / l0 all-reduce the losses are already final
+            l1l0_work.wait()
+            seen.append(red[4:6].clone())
+
         for t in range(STEPS):
             l1c = 2.0 if t else 0.0
-            s, red = step.step(raws[t], factor, l1c, cfg["lr"], (0.9, 0.999), 1e-8, t + 1)
+            cb = on_losses if t % 2 else None
+            s, red = step.step(raws[t], factor, l1c, cfg["lr"], (0.9, 0.999), 1e-8, t + 1, on_losses=cb)
+            if cb is not None:
+                assert torch.equal(seen[-1], red[4:6])
             outs.append(torch.stack([s[0], red[4], red[5]]).clone())
         q.put((rank, [o.tolist() for o in outs], {k: v.detach().clone() for k, v in backend.P.items()}))
     finally:
