@@ -84,4 +84,11 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if os.environ.get("STEPAB_HIPRIO"):  # every launch on a high-priority stream (the side stream stays at 0)
+        torch.cuda.set_device(0)
+        hs = torch.cuda.Stream(priority=-int(os.environ["STEPAB_HIPRIO"]))
+        print("main stream priority", hs.priority, "range", torch.cuda.Stream.priority_range())
+        with torch.cuda.stream(hs):
+            main()
+    else:
+        main()
