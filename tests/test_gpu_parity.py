@@ -847,3 +847,21 @@ def test_fused_tails_match_separate_launches(gpu, enc_dtype, B, n, d, h, monkeyp
     assert out[0][0] == out[1][0]
     for a, b in zip(out[0][1:], out[1][1:]):
         assert torch.equal(a, b)
+
+
+def test_mapped_loss_scalars_match_copy(gpu):
+    """Trainer.mapped_losses (the loss tail writes the scalars straight into mapped host memory and the
+    host polls a sequence word) gives the same loss dicts and parameters as the copy + event path."""
+    B, n, d, h = 512, 2, 128, 1024
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+               num_tokens=B * 20, device=str(gpu))
+    out = []
+    for mapped in (True, False):
+        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=2), crosscoder=ca.CrossCoder(cfg))
+        tr.mapped_losses = mapped
+        losses = [tr.step() for _ in range(3)]
+        tr.synchronize()
+        torch.cuda.synchronize()
+        out.append((losses, tr.crosscoder.arena().data.clone()))
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1])
