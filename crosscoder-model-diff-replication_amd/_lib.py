@@ -60,6 +60,8 @@ SIGNATURES = {
     "cc_clip_finalize": (_i, [_p, ctypes.POINTER(_i64), _i, _f, _i, _p, _p]),
     "cc_grad_tail": (_i, [_p, _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _i, _p, ctypes.POINTER(_i64), _i, _f, _i, _p,
                           _p, _p]),
+    "cc_grad_tail_sums": (_i, [_p, _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _i, _p, ctypes.POINTER(_i64), _i, _i, _p,
+                               _p, _p]),
     "cc_loss_tail": (_i, [_p, _i64, _i64, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _i64,
                           _i64, _i64, _p, _p]),
     "cc_transposed_ok": (_i, [_i64, _i64, _i64, _i]),

@@ -1077,11 +1077,11 @@ int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const 
 
 void cc_debug_set_tail_fence(int all) { g_tail_fence_all = all; }
 
-int cc_grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,
-                 const float* loss_colpart, int64_t R_dec, int64_t K, void* g_b_dec, float* sq_b_dec, int dtype,
-                 const float* sq, const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
-                 uint32_t* counter, void* stream) {
-  if (!gpre_colpart || !g_b_enc || !sq_b_enc || !loss_colpart || !g_b_dec || !sq_b_dec || !sq || !off || !clip_out ||
+static int grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,
+                     const float* loss_colpart, int64_t R_dec, int64_t K, void* g_b_dec, float* sq_b_dec, int dtype,
+                     const float* sq, const int64_t* off, int nparams, float max_norm, int emulate_bf16,
+                     int sums_only, int zero_mask, float* out, uint32_t* counter, void* stream) {
+  if (!gpre_colpart || !g_b_enc || !sq_b_enc || !loss_colpart || !g_b_dec || !sq_b_dec || !sq || !off || !out ||
       !counter)
     return CC_ERR_NULL;
   if (R_enc <= 0 || R_dec <= 0 || h <= 0 || K <= 0) return CC_ERR_SHAPE;
@@ -1097,7 +1097,9 @@ int cc_grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_
   a.clip.nparams = nparams;
   a.clip.max_norm = max_norm;
   a.clip.emulate_bf16 = emulate_bf16;
-  a.clip.out = clip_out;
+  a.clip.out = out;
+  a.clip.sums_only = sums_only;
+  a.clip.zero_mask = zero_mask;
   a.counter = counter;
   a.fence_all = g_tail_fence_all;
   dim3 grid((unsigned)((a.red_blocks[0] + a.red_blocks[1] + 3) / 4));
@@ -1105,6 +1107,22 @@ int cc_grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_
   DISPATCH_DT(dtype, hipLaunchKernelGGL((tail_kernel<DT_>), grid, dim3(SCAL_THREADS), 0, st, a));
   CC_LAUNCH_CHECK();
   return CC_OK;
+}
+
+int cc_grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,
+                 const float* loss_colpart, int64_t R_dec, int64_t K, void* g_b_dec, float* sq_b_dec, int dtype,
+                 const float* sq, const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
+                 uint32_t* counter, void* stream) {
+  return grad_tail(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec, sq_b_dec, dtype, sq,
+                   off, nparams, max_norm, emulate_bf16, 0, 0, clip_out, counter, stream);
+}
+
+int cc_grad_tail_sums(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,
+                      const float* loss_colpart, int64_t R_dec, int64_t K, void* g_b_dec, float* sq_b_dec, int dtype,
+                      const float* sq, const int64_t* off, int nparams, int zero_mask, float* out, uint32_t* counter,
+                      void* stream) {
+  return grad_tail(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec, sq_b_dec, dtype, sq,
+                   off, nparams, 0.f, 0, 1, zero_mask, out, counter, stream);
 }
 
 int cc_loss_tail(const float* acts_colpart, int64_t R, int64_t h, float* colsum_acts, const float* tn,

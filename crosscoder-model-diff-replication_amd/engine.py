@@ -293,11 +293,12 @@ def dacts_rows(ws, P, l1_coeff, r0, r1, l1_grad_weight=1.0):
                           colsum_part=ws.gpre_colpart[c0:c1])
 
 
-def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None):
+def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None, sums_out=None, zero_mask=0):
     """Gradients of l2 + l1_coeff * l1 into the grads Arena G (+ squared-sum partials).
     dacts_done: G3 already ran per batch slice (dacts_rows).  clip (max_norm, single-GPU step): the
     bias-gradient sums and clip_grad_norm_'s coefficient in one launch (clip_and_adam then skips
-    its clip_finalize)."""
+    its clip_finalize).  sums_out (latent-sharded step): instead, the per-parameter squared sums in
+    the same launch (segment_sums semantics, zero_mask), for the all-reduce."""
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
     l1_scale = float(l1_coeff) * l1_grad_weight / B
     if not dacts_done:
@@ -309,6 +310,15 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
         else:
             ops.wgrad_both(ws.acts, ws.g_recon, P.W_dec_hk, ws.inv_norms, ws.colsum_acts, l1_scale, G.W_dec_hk,
                            ws.sq_slice(1), ws.g_pre, ws.x, G.W_enc_hk, ws.sq_slice(0), n, d)
+    if sums_out is not None:
+        if FUSED_TAILS:
+            ops.grad_tail_sums(ws.gpre_colpart, G.b_enc, ws.sq_slice(2), ws.loss_colpart, G.b_dec_flat, ws.sq_slice(3),
+                               ws.sq, ws.sq_off, sums_out, ws.tail_ctr[1:2], zero_mask=zero_mask)
+        else:
+            ops.reduce_rows(ws.gpre_colpart, ws.gpre_colpart.shape[0], h, out_t=G.b_enc, sq_part=ws.sq_slice(2))
+            ops.reduce_rows(ws.loss_colpart, ws.loss_colpart.shape[0], K, out_t=G.b_dec_flat, sq_part=ws.sq_slice(3))
+            ops.segment_sums(ws.sq, ws.sq_off, sums_out, zero_mask=zero_mask)
+        return
     if clip is not None and FUSED_TAILS:
         ops.grad_tail(ws.gpre_colpart, G.b_enc, ws.sq_slice(2), ws.loss_colpart, G.b_dec_flat, ws.sq_slice(3), ws.sq,
                       ws.sq_off, clip, ws.dtype == torch.bfloat16, ws.clip_out, ws.tail_ctr[1:2])

@@ -224,6 +224,16 @@ def grad_tail(gpre_colpart, g_b_enc, sq_b_enc, loss_colpart, g_b_dec, sq_b_dec, 
                              max_norm, int(emulate_bf16), _ptr(out), _ptr(counter), _stream(sq)))
 
 
+def grad_tail_sums(gpre_colpart, g_b_enc, sq_b_enc, loss_colpart, g_b_dec, sq_b_dec, sq, offsets, out, counter,
+                   zero_mask=0):
+    """The two bias-gradient reduce_rows (+ sq partials) + segment_sums as one launch (same bits)."""
+    arr = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
+    check(lib().cc_grad_tail_sums(_ptr(gpre_colpart), gpre_colpart.shape[0], gpre_colpart.shape[1], _ptr(g_b_enc),
+                                  _ptr(sq_b_enc), _ptr(loss_colpart), loss_colpart.shape[0], loss_colpart.shape[1],
+                                  _ptr(g_b_dec), _ptr(sq_b_dec), dtype_code(g_b_enc.dtype), _ptr(sq), arr,
+                                  len(offsets) - 1, int(zero_mask), _ptr(out), _ptr(counter), _stream(sq)))
+
+
 def segment_sums(sq, offsets, out, zero_mask=0):
     """out[p] = sum(sq[offsets[p]:offsets[p+1]]) (0 where bit p of zero_mask is set)."""
     arr = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])

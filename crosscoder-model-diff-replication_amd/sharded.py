@@ -121,10 +121,10 @@ class HipShardBackend:
 
     def backward(self, l1c, red, rank):
         ws = self.ws
-        engine.backward(ws, self.cc.arena(), self.G, l1c, dacts_done=True)
-        # per-parameter squared sums straight into the all-reduce buffer; the replicated b_dec's
-        # counts on rank 0 only
-        ops.segment_sums(ws.sq, ws.sq_off, red[0:4], zero_mask=0 if rank == 0 else 1 << 3)
+        # per-parameter squared sums straight into the all-reduce buffer (same launch as the bias
+        # gradients); the replicated b_dec's counts on rank 0 only
+        engine.backward(ws, self.cc.arena(), self.G, l1c, dacts_done=True, sums_out=red[0:4],
+                        zero_mask=0 if rank == 0 else 1 << 3)
 
     def reduce_buffer(self):
         return self.red

@@ -234,6 +234,12 @@ int cc_grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_
                  const float* loss_colpart, int64_t R_dec, int64_t K, void* g_b_dec, float* sq_b_dec, int dtype,
                  const float* sq, const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
                  uint32_t* counter, void* stream);
+/* cc_grad_tail whose finaliser is cc_segment_sums instead of the clip (the latent-sharded step:
+ * out[p] = the per-parameter squared sums, 0 where bit p of zero_mask is set, to be all-reduced). */
+int cc_grad_tail_sums(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,
+                      const float* loss_colpart, int64_t R_dec, int64_t K, void* g_b_dec, float* sq_b_dec, int dtype,
+                      const float* sq, const int64_t* off, int nparams, int zero_mask, float* out, uint32_t* counter,
+                      void* stream);
 
 /* Per-parameter sums of the squared-gradient partials, sq[off[p] .. off[p+1]) (nparams <= 8, off on
  * the HOST), for the latent-sharded step's all-reduce: out[p] = the sum (fp32), or 0 where bit p of

@@ -777,6 +777,40 @@ def test_segment_sums(gpu):
     assert all(math.isclose(out[i].item(), ref[i], rel_tol=1e-6) for i in range(3)) and out[3].item() == 0.0
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("zero_mask", [0, 1 << 3])
+def test_grad_tail_sums_match_separate_launches(gpu, dtype, zero_mask):
+    """cc_grad_tail_sums (bias-gradient column sums + squared-sum partials + per-parameter sums, one
+    launch: the latent-sharded step's backward tail) == 2 x reduce_rows + segment_sums, bit for bit."""
+    h, K, R1, R2, nw = 1000, 4608, 16, 128, 3000
+    g = torch.Generator().manual_seed(7)
+    gpc = torch.randn(R1, h, generator=g).to(gpu)
+    lpc = torch.randn(R2, K, generator=g).to(gpu)
+    nr1, nr2 = ops.reduce_parts(h), ops.reduce_parts(K)
+    off = [0, nw, 2 * nw, 2 * nw + nr1, 2 * nw + nr1 + nr2]
+    res = []
+    for fused in (True, False):
+        sq = torch.rand(off[-1], generator=torch.Generator().manual_seed(8)).to(gpu)
+        gb_enc, gb_dec = torch.empty(h, dtype=dtype, device=gpu), torch.empty(K, dtype=dtype, device=gpu)
+        out = torch.full((4,), float("nan"), device=gpu)
+        if fused:
+            ctr = torch.zeros(1, dtype=torch.int32, device=gpu)
+            for _ in range(2):  # the counter is left at zero: a second launch works the same
+                ops.grad_tail_sums(gpc, gb_enc, sq[off[2]:off[3]], lpc, gb_dec, sq[off[3]:off[4]], sq, off, out, ctr,
+                                   zero_mask=zero_mask)
+            torch.cuda.synchronize()
+            assert int(ctr.item()) == 0
+        else:
+            ops.reduce_rows(gpc, R1, h, out_t=gb_enc, sq_part=sq[off[2]:off[3]])
+            ops.reduce_rows(lpc, R2, K, out_t=gb_dec, sq_part=sq[off[3]:off[4]])
+            ops.segment_sums(sq, off, out, zero_mask=zero_mask)
+        torch.cuda.synchronize()
+        res.append((gb_enc, gb_dec, sq, out))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    assert (res[0][3][3].item() == 0.0) == bool(zero_mask)
+
+
 # ----------------------------------------------------------------------------- BASELINE configs 4 / 5 shapes
 @pytest.mark.parametrize("B,n,d,h", [(8192, 2, 3584, 8192),     # config 4 per-GPU shard (2x3584->65536 / 8)
                                      (4096, 4, 2304, 32768)])   # config 5: 4x2304->32768 on one GPU
