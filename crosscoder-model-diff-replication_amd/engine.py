@@ -210,7 +210,8 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     (loss=False: stops at the fp32 reconstruction, for loss_rows / loss_finalize by slices)."""
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
     ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart, out_t=ws.x_t)
-    ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
+    if not XMEAN_AFTER_G1:
+        ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
     # G1 reads only the encoder half: it may overlap the previous step's decoder-half Adam
     with _span("G1_encode"):
         if ws.tr:
@@ -219,6 +220,10 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
         else:
             ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, colsum_part=ws.acts_colpart,
                            l0_part=ws.l0_part)
+    if XMEAN_AFTER_G1:
+        # x.mean(0) is first read by the loss kernel: reduced here it runs while the stream would
+        # otherwise idle waiting for the side stream's decoder-half Adam (G1 starts 8 us earlier)
+        ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
     P.wait_pending()
     decoder_norms(ws, P)  # (+ W_dec^T), unless launched already after the last Adam
     with _span("G2_decode"):
@@ -331,6 +336,9 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
 # the forward's / backward's small reductions + finalisers as single launches (loss_tail, grad_tail;
 # bit-identical to the separate launches -- A/B switch for tools/ and tests)
 FUSED_TAILS = True
+
+# x.mean(0)'s reduction after G1 (True) or between prep and G1 (False) -- A/B switch for tools/
+XMEAN_AFTER_G1 = True
 
 # the side-stream decoder-half Adam starts after the encoder half (True) or beside it (False)
 SIDE_AFTER_ENC = True

@@ -28,9 +28,10 @@ def main():
     defaults = (tr.mapped_losses, tr.overlap_decoder_adam, engine.DEC_ADAM_BLOCKS)
 
     def setup(ws, mapped=defaults[0], fused=True, side=defaults[1], blocks=defaults[2], fused_adam="serial",
-              tails=True, fence_all=0, after_enc=True, dec_one=1):
+              tails=True, fence_all=0, after_enc=True, dec_one=1, xmean_after=True):
         def f():
             cc._ws = ws
+            engine.XMEAN_AFTER_G1 = xmean_after
             ca._lib.load().cc_debug_set_dec_one_launch(dec_one)
             engine.SIDE_AFTER_ENC = after_enc
             engine.FUSED_TAILS = tails
@@ -50,7 +51,7 @@ def main():
                 "separate tails": setup(ws_t, tails=False), "tails fence all": setup(ws_t, fence_all=1),
                 "mapped losses": setup(ws_t, mapped=True), "side Adam 128 blocks": setup(ws_t, blocks=128),
                 "side Adam 192 blocks": setup(ws_t, blocks=192), "side Adam beside enc": setup(ws_t, after_enc=False),
-                "G2 two launches": setup(ws_t, dec_one=0)}
+                "G2 two launches": setup(ws_t, dec_one=0), "x mean before G1": setup(ws_t, xmean_after=False)}
     only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--only=")]
     if only:
         variants = {k: v for k, v in variants.items() if k in only[0].split(",")}
