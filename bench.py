@@ -1,18 +1,21 @@
 """Benchmark: activations/sec of the full crosscoder training step (fwd + bwd + clip + Adam).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C] [--batch B] [--n-models n]
+                  [--d-model d] [--dict-size h] [--no-cpu-baseline]
 
-N = 1: BASELINE config 2 — CrossCoder 2x2304->16384, batch 4096, bf16 on one MI355X
-(synthetic normalised activations, reference init with seed 49), timed through
-Trainer.step() (the reference's step contract, incl. its per-step loss-dict host copy).
-N > 1 (torchrun, one rank per GPU): the dictionary is latent-sharded — every rank owns a
-16384-latent slice (so the whole job trains 2x2304 -> 16384*N, BASELINE config 3 at N = 8)
-on the same 4096-row batch, with an RCCL all-reduce of the fp32 partial reconstructions.
-Per-GPU work is fixed (weak scaling); `value` counts config-2-equivalent activations
-(batch x h_total / 16384) per second over the whole job.
+Workloads are BASELINE.json's configs (synthetic normalised activations, reference init seed 49, bf16):
+  config 2  CrossCoder 2x2304->16384, batch 4096          -- the default at N = 1 (the metric's config)
+  config 3  2x2304->131072 (2^17), batch 4096, latent-sharded over the N ranks -- the default at N > 1
+  config 4  2x3584->65536, batch 8192                       config 5  4x2304->32768, batch 4096
+(--batch / --n-models / --d-model / --dict-size override single fields).  N > 1 (torchrun, one rank per
+GPU): the FIXED dictionary of the config is split into N latent slices (strong scaling) with an RCCL
+all-reduce of the fp32 partial reconstructions; every rank processes the same batch.  `value` is the
+real number of activations (batch rows) trained per second by the whole job; `latent_acts_per_s`
+(= value x dict_size) is the work-normalised throughput that is comparable across configs and N.
 
-The JSON line also carries `roofline` (dominant kernel's achieved TFLOP/s from HIP events
-around every launch of it in the timed region, vs the bf16 dense MFMA peak) and
+The JSON line also carries `roofline` (dominant kernel's achieved TFLOP/s from HIP events around its
+launches inside the timed region, vs the bf16 dense MFMA peak), `hbm` (achieved GB/s of the
+streaming kernels: Adam halves, input prep, loss, W_dec^T pass, from an untimed attribution pass) and
 `cpu_baseline` (the oracle CPU step timed on this host, rank 0, N = 1 only).
 """
 import argparse
@@ -30,8 +33,10 @@ sys.path.insert(0, ROOT)
 import crosscoder_amd as ca  # noqa: E402
 from crosscoder_amd import engine  # noqa: E402
 
-B, N_MODELS, D_MODEL, H_LOCAL = 4096, 2, 2304, 16384
+CONFIGS = {2: (4096, 2, 2304, 16384), 3: (4096, 2, 2304, 131072), 4: (8192, 2, 3584, 65536),
+           5: (4096, 4, 2304, 32768)}  # (batch, n_models, d_model, dict_size)
 PEAK_BF16_TFLOPS = 256 * 2.4e9 * 4096 / 1e12  # 256 CU x 2.4 GHz x 4096 bf16 FLOP/clk/CU (dense)
+PEAK_HBM_GBS = 8000.0  # HBM3E spec (MI355X_MICROARCH.md; ~6300 measured for a float4 copy)
 
 
 class EventTimer:
@@ -73,7 +78,7 @@ SPAN_EVERY = 4  # timed steps per roofline-kernel sample (events around the laun
 
 # span name -> kernel-name prefix in the rocprofv3 traces
 SPAN_KERNEL = {"G1_encode": "gemm_pp_kernel<true, true, 1>", "G2_decode": "gemm_pp_kernel<true, false, 2>",
-               "G3_dacts": "gemm_pp_kernel<true, true, 3>", "G4G5_wgrad": "gemm_pp_dual_kernel<false, false, 4, 5>",
+               "G3_dacts": "gemm_pp_kernel<true, true, 3>", "G4G5_wgrad": "gemm_pp_dual_kernel<true, true, 4, 5>",
                "adam": "adam_bulk_kernel"}
 
 
@@ -94,40 +99,85 @@ def pmc_traffic(span):
     return None, None
 
 
-def make_cfg(h, steps_total):
+def make_cfg(B, n, d, h):
     return {
         "seed": 49, "batch_size": B, "buffer_mult": 128, "lr": 5e-5, "num_tokens": 400_000_000, "l1_coeff": 2,
         "beta1": 0.9, "beta2": 0.999, "dict_size": h, "seq_len": 1024, "enc_dtype": "bf16", "model_name": "synthetic",
         "device": f"cuda:{torch.cuda.current_device()}", "model_batch_size": 4, "log_every": 100,
-        "save_every": 30000, "dec_init_norm": 0.08, "d_in": D_MODEL,
+        "save_every": 30000, "dec_init_norm": 0.08, "d_in": d, "n_models": n,
     }
 
 
-def cpu_baseline(seconds_budget=20.0):
-    """Oracle (reference PyTorch fp32 step restated, CPU) on a bounded sample of config 1."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(B, n, d, h):
+    """Oracle (the reference's PyTorch fp32 step restated, CPU) on a bounded sample of the same workload:
+    `rows` batch rows of normalised synthetic activations (Buffer.next scaling, buffer.py:115-125) for the
+    config's crosscoder, median of 5 steps after 1 warm-up; the per-step cost is linear in the rows."""
     from oracle import cpu_reference as O
 
     # this process's CPU share: OMP_NUM_THREADS (16 per GPU on the box), else the affinity mask
     cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
     torch.set_num_threads(cores)
-    cfg = {"seed": 49, "dict_size": H_LOCAL, "d_in": D_MODEL, "enc_dtype": "fp32", "dec_init_norm": 0.08,
-           "batch_size": B, "num_tokens": 400_000_000, "lr": 5e-5, "beta1": 0.9, "beta2": 0.999, "l1_coeff": 2}
-    P = O.init_params(cfg)
-    tr = O.OracleTrainer(cfg, P)
+    # ~3 s per oracle step on the box's 16 threads at config 2 (4096 rows): keep every config near that
+    rows = max(256, min(B, int(B * (2 * 2304 * 16384) / (n * d * h)) // 256 * 256))
+    cfg = {"seed": 49, "dict_size": h, "d_in": d, "enc_dtype": "fp32", "dec_init_norm": 0.08,
+           "batch_size": rows, "num_tokens": 400_000_000, "lr": 5e-5, "beta1": 0.9, "beta2": 0.999, "l1_coeff": 2}
+    P = O.init_params(cfg, n_models=n)
+    tr = O.OracleTrainer(cfg, P, n_models=n)
     g = torch.Generator().manual_seed(0)
-    x = torch.randn(B, N_MODELS, D_MODEL, generator=g)
+    scales = torch.tensor([(1 / 0.2759, 1 / 0.2442, 1 / 0.31, 1 / 0.27)[i % 4] for i in range(n)])
+    buf = (torch.randn(rows, n, d, generator=g) * scales[None, :, None]).to(torch.bfloat16)
+    factor = torch.tensor([(d ** 0.5) / buf[:, i].float().norm(dim=-1).mean().item() for i in range(n)]).to(
+        torch.bfloat16)
+    x = O.buffer_next(buf, factor)  # normalised: ||x_n|| ~ sqrt(d)
     tr.step(x)  # warm-up
     times = []
     t_start = time.perf_counter()
-    while len(times) < 5 and (time.perf_counter() - t_start) < seconds_budget:
+    while len(times) < 5 and (time.perf_counter() - t_start) < 25.0:
         t0 = time.perf_counter()
         tr.step(x)
         times.append(time.perf_counter() - t0)
     times.sort()
     med = times[len(times) // 2]
-    return {"value": B / med, "unit": "activations/s", "cores": cores, "kind": "port",
-            "sample": f"oracle fp32 Trainer.step, config 1 (B={B}, 2x{D_MODEL}->{H_LOCAL}), "
-                      f"median of {len(times)} steps after 1 warm-up, {med:.2f} s/step"}
+    return {"value": round(rows / med, 1), "unit": "activations/s", "cores": cores, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"oracle fp32 Trainer.step on {rows} normalised rows of the {n}x{d}->{h} crosscoder "
+                      f"(bench batch {B}; cost is linear in rows), median of {len(times)} steps after 1 "
+                      f"warm-up, {med:.2f} s/step"}
+
+
+def hbm_rows(kern, B, n, d, h_local, es=2):
+    """Achieved HBM rate of the streaming kernels from the attribution pass (algorithmic bytes: every
+    operand read once, every output written once)."""
+    K = n * d
+    enc = h_local * K + h_local  # encoder half of the arena (W_enc + b_enc)
+    dec = h_local * K + K
+    per = 7 * es  # Adam: p, g, m, v read + p, m, v written
+    byts = {"adam": enc * per, "adam_dec": dec * per,
+            "prep": B * K * es + 2 * B * K * es,            # raw batch in; x and x^T out
+            "loss": B * K * 4 + B * K * es + 2 * B * K * es,  # recon fp32 + x in; g_recon and g_recon^T out
+            "dec_norms_T": 2 * h_local * K * es}             # W_dec in, W_dec^T out (+ norms)
+    out = {}
+    for k, b in byts.items():
+        if k in kern and kern[k] > 0:
+            gbs = b / (kern[k] * 1e-3) / 1e9
+            out[k] = {"ms": round(kern[k], 4), "bytes": b, "GB_s": round(gbs, 1),
+                      "frac": round(gbs / PEAK_HBM_GBS, 3)}
+    if "adam_dec" in out:
+        out["adam_dec"]["note"] = "side stream, concurrent with the next step's prep / G1"
+    if "dec_norms_T" in out:
+        out["dec_norms_T"]["note"] = "side stream, concurrent with G1"
+    return out
 
 
 def main():
@@ -135,6 +185,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, choices=sorted(CONFIGS), default=None,
+                    help="BASELINE.json config (default: 2 on one GPU, 3 when sharded over N > 1)")
+    ap.add_argument("--batch", type=int)
+    ap.add_argument("--n-models", type=int)
+    ap.add_argument("--d-model", type=int)
+    ap.add_argument("--dict-size", type=int, help="the WHOLE dictionary (split over the ranks when N > 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-sharded", action="store_true",
                     help="diagnostic: run the latent-sharded step even on one rank (1-rank RCCL group)")
@@ -149,17 +205,25 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), rank=rank, world_size=world)
-    h_total = H_LOCAL * world
-    cfg = make_cfg(h_total, args.warmup + args.steps)
+    config = args.config if args.config is not None else (2 if world == 1 else 3)
+    B, n, d, h_total = CONFIGS[config]
+    B = args.batch or B
+    n = args.n_models or n
+    d = args.d_model or d
+    h_total = args.dict_size or h_total
+    custom = (B, n, d, h_total) != CONFIGS[config]
+    h_local = h_total // world
+    K = n * d
+    cfg = make_cfg(B, n, d, h_total)
 
     if not sharded_path:
         cc = ca.CrossCoder(cfg)
-        buf = ca.SyntheticBuffer(cfg, rows=B * 8, seed=0)
+        buf = ca.SyntheticBuffer(cfg, rows=B * 8, n_models=n, seed=0)
         tr = ca.Trainer(cfg, buffer=buf, crosscoder=cc)
     else:
         from crosscoder_amd import sharded
 
-        buf = ca.SyntheticBuffer(cfg, rows=B * 8, seed=0)  # same seed on every rank: replicated batch
+        buf = ca.SyntheticBuffer(cfg, rows=B * 8, n_models=n, seed=0)  # same seed on every rank: replicated batch
         tr = sharded.ShardedTrainer(cfg, buffer=buf)
 
     timer = EventTimer()
@@ -180,6 +244,7 @@ def main():
     timer.only = dom  # the roofline kernel, measured live inside the timed region
     if sharded_path:
         dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         # the roofline launch is bracketed on every SPAN_EVERY-th timed step (each event record
@@ -196,26 +261,26 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    ms = elapsed / args.steps * 1e3
-    acts_equiv = B * (h_total / H_LOCAL)
-    value = acts_equiv / (elapsed / args.steps)
+    step_s = elapsed / args.steps
+    ms = step_s * 1e3
+    value = B / step_s  # activations (batch rows) trained per second by the whole job
     dom_ms = timer.averages_ms()[dom]
-    gemm_flop = 2.0 * B * N_MODELS * D_MODEL * H_LOCAL  # per GEMM (per rank)
+    gemm_flop = 2.0 * B * K * h_local  # per GEMM (per rank)
     # G4G5_wgrad is one launch computing both weight gradients (cc_wgrad_both)
     dom_flop = gemm_flop * (2 if dom == "G4G5_wgrad" else 1)
     achieved = dom_flop / (dom_ms * 1e-3) / 1e12
-    step_flop = 5 * gemm_flop
-    if engine.transposed_wgrad(B, N_MODELS * D_MODEL, H_LOCAL, torch.bfloat16):  # KC/KC form (cc_wgrad_both_t)
-        SPAN_KERNEL["G4G5_wgrad"] = "gemm_pp_dual_kernel<true, true, 4, 5>"
-    traffic, traffic_src = pmc_traffic(dom)
+    step_flop = 5 * 2.0 * B * K * h_total  # whole job
+    if not engine.transposed_wgrad(B, K, h_local, torch.bfloat16):  # batch-major MN/MN form (cc_wgrad_both)
+        SPAN_KERNEL["G4G5_wgrad"] = "gemm_pp_dual_kernel<false, false, 4, 5>"
+    traffic, traffic_src = pmc_traffic(dom) if (config, world, custom) == (2, 1, False) else (None, None)
     # algorithmic operand/output bytes of the dominant launch (each input read once, output written once)
     es = 2  # bf16
-    K_ = N_MODELS * D_MODEL
-    alg = {"G1_encode": (B * K_ + H_LOCAL * K_ + B * H_LOCAL) * es,
-           "G2_decode": (B * H_LOCAL + H_LOCAL * K_) * es + B * K_ * 4,
-           "G3_dacts": (B * K_ + H_LOCAL * K_ + 2 * B * H_LOCAL) * es,
-           "G4G5_wgrad": (2 * B * H_LOCAL + 2 * B * K_ + 3 * H_LOCAL * K_) * es}
+    alg = {"G1_encode": (B * K + h_local * K + 2 * B * h_local) * es,
+           "G2_decode": (B * h_local + h_local * K) * es + B * K * 4,
+           "G3_dacts": (B * K + h_local * K + 2 * B * h_local) * es,
+           "G4G5_wgrad": (2 * B * h_local + 2 * B * K + 3 * h_local * K) * es}
     dom_alg_bytes = alg.get(dom)
+    name = f"{n}x{d}->{h_total}"
     result = {
         "metric": "activations/sec per train step (fwd+bwd+Adam), 2x2304->16384; % bf16 MFMA peak",
         "value": round(value, 1),
@@ -225,26 +290,31 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (seeded N(0,1) activations scaled per model, reference init seed 49)",
-        "config": {"workload": f"crosscoder train step 2x{D_MODEL}->{h_total}, batch {B}, latent-sharded over "
-                               f"{world} GPU(s) ({H_LOCAL} latents per GPU)",
-                   "global_batch": B, "n_models": N_MODELS, "d_model": D_MODEL, "dict_size": h_total,
+        "data": "synthetic (seeded N(0,1) activations scaled per model, normalised as Buffer.next; reference "
+                "init seed 49)",
+        "config": {"workload": f"crosscoder train step {name}, batch {B}"
+                               + (f", latent-sharded over {world} GPUs ({h_local} latents per GPU)" if world > 1
+                                  else ""),
+                   "baseline_config": None if custom else config,
+                   "global_batch": B, "n_models": n, "d_model": d, "dict_size": h_total,
                    "parallelism": f"latent{world}"},
-        "step_mfma_frac": round(step_flop / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+        "latent_acts_per_s": round(value * h_total, 1),
+        "step_mfma_frac": round(step_flop / step_s / 1e12 / (PEAK_BF16_TFLOPS * world), 4),
         "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items())},
         "roofline": {"bound": "mfma", "kernel": dom, "kernel_ms": round(dom_ms, 4),
                      "kernel_samples": len(timer.rec.get(dom, [])), "achieved": round(achieved, 1),
                      "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                      "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
                      "algorithmic_bytes": dom_alg_bytes},
+        "hbm": hbm_rows(kern, B, n, d, h_local),
         "last_loss": {k: round(v, 6) for k, v in last.items()},
     }
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline()
+            result["cpu_baseline"] = cpu_baseline(B, n, d, h_total)
         print(json.dumps(result), flush=True)
     if sharded_path:
         dist.destroy_process_group()

@@ -8,8 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# CC_HIP_LIB: an experiment build (tools/build_variant.sh) for in-process A/B timing; default in-tree
-LIB_PATH = os.environ.get("CC_HIP_LIB") or os.path.join(_HERE, "libcrosscoder_hip.so")
+LIB_PATH = os.path.join(_HERE, "libcrosscoder_hip.so")
 DEFAULT_PP_MASK = 5  # CC_PP_MASK the library is built with (csrc/gemm.hip)
 
 CC_BF16 = 1
@@ -86,11 +85,13 @@ class HipLibraryMissing(RuntimeError):
     pass
 
 
-def load(path=LIB_PATH):
-    """Load (once) and type the library; raises HipLibraryMissing if it is not built."""
+def load(path=None):
+    """Load (once) and type the in-tree library; raises HipLibraryMissing if it is not built.  (A tool
+    may pass the path of an experiment build on the FIRST call; the product never does.)"""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or LIB_PATH
     if not os.path.exists(path):
         raise HipLibraryMissing(
             f"{path} not found: build it with `make -C {os.path.dirname(path)}/csrc` "

@@ -7,6 +7,7 @@ all of them in one launch; `W_enc` keeps the reference's h-major strides (d, 1, 
 """
 import json
 import pprint
+import weakref
 from pathlib import Path
 from typing import NamedTuple, Optional, Union
 
@@ -42,8 +43,26 @@ def reference_init(cfg, n_models=2):
     return W_dec
 
 
+def write_checkpoint(state_dict, cfg, save_dir=None, version=0):
+    """crosscoder.py:132-146's two-file format: {save_dir}/{version}.pt (state_dict) + {version}_cfg.json,
+    save_dir = ./checkpoints/version_N (next free N) when None.  Returns (save_dir, version + 1)."""
+    if save_dir is None:
+        SAVE_DIR.mkdir(parents=True, exist_ok=True)
+        versions = [int(f.name.split("_")[1]) for f in SAVE_DIR.iterdir() if "version" in str(f)]
+        save_dir = SAVE_DIR / f"version_{1 + max(versions) if versions else 0}"
+        save_dir.mkdir(parents=True)
+    torch.save(state_dict, save_dir / f"{version}.pt")
+    with open(save_dir / f"{version}_cfg.json", "w") as f:
+        json.dump(cfg, f)
+    print(f"Saved as version {version} in {save_dir}")
+    return save_dir, version + 1
+
+
 class CrossCoder(nn.Module):
-    def __init__(self, cfg, n_models: Optional[int] = None):
+    def __init__(self, cfg, n_models: Optional[int] = None, init_W_dec: Optional[torch.Tensor] = None):
+        """init_W_dec (framework extension): start from this decoder ([h, n, d], W_enc = its rearranged
+        copy, zero biases) instead of the seeded reference draw -- the latent-sharded trainer passes
+        its slice of the full dictionary's reference init."""
         super().__init__()
         self.cfg = cfg
         d_hidden = cfg["dict_size"]
@@ -53,7 +72,7 @@ class CrossCoder(nn.Module):
         if self.dtype not in (torch.float32, torch.bfloat16):
             raise TypeError("crosscoder_amd kernels support enc_dtype 'bf16' and 'fp32'")
         device = torch.device(cfg["device"])
-        W_dec = reference_init(cfg, self.n_models)
+        W_dec = reference_init(cfg, self.n_models) if init_W_dec is None else init_W_dec.to(self.dtype)
         self._arena = engine.Arena(d_hidden, self.n_models, d_in, self.dtype, device)
         with torch.no_grad():
             self._arena.W_dec().copy_(W_dec)
@@ -72,11 +91,36 @@ class CrossCoder(nn.Module):
         self.b_enc = nn.Parameter(v["b_enc"])
         self.b_dec = nn.Parameter(v["b_dec"])
 
+    # The Trainer runs the decoder half of Adam on a side stream (engine.adam); every public way to
+    # reach the parameters orders torch's current stream after it first (a stream wait, no host sync):
+    # attribute access to W_dec / b_dec, parameters() / named_parameters(), state_dict(), .to() and
+    # friends (_apply), the arena re-pack, and the optimizer's state.  The step itself reaches the
+    # params through the arena only, so it keeps the overlap.
+    _SIDE_UPDATED = ("W_dec", "b_dec")
+
+    def _sync_pending(self):
+        a = self.__dict__.get("_arena")
+        if a is not None:
+            a.wait_pending()
+
+    def __getattr__(self, name):
+        if name in CrossCoder._SIDE_UPDATED:
+            self._sync_pending()
+        return super().__getattr__(name)
+
+    def named_parameters(self, *args, **kwargs):
+        self._sync_pending()
+        return super().named_parameters(*args, **kwargs)
+
+    def _apply(self, fn, *args, **kwargs):
+        self._sync_pending()
+        return super()._apply(fn, *args, **kwargs)
+
     def _arena_ok(self):
         a = self._arena
         v = a.views()
         for name in ("W_enc", "W_dec", "b_enc", "b_dec"):
-            p = getattr(self, name)
+            p = self._parameters[name]
             if p.data_ptr() != v[name].data_ptr() or p.stride() != v[name].stride() or p.device != a.data.device:
                 return False
         return True
@@ -84,23 +128,30 @@ class CrossCoder(nn.Module):
     def arena(self):
         """The flat parameter arena; re-packs the params if something (e.g. .to()) replaced them."""
         if not self._arena_ok():
-            dev = self.W_dec.device
+            self._arena.wait_pending()  # the old arena's decoder half may still be written
+            prm = self._parameters
+            dev = prm["W_dec"].device
             new = engine.Arena(self.d_hidden, self.n_models, self.cfg["d_in"], self.dtype, dev)
             with torch.no_grad():
                 for name, dst in new.views().items():
-                    dst.copy_(getattr(self, name).data)
+                    dst.copy_(prm[name].data)
             self._arena = new
-            grads = {n: getattr(self, n).grad for n in ("W_enc", "W_dec", "b_enc", "b_dec")}
+            grads = {n: prm[n].grad for n in ("W_enc", "W_dec", "b_enc", "b_dec")}
             self._bind_params()
             for n, g in grads.items():
-                getattr(self, n).grad = g
+                self._parameters[n].grad = g
             self._ws = None
         return self._arena
 
-    def _workspace(self, B):
+    def _workspace(self, B, step=False):
+        """The cached step workspace for batch size B.  A workspace that a get_losses() graph still
+        needs for its backward (ws.busy) is never reused: the next call gets a fresh one, which is
+        cached in its place (so a second get_losses() before the first backward cannot overwrite
+        the first one's activations)."""
         a = self.arena()
         ws = self._ws
-        if ws is None or ws.B != B or ws.x.device != a.data.device:
+        if (ws is None or ws.B != B or ws.x.device != a.data.device
+                or (ws.busy is not None and ws.busy() is not None)):
             ws = engine.StepWorkspace(B, self.n_models, self.cfg["d_in"], self.d_hidden, self.dtype, a.data.device)
             self._ws = ws
         return ws
@@ -158,13 +209,8 @@ class CrossCoder(nn.Module):
     def save(self):
         if self.save_dir is None:
             self.create_save_dir()
-        weight_path = self.save_dir / f"{self.save_version}.pt"
-        cfg_path = self.save_dir / f"{self.save_version}_cfg.json"
-        torch.save(self.state_dict(), weight_path)
-        with open(cfg_path, "w") as f:
-            json.dump(self.cfg, f)
-        print(f"Saved as version {self.save_version} in {self.save_dir}")
-        self.save_version += 1
+        self.save_dir, self.save_version = write_checkpoint(self.state_dict(), self.cfg, self.save_dir,
+                                                            self.save_version)
 
     def _load_checked(self, state_dict):
         self.load_state_dict(state_dict)
@@ -203,6 +249,11 @@ class CrossCoder(nn.Module):
         return cls.load_from_path(base / "cfg.json", base / "cc_weights.pt", device)
 
 
+class _GraphToken:
+    """Held by one get_losses() autograd node while its backward may still run; the workspace it used
+    keeps a weak reference (engine.StepWorkspace.busy)."""
+
+
 class _LossFn(torch.autograd.Function):
     """get_losses as one autograd node over the fused kernels."""
 
@@ -217,6 +268,9 @@ class _LossFn(torch.autograd.Function):
                ws.ev_b.to(dt, copy=True))
         ctx.cc = cc
         ctx.ws = ws
+        if any(ctx.needs_input_grad[3:]):  # a graph whose backward will read ws
+            ctx.token = _GraphToken()
+            ws.busy = weakref.ref(ctx.token)  # freed with the graph, or cleared by backward
         ctx.mark_non_differentiable(out[2], out[3], out[4], out[5])
         return out
 
@@ -230,5 +284,6 @@ class _LossFn(torch.autograd.Function):
             engine.loss_from_recon(ws, a, grad_scale=2.0 * w2 / ws.B)
         G = engine.Arena(cc.d_hidden, cc.n_models, cc.cfg["d_in"], cc.dtype, a.data.device)
         engine.backward(ws, a, G, l1_coeff=w1)
+        ws.busy = None
         v = G.views()
         return None, None, None, v["W_enc"], v["W_dec"], v["b_enc"], v["b_dec"]

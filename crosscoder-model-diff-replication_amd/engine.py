@@ -28,7 +28,6 @@ Step (reference trainer.py:41-63 -> crosscoder.py:96-130 -> autograd -> clip -> 
   adam      fused over the whole arena                                     trainer.py:47
 """
 import contextlib
-import os
 
 import torch
 
@@ -99,14 +98,16 @@ class Arena:
 class StepWorkspace:
     """All activations / partial-sum slabs of one step, allocated once per (B, shape, dtype)."""
 
-    def __init__(self, B, n, d, h, dtype, device):
+    def __init__(self, B, n, d, h, dtype, device, transposed=None):
         f32 = torch.float32
         K = n * d
         self.B, self.n, self.d, self.h, self.K, self.dtype = B, n, d, h, K, dtype
         E = lambda *s, dt=f32: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
         # batch-contiguous copies for the weight gradients (G4/G5 then read row-contiguous KC tiles on
-        # both operands: ~20 % faster than the batch-major MN/MN form at config 2)
-        self.tr = transposed_wgrad(B, K, h, dtype)
+        # both operands: ~20 % faster than the batch-major MN/MN form at config 2).  transposed=False
+        # forces the batch-major form (same results; the parity test compares the two)
+        self.tr = transposed_wgrad(B, K, h, dtype) if transposed is None else bool(transposed) and \
+            transposed_wgrad(B, K, h, dtype)
         self.x = E(B, K, dt=dtype)
         self.x_t = E(K, B, dt=dtype) if self.tr else None
         self.x_colpart = E(ops.prep_part_rows(B), K)
@@ -154,18 +155,14 @@ class StepWorkspace:
         # arrival counters of the fused tail launches (loss tail, grad tail); each launch leaves 0
         self.tail_ctr = torch.zeros(2, dtype=torch.int32, device=device)
         self.norms_token = None
-        self.host = None  # _hip.MappedHostBuffer for the loss scalars (Trainer), or None
-        self.host_seq = 0
+        self.busy = None  # weakref to the token of an autograd graph whose backward still needs this workspace
 
     def sq_slice(self, i):
         return self.sq[self.sq_off[i]:self.sq_off[i + 1]]
 
 
 def transposed_wgrad(B, K, h, dtype):
-    """Whether the step keeps batch-contiguous operand copies for G4/G5 (bf16 ping-pong shapes;
-    CC_TRANSPOSED_WGRAD=0 forces the batch-major MN/MN form -- same results, for A/B timing)."""
-    if os.environ.get("CC_TRANSPOSED_WGRAD", "1") == "0":
-        return False
+    """Whether the step keeps batch-contiguous operand copies for G4/G5 (bf16 ping-pong shapes)."""
     return bool(ops.lib().cc_transposed_ok(B, K, h, ops.dtype_code(dtype)))
 
 
@@ -188,7 +185,8 @@ def norms_for_next(ws, P):
 
 def _decoder_derived(ws, P):
     if ws.norm_part is not None:  # W_dec^T and the norms from one pass over W_dec
-        ops.transpose_dec_norms(P.W_dec_hk, ws.n, ws.d, ws.W_dec_t, ws.norm_part, ws.norms, ws.tn, ws.inv_norms)
+        with _span("dec_norms_T"):
+            ops.transpose_dec_norms(P.W_dec_hk, ws.n, ws.d, ws.W_dec_t, ws.norm_part, ws.norms, ws.tn, ws.inv_norms)
         return
     if ws.tr:
         ops.transpose(P.W_dec_hk, out=ws.W_dec_t)
@@ -209,9 +207,8 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     fp32/bf16, factor [n] or None.  Leaves losses in ws.scalars / ws.ev*, g_recon ready
     (loss=False: stops at the fp32 reconstruction, for loss_rows / loss_finalize by slices)."""
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
-    ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart, out_t=ws.x_t)
-    if not XMEAN_AFTER_G1:
-        ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
+    with _span("prep"):
+        ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart, out_t=ws.x_t)
     # G1 reads only the encoder half: it may overlap the previous step's decoder-half Adam
     with _span("G1_encode"):
         if ws.tr:
@@ -220,10 +217,9 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
         else:
             ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, colsum_part=ws.acts_colpart,
                            l0_part=ws.l0_part)
-    if XMEAN_AFTER_G1:
-        # x.mean(0) is first read by the loss kernel: reduced here it runs while the stream would
-        # otherwise idle waiting for the side stream's decoder-half Adam (G1 starts 8 us earlier)
-        ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
+    # x.mean(0) is first read by the loss kernel: reduced here it runs while the stream would
+    # otherwise idle waiting for the side stream's decoder-half Adam (G1 starts 8 us earlier)
+    ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
     P.wait_pending()
     decoder_norms(ws, P)  # (+ W_dec^T), unless launched already after the last Adam
     with _span("G2_decode"):
@@ -231,13 +227,9 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
             ops.decode_partial_t(ws.acts, ws.W_dec_t, ws.recon, ws.dec_ws)
         else:
             ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
-    if FUSED_TAILS:
-        # the activation column sums + l1 partials ride in the loss finaliser's launch (loss_tail)
-        ws.acts_pending = True
-    else:
-        # sum_b acts (for dL1/dW_dec) and B * l1 = sum_h colsum_acts[h] * tn[h] (crosscoder.py:126)
-        ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts, dot_w=ws.tn,
-                        dot_part=ws.l1_part)
+    # sum_b acts (for dL1/dW_dec) and B * l1 = sum_h colsum_acts[h] * tn[h] (crosscoder.py:126) ride in
+    # the loss finaliser's launch (loss_tail)
+    ws.acts_pending = True
     if loss:
         loss_from_recon(ws, P, grad_scale)
 
@@ -245,31 +237,21 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
 def loss_rows(ws, P, r0, r1, grad_scale=None):
     """Loss row terms + g_recon for batch rows [r0, r1) (r0 % 32 == 0); slabs keep the batch layout."""
     gs = 2.0 / ws.B if grad_scale is None else grad_scale
-    ops.loss_fwd_bwd(ws.recon, P.b_dec_flat, ws.x, ws.x_mean, ws.g_recon, ws.row_part, ws.loss_colpart, gs, ws.B,
-                     ws.n, ws.d, row0=r0, rows=r1 - r0, g_recon_t=ws.g_recon_t)
+    with _span("loss"):
+        ops.loss_fwd_bwd(ws.recon, P.b_dec_flat, ws.x, ws.x_mean, ws.g_recon, ws.row_part, ws.loss_colpart, gs, ws.B,
+                         ws.n, ws.d, row0=r0, rows=r1 - r0, g_recon_t=ws.g_recon_t)
 
 
 def loss_finalize(ws, l1l0_out=None):
-    """Loss scalars / EV vectors; with ws.host (a mapped host buffer, set by the Trainer) the
-    scalars also land in host memory followed by the sequence word ws.host_seq.  After a forward
-    that deferred the activation column sums (FUSED_TAILS), one launch does both (loss_tail)."""
+    """Loss scalars / EV vectors.  After a forward (which deferred the activation column sums) one
+    launch does both (cc_loss_tail); a re-formed loss (same activations) only the finaliser."""
     if ws.acts_pending:
-        loss_tail(ws, l1l0_out)
+        ops.loss_tail(ws.acts_colpart, ws.h, ws.colsum_acts, ws.tn, ws.l1_part, ws.row_part, ws.l0_part, ws.n_wave,
+                      ws.ev, ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], l1l0_out=l1l0_out)
+        ws.acts_pending = False
         return
-    if ws.host is not None:
-        ws.host_seq = (ws.host_seq + 1) & 0xFFFFFFFF or 1
     ops.loss_finalize(ws.row_part, ws.l1_part, ws.n_l1, ws.l0_part, ws.n_wave, ws.ev, ws.ev_a, ws.ev_b, ws.scalars,
-                      ws.B, ws.n, ws.d, l1l0_out=l1l0_out, host=ws.host, seq=ws.host_seq)
-
-
-def loss_tail(ws, l1l0_out=None):
-    """= reduce_rows(acts column sums, dot_w=tn -> l1 partials) + loss_finalize, one launch."""
-    if ws.host is not None:
-        ws.host_seq = (ws.host_seq + 1) & 0xFFFFFFFF or 1
-    ops.loss_tail(ws.acts_colpart, ws.h, ws.colsum_acts, ws.tn, ws.l1_part, ws.row_part, ws.l0_part, ws.n_wave, ws.ev,
-                  ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], l1l0_out=l1l0_out, host=ws.host,
-                  seq=ws.host_seq)
-    ws.acts_pending = False
+                      ws.B, ws.n, ws.d, l1l0_out=l1l0_out)
 
 
 def loss_from_recon(ws, P, grad_scale=None):
@@ -316,15 +298,10 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
             ops.wgrad_both(ws.acts, ws.g_recon, P.W_dec_hk, ws.inv_norms, ws.colsum_acts, l1_scale, G.W_dec_hk,
                            ws.sq_slice(1), ws.g_pre, ws.x, G.W_enc_hk, ws.sq_slice(0), n, d)
     if sums_out is not None:
-        if FUSED_TAILS:
-            ops.grad_tail_sums(ws.gpre_colpart, G.b_enc, ws.sq_slice(2), ws.loss_colpart, G.b_dec_flat, ws.sq_slice(3),
-                               ws.sq, ws.sq_off, sums_out, ws.tail_ctr[1:2], zero_mask=zero_mask)
-        else:
-            ops.reduce_rows(ws.gpre_colpart, ws.gpre_colpart.shape[0], h, out_t=G.b_enc, sq_part=ws.sq_slice(2))
-            ops.reduce_rows(ws.loss_colpart, ws.loss_colpart.shape[0], K, out_t=G.b_dec_flat, sq_part=ws.sq_slice(3))
-            ops.segment_sums(ws.sq, ws.sq_off, sums_out, zero_mask=zero_mask)
+        ops.grad_tail_sums(ws.gpre_colpart, G.b_enc, ws.sq_slice(2), ws.loss_colpart, G.b_dec_flat, ws.sq_slice(3),
+                           ws.sq, ws.sq_off, sums_out, ws.tail_ctr[1:2], zero_mask=zero_mask)
         return
-    if clip is not None and FUSED_TAILS:
+    if clip is not None:
         ops.grad_tail(ws.gpre_colpart, G.b_enc, ws.sq_slice(2), ws.loss_colpart, G.b_dec_flat, ws.sq_slice(3), ws.sq,
                       ws.sq_off, clip, ws.dtype == torch.bfloat16, ws.clip_out, ws.tail_ctr[1:2])
         ws.clip_ready = True
@@ -333,24 +310,9 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
     ops.reduce_rows(ws.loss_colpart, ws.loss_colpart.shape[0], K, out_t=G.b_dec_flat, sq_part=ws.sq_slice(3))
 
 
-# the forward's / backward's small reductions + finalisers as single launches (loss_tail, grad_tail;
-# bit-identical to the separate launches -- A/B switch for tools/ and tests)
-FUSED_TAILS = True
-
-# x.mean(0)'s reduction after G1 (True) or between prep and G1 (False) -- A/B switch for tools/
-XMEAN_AFTER_G1 = True
-
-# the side-stream decoder-half Adam starts after the encoder half (True) or beside it (False)
-SIDE_AFTER_ENC = True
-
-# workgroups of the decoder-half Adam that runs beside the next step's G1 (0: uncapped one-pass)
+# workgroups of the decoder-half Adam that runs beside the next step's G1 (128 / 192 / 384 measured
+# slower)
 DEC_ADAM_BLOCKS = 256
-# decoder-half Adam in 64x64 tiles that also write W_dec^T and the norm partials (transposed mode,
-# d % 64 == 0), instead of the flat Adam + a separate W_dec^T / norms pass.  "serial": only when the
-# decoder half runs on torch's stream -- beside G1 the fused kernel's faster HBM stream slows G1 more
-# than it saves (tools/step_ab.py: 2.88 vs 2.79 ms/step side-stream; 2.81 serial).  True / False
-# force it on / off (A/B switch for tools/).
-FUSED_DEC_ADAM = "serial"
 
 
 def clip_and_adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, max_norm=1.0, side_stream=None):
@@ -363,51 +325,29 @@ def clip_and_adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, max_norm=1.0, sid
 
 
 def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None):
-    """Adam with the clip coefficient in ws.clip_out[0].  side_stream: the decoder half's Adam (+ the
-    next step's decoder norms / W_dec^T) runs there, so it overlaps the next step's encoder GEMM (G1
-    reads only the encoder half, which Adam updates on torch's stream); P.pending orders every later
-    decoder-half use (forward() waits before G2; CrossCoder's methods wait; Trainer.synchronize())."""
-    fused = ws.norm_part is not None and (FUSED_DEC_ADAM is True or (FUSED_DEC_ADAM == "serial" and side_stream is None))
-    if side_stream is None and not fused:
-        with _span("adam"):
-            ops.adam_step(P.data, G.data, M.data, V.data, ws.clip_out[0:1], lr, beta1, beta2, eps, step)
-        return
+    """Adam with the clip coefficient in ws.clip_out[0].  side_stream: the encoder half runs on torch's
+    stream, then the decoder half (+ the next step's decoder norms / W_dec^T) on the side stream, so it
+    overlaps the next step's prep / encoder GEMM (G1 reads only the encoder half); P.pending orders every
+    later decoder-half use (forward() waits before G2; CrossCoder's accessors, FusedAdam.state and
+    Trainer.synchronize() wait).  Without a side stream: one launch over the whole arena."""
     coef = ws.clip_out[0:1]
     if side_stream is None:
         with _span("adam"):
-            ops.adam_step(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), coef, lr, beta1, beta2, eps, step)
-    if side_stream is not None:
-        # the decoder half starts after the encoder half (both are HBM-bound: run together they only
-        # share the bandwidth), i.e. beside the next step's prep / G1 on the main stream
-        # (SIDE_AFTER_ENC False: it waits for the clip coefficient only -- A/B switch for tools/)
-        enc_done = torch.cuda.Event()
-        if not SIDE_AFTER_ENC:
-            enc_done.record(torch.cuda.current_stream(P.data.device))
-        with _span("adam"):
-            ops.adam_step(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), coef, lr, beta1, beta2, eps, step)
-        if SIDE_AFTER_ENC:
-            enc_done.record(torch.cuda.current_stream(P.data.device))
-        ctx = torch.cuda.stream(side_stream)
-    else:
-        ctx = contextlib.nullcontext()
-    with ctx:
-        if side_stream is not None:
-            side_stream.wait_event(enc_done)
+            ops.adam_step(P.data, G.data, M.data, V.data, coef, lr, beta1, beta2, eps, step)
+        return
+    dev = P.data.device
+    with _span("adam"):
+        ops.adam_step(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), coef, lr, beta1, beta2, eps, step)
+    # both halves are HBM-bound: the decoder half starts after the encoder half (run together they only
+    # share the bandwidth), i.e. beside the next step's prep / G1 on the main stream
+    enc_done = torch.cuda.Event()
+    enc_done.record(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side_stream):
+        side_stream.wait_event(enc_done)
         with _span("adam_dec"):
-            if fused:
-                # W_dec in tiles that also emit W_dec^T + the norm partials; then b_dec; then the norms
-                ops.adam_dec_transposed(P.W_dec_hk, G.W_dec_hk, M.W_dec_hk, V.W_dec_hk, coef, lr, beta1, beta2, eps,
-                                        step, ws.W_dec_t, ws.norm_part,
-                                        max_blocks=DEC_ADAM_BLOCKS if side_stream is not None else 0)
-                ops.adam_step(P.b_dec_flat, G.b_dec_flat, M.b_dec_flat, V.b_dec_flat, coef, lr, beta1, beta2, eps,
-                              step)
-                ops.dec_norms_finalize(ws.norm_part, ws.h, ws.n, ws.d, ws.norms, ws.tn, ws.inv_norms)
-                ws.norms_token = _norms_token(P)
-            else:
-                ops.adam_step(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), coef, lr, beta1, beta2, eps,
-                              step, max_blocks=DEC_ADAM_BLOCKS)
+            ops.adam_step(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), coef, lr, beta1, beta2, eps, step,
+                          max_blocks=DEC_ADAM_BLOCKS)
         norms_for_next(ws, P)
-        if side_stream is not None:
-            done = torch.cuda.Event()
-            done.record(side_stream)
-            P.pending = done
+        done = torch.cuda.Event()
+        done.record(side_stream)
+    P.pending = done

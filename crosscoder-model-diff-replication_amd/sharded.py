@@ -27,7 +27,8 @@ import torch
 import torch.distributed as dist
 
 from . import engine, ops
-from .crosscoder import CrossCoder
+from .crosscoder import CrossCoder, reference_init, write_checkpoint
+from .trainer import reference_loss, rounded
 
 
 def shard_range(h_total, world, rank):
@@ -136,21 +137,29 @@ class HipShardBackend:
         engine.adam(ws, self.cc.arena(), self.G, self.M, self.V, lr, betas[0], betas[1], eps, t, self.side)
 
 
+def shard_crosscoder(cfg, lo, hi, n_models=None):
+    """This rank's CrossCoder: latents [lo, hi) of exactly the crosscoder `CrossCoder(cfg)` builds for
+    the whole dictionary (reference crosscoder.py:31-62: the seeded CPU draws are made for all
+    cfg["dict_size"] latents, then sliced), so a sharded run trains the reference's model."""
+    n = int(n_models if n_models is not None else cfg.get("n_models", 2))
+    W_dec = reference_init(cfg, n)[lo:hi]
+    return CrossCoder(dict(cfg, dict_size=hi - lo), n_models=n, init_W_dec=W_dec)
+
+
 class ShardedTrainer:
     """Trainer.step contract over latent shards (the whole job is one crosscoder with
     cfg["dict_size"] latents; this rank trains its slice)."""
 
-    def __init__(self, cfg, buffer, group=None, crosscoder=None, recon_chunks=None):
+    def __init__(self, cfg, buffer, group=None, crosscoder=None, recon_chunks=None, logger=None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.cfg = cfg
+        self.logger = logger
         lo, hi = shard_range(cfg["dict_size"], self.world, self.rank)
         self.lo, self.hi = lo, hi
         if crosscoder is None:
-            # per-shard seeded init (the reference's construction applied to the slice)
-            local = dict(cfg, dict_size=hi - lo, seed=cfg["seed"] + self.rank)
-            crosscoder = CrossCoder(local)
+            crosscoder = shard_crosscoder(cfg, lo, hi)
         self.crosscoder = crosscoder
         self.buffer = buffer
         chunks = recon_chunks if recon_chunks is not None else cfg.get("recon_chunks", 4)
@@ -161,6 +170,7 @@ class ShardedTrainer:
         self.t = 0
         self.lr = cfg["lr"] * self.lr_lambda(0)
         self._host = None
+        self.save_dir, self.save_version = None, 0  # rank 0's checkpoint directory (save())
 
     def lr_lambda(self, step):
         if step < 0.8 * self.total_steps:
@@ -204,24 +214,59 @@ class ShardedTrainer:
         s[1], s[2] = self._host_red[4:6].tolist()  # l1, l0 over all ranks' latents
         # the reference's l1 / EV_A / EV_B are param-dtype tensors (crosscoder.py:115-126): same rounding as Trainer.step
         dt = self.crosscoder.dtype
-        rd = (lambda v: float(torch.tensor(v, dtype=dt))) if dt != torch.float32 else float
-        l1 = rd(s[1])
-        d = {"loss": s[0] + l1c * l1, "l2_loss": s[0], "l1_loss": l1, "l0_loss": s[2], "l1_coeff": l1c,
-             "lr": self.lr, "explained_variance": s[3], "explained_variance_A": rd(s[4]),
-             "explained_variance_B": rd(s[5])}
+        l1 = rounded(s[1], dt)
+        d = {"loss": reference_loss(s[0], l1, l1c, dt), "l2_loss": s[0], "l1_loss": l1, "l0_loss": s[2],
+             "l1_coeff": l1c, "lr": self.lr, "explained_variance": s[3], "explained_variance_A": rounded(s[4], dt),
+             "explained_variance_B": rounded(s[5], dt)}
         self.step_counter += 1
         return d
 
+    def log(self, loss_dict):
+        if self.rank != 0:
+            return
+        if self.logger is not None:
+            self.logger(loss_dict, self.step_counter)
+        print(loss_dict)
+
+    def save(self):
+        """Gather every rank's slice and write ONE reference-format checkpoint on rank 0
+        (crosscoder.py:132-146: checkpoints/version_N/{k}.pt + {k}_cfg.json, the full dictionary)."""
+        sd = self.gather_state_dict()
+        if self.rank == 0:
+            self.save_dir, self.save_version = write_checkpoint(
+                {k: v.cpu() for k, v in sd.items()}, self.cfg, self.save_dir, self.save_version)
+        dist.barrier(group=self.group)
+
+    def train(self):
+        """trainer.py:69-82 over the shards (logging and checkpoints on rank 0)."""
+        self.step_counter = 0
+        try:
+            for i in range(self.total_steps):
+                loss_dict = self.step()
+                if i % self.cfg["log_every"] == 0:
+                    self.log(loss_dict)
+                if (i + 1) % self.cfg["save_every"] == 0:
+                    self.save()
+        finally:
+            self.save()
+
     def gather_state_dict(self):
-        """Full reference-layout state_dict on every rank (all_gather of the latent slices)."""
-        a = self.crosscoder.arena()
-        a.wait_pending()
-        out = {}
-        for name, t in (("W_dec", a.W_dec_hk), ("W_enc", a.W_enc_hk), ("b_enc", a.b_enc)):
-            parts = [torch.empty_like(t) for _ in range(self.world)]
-            dist.all_gather(parts, t.contiguous(), group=self.group)
-            out[name] = torch.cat(parts, 0)
-        h, n, d = self.cfg["dict_size"], a.n, a.d
-        W_enc = out["W_enc"].view(h, n, d).permute(1, 2, 0)
-        return {"W_enc": W_enc, "W_dec": out["W_dec"].view(h, n, d), "b_enc": out["b_enc"],
-                "b_dec": a.b_dec().clone()}
+        return gather_state_dict(self.crosscoder, self.cfg["dict_size"], self.group)
+
+
+def gather_state_dict(cc, h_total, group=None):
+    """Full reference-layout state_dict of a latent-sharded crosscoder on every rank (all_gather of the
+    ranks' latent slices; W_enc with the reference's strides (d, 1, n*d), b_dec from this rank -- it
+    is replicated and identical on all ranks)."""
+    a = cc.arena()
+    a.wait_pending()
+    world = dist.get_world_size(group)
+    out = {}
+    for name, t in (("W_dec", a.W_dec_hk), ("W_enc", a.W_enc_hk), ("b_enc", a.b_enc)):
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t.contiguous(), group=group)
+        out[name] = torch.cat(parts, 0)
+    n, d = a.n, a.d
+    W_enc = out["W_enc"].view(h_total, n, d).permute(1, 2, 0)
+    return {"W_enc": W_enc, "W_dec": out["W_dec"].view(h_total, n, d), "b_enc": out["b_enc"],
+            "b_dec": a.b_dec().clone()}

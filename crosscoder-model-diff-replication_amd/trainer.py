@@ -9,9 +9,22 @@ reference's) lives in arenas mirroring the parameter arena, exposed through
 import torch
 import tqdm
 
-from . import _hip, engine
+from . import engine
 from .buffer import Buffer
 from .crosscoder import CrossCoder
+
+
+def reference_loss(l2, l1, l1c, dtype):
+    """The reference's logged "loss" (trainer.py:44,52): `l2_loss + l1_coeff * l1_loss` where l2 is an
+    fp32 0-dim tensor and l1 one in the parameter dtype, so the product is rounded to that dtype
+    first and the sum to fp32 (torch's type promotion), then `.item()`."""
+    t = torch.tensor(l2, dtype=torch.float32) + l1c * torch.tensor(l1, dtype=dtype)
+    return t.item()
+
+
+def rounded(v, dtype):
+    """float(v) rounded to the parameter dtype (the reference's param-dtype loss tensors, crosscoder.py:115-126)."""
+    return float(torch.tensor(v, dtype=dtype)) if dtype != torch.float32 else float(torch.tensor(v))
 
 
 class FusedAdam:
@@ -28,6 +41,7 @@ class FusedAdam:
 
     @property
     def state(self):
+        self.cc.arena().wait_pending()  # the decoder half may still be updating on the side stream
         m, v = self.exp_avg.views(), self.exp_avg_sq.views()
         st = {}
         for name in ("W_enc", "W_dec", "b_enc", "b_dec"):
@@ -74,7 +88,6 @@ class Trainer:
         self.logger = logger
         self._host = None  # pinned loss-scalar landing buffer (allocated on the first step)
         self._side = None  # stream of the decoder half's Adam (created on the first step)
-        self._map = None  # mapped host buffer the loss-finalize kernel writes (mapped_losses)
 
     def lr_lambda(self, step):
         if step < 0.8 * self.total_steps:
@@ -92,15 +105,7 @@ class Trainer:
         backward / clip / Adam launches."""
         cc = self.crosscoder
         raw, factor = self.buffer.next_raw()
-        ws = cc._workspace(raw.shape[0])
-        self._last_B = raw.shape[0]
-        if self.mapped_losses:
-            if self._map is None:
-                self._map = _hip.MappedHostBuffer(16)
-            ws.host = self._map
-        else:
-            ws.host = None
-        self._ws = ws
+        ws = cc._workspace(raw.shape[0], step=True)
         P = cc.arena()
         opt = self.optimizer
         engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None)
@@ -113,8 +118,6 @@ class Trainer:
         b1, b2 = g["betas"]
         engine.clip_and_adam(ws, P, opt.grads, opt.exp_avg, opt.exp_avg_sq, g["lr"], b1, b2, g["eps"], opt.t,
                              side_stream=self._side_stream())
-        # the next step's decoder norms, straight behind Adam (consumed by the next forward)
-        engine.norms_for_next(ws, P)
         self.scheduler.step()
         self._last_l1c = l1c
         return ws.scalars
@@ -129,51 +132,36 @@ class Trainer:
         self._host.copy_(scalars[:8], non_blocking=True)
         self._copied.record()
 
-    early_loss_copy = True  # False: copy the losses after the whole step (A/B switch for tools/)
-    # True: the loss kernel writes the scalars straight into mapped host memory and the host polls
-    # a sequence word (no copy kernel, no event on the compute stream).  Measured neutral at
-    # config 2 (tools/step_ab.py), so the copy + event stays the default.
-    mapped_losses = False
-    overlap_decoder_adam = True  # False: one Adam launch on torch's stream (A/B switch for tools/)
-
     def _side_stream(self):
-        if not self.overlap_decoder_adam:
-            return None
+        # the decoder half of Adam (+ the next step's decoder norms / W_dec^T) runs here, beside the
+        # next step's prep / encoder GEMM (engine.adam)
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.crosscoder.arena().data.device)
         return self._side
 
     def synchronize(self):
         """Order torch's current stream after every launch of the last step (the decoder half of
-        Adam may still run on the side stream; CrossCoder's own methods wait by themselves)."""
+        Adam may still run on the side stream; CrossCoder's accessors and optimizer.state wait by
+        themselves)."""
         self.crosscoder.arena().wait_pending()
 
     def step(self):
-        if self.mapped_losses:
-            self.step_async()
-            self._map.wait(8, self._ws.host_seq)
-            s = self._map.f32[:6].tolist()
-        else:
-            if self.early_loss_copy:
-                self.step_async(on_losses=self._copy_losses)
-            else:
-                self._copy_losses(self.step_async())
-            self._copied.synchronize()
-            s = self._host[:6].tolist()
+        self.step_async(on_losses=self._copy_losses)
+        self._copied.synchronize()
+        s = self._host[:6].tolist()
         l1c = self._last_l1c
         dt = self.crosscoder.dtype
-        rd = (lambda v: float(torch.tensor(v, dtype=dt))) if dt != torch.float32 else float
-        l2, l1, l0 = s[0], rd(s[1]), s[2]
+        l2, l1, l0 = s[0], rounded(s[1], dt), s[2]
         loss_dict = {
-            "loss": l2 + l1c * l1,
+            "loss": reference_loss(l2, l1, l1c, dt),
             "l2_loss": l2,
             "l1_loss": l1,
             "l0_loss": l0,
             "l1_coeff": l1c,
             "lr": self.scheduler.get_last_lr()[0],
             "explained_variance": s[3],
-            "explained_variance_A": rd(s[4]),
-            "explained_variance_B": rd(s[5]),
+            "explained_variance_A": rounded(s[4], dt),
+            "explained_variance_B": rounded(s[5], dt),
         }
         self.step_counter += 1
         return loss_dict

@@ -21,7 +21,6 @@ from tests._golden import load, step_fixtures
 pytestmark = pytest.mark.gpu
 
 STEP_FIXTURES = step_fixtures()
-FIXTURES_2 = [f for f in STEP_FIXTURES if "_n2_" in f]
 
 
 def rel(a, b):
@@ -264,30 +263,68 @@ class _Replay:
         return b, f
 
 
-@pytest.mark.parametrize("name", FIXTURES_2)
+def _bf16_ulp(t):
+    t = t.float().abs()
+    return torch.where(t > 0, 2.0 ** (torch.floor(torch.log2(t.clamp_min(1e-38))) - 7), torch.zeros_like(t))
+
+
+@pytest.mark.parametrize("name", [f for f in STEP_FIXTURES if f.startswith("step_")])
 def test_trainer_steps(gpu, name):
+    """Trainer.step over the reference's stored trajectories (tools/gen_golden.py: 2 or 10 reference
+    Trainer.step calls, warm-up and decay branches included; n_models 2 and 4): all 9 loss-dict keys
+    every step, and params, exp_avg and exp_avg_sq after every stored step.  Bounds (measured by
+    tools/trainer_parity_stats.py; a Trainer whose Adam never runs fails every one of them):
+      fp32  params within 0.01 lr elementwise (measured <= 0.001 lr); moments rel <= 1e-5 (~3e-7);
+            l2 / loss / l1 rel 1e-6, EVs 1e-6 abs, l0 exact
+      bf16  W_enc / W_dec bit-identical on >= 94 % of elements (measured >= 96.4 %; without Adam 27-31 %)
+            and within 2 bf16 ulps + 3 lr everywhere (measured <= 2.44 lr); biases bit-identical on >= 50 % (>= 58 %; without Adam
+            0 %) and within 0.25 lr; moments rel <= 0.05 (<= 0.023); l2 rel 1e-4, l1 one bf16 ulp,
+            l0 within 1e-3 h + 1/B, EV 2e-3, EV_A / EV_B 4e-3 abs, loss to the sum of those."""
     r = load(name)
     cfg = dict(r["cfg"], device=str(gpu))
     dt = O.DTYPES[cfg["enc_dtype"]]
-    cc = make_cc(cfg, r["init"], gpu, r["n_models"])
+    n = r["n_models"]
+    cc = make_cc(cfg, r["init"], gpu, n)
     tr = ca.Trainer(cfg, buffer=_Replay(r["buf"], r["factor"], gpu), crosscoder=cc)
     steps = len(r["x"])
-    tol = 2e-5 if dt == torch.float32 else 2e-2
+    lr = cfg["lr"]
+    B, h = cfg["batch_size"], cfg["dict_size"]
+    fp32 = dt == torch.float32
     for s in range(steps):
         d = tr.step()
         ref = r["steps"]["loss_dicts"][s]
-        assert d.keys() == ref.keys()
+        assert list(d) == list(ref)
         assert d["l1_coeff"] == ref["l1_coeff"] and d["lr"] == ref["lr"]
-        for k in ("l2_loss", "l1_loss", "explained_variance"):
-            assert math.isclose(d[k], ref[k], rel_tol=tol, abs_tol=tol), (s, k, d[k], ref[k])
-        assert abs(d["l0_loss"] - ref["l0_loss"]) <= (1e-6 if dt == torch.float32 else 2e-3 * cfg["dict_size"] + 1)
-    last = r["steps"]["after"][steps - 1]
-    lr = cfg["lr"]
-    for k in O.PARAM_ORDER:
-        p = getattr(cc, k).detach().cpu().float()
-        ref = last["params"][k].float()
-        ulp = ref.abs().max().item() * (2 ** -7 if dt == torch.bfloat16 else 2 ** -22)
-        assert (p - ref).abs().max().item() <= 2 * lr * steps + 2 * ulp, k
+        l1_tol = 1e-6 * abs(ref["l1_loss"]) + 1e-7 if fp32 else 2 ** -7 * abs(ref["l1_loss"])
+        checks = {"l2_loss": 1e-6 * abs(ref["l2_loss"]) if fp32 else 1e-4 * abs(ref["l2_loss"]),
+                  "l1_loss": l1_tol,
+                  "l0_loss": 0.0 if fp32 else 1e-3 * h + 1.0 / B,
+                  "explained_variance": 1e-6 if fp32 else 2e-3,
+                  "explained_variance_A": 1e-6 if fp32 else 4e-3,
+                  "explained_variance_B": 1e-6 if fp32 else 4e-3}
+        checks["loss"] = checks["l2_loss"] + d["l1_coeff"] * l1_tol * (1 if fp32 else 2) + 1e-6 * abs(ref["loss"])
+        for k, tol in checks.items():
+            assert abs(d[k] - ref[k]) <= tol, (s, k, d[k], ref[k], tol)
+        if s not in r["steps"]["after"]:
+            continue
+        want = r["steps"]["after"][s]
+        st = tr.optimizer.state  # (waits for the side-stream decoder half)
+        for k in O.PARAM_ORDER:
+            p = getattr(cc, k).detach().cpu()
+            pr = want["params"][k]
+            diff = (p.float() - pr.float()).abs()
+            if fp32:
+                assert diff.max().item() <= 0.01 * lr, (s, k, diff.max().item() / lr)
+            else:
+                exact = (diff == 0).float().mean().item()
+                assert exact >= (0.94 if k.startswith("W") else 0.50), (s, k, exact)
+                if k.startswith("W"):  # (near-zero params: the update's own rounding, ~lr)
+                    assert (diff <= 2 * _bf16_ulp(pr) + 3 * lr).all(), (s, k, (diff / lr).max().item())
+                else:
+                    assert diff.max().item() <= 0.25 * lr, (s, k, diff.max().item() / lr)
+            for mom in ("exp_avg", "exp_avg_sq"):
+                e = rel(st[getattr(cc, k)][mom].cpu(), want[mom][k])
+                assert e <= (1e-5 if fp32 else 0.05), (s, k, mom, e)
 
 
 # ----------------------------------------------------------------------------- adam / clip
@@ -441,7 +478,7 @@ def test_sliced_loss_and_dacts_match_whole_batch(gpu, B):
 
 
 @pytest.mark.parametrize("B", [1024, 1000])
-def test_transposed_wgrad_step_matches_batch_major(gpu, B, monkeypatch):
+def test_transposed_wgrad_step_matches_batch_major(gpu, B):
     """The step with batch-contiguous copies (x^T, acts^T, g_recon^T, g_pre^T; G4/G5 KC/KC) gives the
     same gradients, partial sums and losses bit for bit as the batch-major MN/MN form."""
     n, d, h = 2, 256, 1024
@@ -453,10 +490,9 @@ def test_transposed_wgrad_step_matches_batch_major(gpu, B, monkeypatch):
     factor = torch.tensor([0.7, 1.3]).to(torch.bfloat16).to(gpu)
     a = cc.arena()
     outs = []
-    for tr in ("1", "0"):
-        monkeypatch.setenv("CC_TRANSPOSED_WGRAD", tr)
-        ws = engine.StepWorkspace(B, n, d, h, torch.bfloat16, gpu)
-        assert ws.tr == (tr == "1")
+    for tr in (True, False):
+        ws = engine.StepWorkspace(B, n, d, h, torch.bfloat16, gpu, transposed=tr)
+        assert ws.tr == tr
         G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
         engine.forward(ws, a, raw, factor)
         engine.backward(ws, a, G, 2.0)
@@ -564,32 +600,34 @@ def test_transposed_epilogue_outputs(gpu, B, K, h):
 
 
 @pytest.mark.parametrize("h", [2048, 200])
-def test_fused_decoder_adam_matches_flat(gpu, h, monkeypatch):
-    """The side-stream decoder Adam in 64x64 tiles that also writes W_dec^T and the norm partials
-    (cc_adam_dec_transposed) takes bit-identical Trainer steps to the flat Adam + separate
-    W_dec^T / norms pass, and its W_dec^T / norms are those of the updated W_dec."""
-    B, n, d = 1024, 2, 256
-    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
-               num_tokens=B * 20, device=str(gpu))
-    out = []
-    for fused in (True, False):
-        monkeypatch.setattr(engine, "FUSED_DEC_ADAM", fused)  # (beside G1 when True)
-        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=1), crosscoder=ca.CrossCoder(cfg))
-        losses = [tr.step() for _ in range(3)]
-        tr.synchronize()
-        torch.cuda.synchronize()
-        ws, P = tr.crosscoder._ws, tr.crosscoder.arena()
-        assert ws.norm_part is not None
-        assert torch.equal(ws.W_dec_t, P.W_dec_hk.t())
-        nm = torch.empty(h, n, device=gpu)
-        ops.dec_norms(P.W_dec_hk, h, n, d, norms=nm, total=torch.empty(h, device=gpu))
-        torch.cuda.synchronize()
-        assert torch.equal(ws.norms, nm)
-        opt = tr.optimizer
-        out.append((losses, P.data.clone(), opt.exp_avg.data.clone(), opt.exp_avg_sq.data.clone()))
-    assert out[0][0] == out[1][0]
-    for a, b in zip(out[0][1:], out[1][1:]):
-        assert torch.equal(a, b)
+@pytest.mark.parametrize("max_blocks", [0, 256])
+def test_tiled_decoder_adam_matches_flat(gpu, h, max_blocks):
+    """cc_adam_dec_transposed (decoder-half Adam in 64x64 tiles that also writes W_dec^T and the decoder
+    norm partials) == the flat cc_adam_step over the same half, bit for bit; its W_dec^T is the exact
+    transpose of the updated W_dec and cc_dec_norms_finalize gives cc_dec_norms' bits."""
+    n, d = 2, 256
+    K = n * d
+    g = torch.Generator().manual_seed(h + max_blocks)
+    bf = torch.bfloat16
+    mk = lambda sc: (torch.randn(h, K, generator=g) * sc).to(bf).to(gpu)  # noqa: E731
+    p0, gr, m0, v0 = mk(0.05), mk(1e-3), mk(1e-4), (torch.rand(h, K, generator=g) * 1e-6).to(bf).to(gpu)
+    coef = torch.tensor([0.7], device=gpu)
+    args = (coef, 5e-5, 0.9, 0.999, 1e-8, 3)
+    pf, mf, vf = p0.clone(), m0.clone(), v0.clone()
+    ops.adam_step(pf, gr.clone(), mf, vf, *args)
+    pt, mt, vt = p0.clone(), m0.clone(), v0.clone()
+    Wt = torch.empty(K, h, dtype=bf, device=gpu)
+    part = torch.empty(ops.dec_norms_part_floats(h, n, d), device=gpu)
+    ops.adam_dec_transposed(pt, gr.clone(), mt, vt, *args, Wt, part, max_blocks=max_blocks)
+    E = lambda *s_: torch.empty(*s_, device=gpu)  # noqa: E731
+    nm1, tn1, inv1 = E(h, n), E(h), E(h, n)
+    ops.dec_norms_finalize(part, h, n, d, nm1, tn1, inv1)
+    nm2, tn2, inv2 = E(h, n), E(h), E(h, n)
+    ops.dec_norms(pf, h, n, d, norms=nm2, total=tn2, inv_norms=inv2)
+    torch.cuda.synchronize()
+    assert torch.equal(pt, pf) and torch.equal(mt, mf) and torch.equal(vt, vf)
+    assert torch.equal(Wt, pf.t())
+    assert torch.equal(nm1, nm2) and torch.equal(tn1, tn2) and torch.equal(inv1, inv2)
 
 
 def test_sharded_trainer_world1_matches_trainer(gpu):
@@ -860,42 +898,91 @@ def test_baseline_config_shapes_spot_check(gpu, B, n, d, h):
 
 @pytest.mark.parametrize("enc_dtype,B,n,d,h", [("bf16", 1024, 2, 256, 2048), ("fp32", 96, 2, 40, 200),
                                                ("bf16", 512, 4, 64, 384), ("fp32", 256, 2, 64, 1000)])
-def test_fused_tails_match_separate_launches(gpu, enc_dtype, B, n, d, h, monkeypatch):
+def test_fused_tails_match_separate_launches(gpu, enc_dtype, B, n, d, h):
     """The one-launch loss tail (acts column sums + l1 partials + EV + loss scalars, cc_loss_tail) and
-    grad tail (bias-gradient sums + clip coefficient, cc_grad_tail) take bit-identical Trainer steps
-    to the separate reduce_rows / loss_finalize / clip_finalize launches, and leave their arrival
-    counters at zero."""
+    grad tail (bias-gradient sums + clip coefficient, cc_grad_tail) the step runs equal the separate
+    reduce_rows / loss_finalize / clip_finalize launches bit for bit, and leave their arrival counters
+    at zero; the mapped-host form of the loss finaliser delivers the same scalars + sequence word."""
+    from crosscoder_amd import _hip
+
     cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype=enc_dtype,
-               num_tokens=B * 20, device=str(gpu))
-    out = []
-    for fused in (True, False):
-        monkeypatch.setattr(engine, "FUSED_TAILS", fused)
-        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=1), crosscoder=ca.CrossCoder(cfg))
-        losses = [tr.step() for _ in range(3)]
-        tr.synchronize()
-        torch.cuda.synchronize()
-        ws, P, opt = tr.crosscoder._ws, tr.crosscoder.arena(), tr.optimizer
-        assert not bool(ws.tail_ctr.any())
-        out.append((losses, P.data.clone(), opt.exp_avg.data.clone(), opt.exp_avg_sq.data.clone(), opt.grads.data.clone(),
-                    ws.clip_out[:6].clone(), ws.ev.clone(), ws.ev_a.clone(), ws.colsum_acts.clone(), ws.l1_part.clone()))
-    assert out[0][0] == out[1][0]
-    for a, b in zip(out[0][1:], out[1][1:]):
-        assert torch.equal(a, b)
+               device=str(gpu))
+    cc = ca.CrossCoder(cfg, n_models=n)
+    g = torch.Generator().manual_seed(B + h)
+    raw = (torch.randn(B, n, d, generator=g) * 3).to(gpu)
+    factor = torch.tensor([0.7, 1.3, 0.9, 1.1][:n]).to(cc.dtype).to(gpu)
+    ws = cc._workspace(B)
+    a = cc.arena()
+    G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+    engine.forward(ws, a, raw, factor)          # loss tail
+    engine.backward(ws, a, G, 2.0, clip=1.0)    # grad tail
+    torch.cuda.synchronize()
+    assert not bool(ws.tail_ctr.any())
+    f32 = lambda t: torch.empty_like(t)  # noqa: E731
+    # loss side, separately
+    colsum, l1p = f32(ws.colsum_acts), f32(ws.l1_part)
+    ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=colsum, dot_w=ws.tn, dot_part=l1p)
+    ev, ev_a, ev_b, sc = f32(ws.ev), f32(ws.ev_a), f32(ws.ev_b), f32(ws.scalars)
+    ops.loss_finalize(ws.row_part, l1p, ws.n_l1, ws.l0_part, ws.n_wave, ev, ev_a, ev_b, sc, B, n, d)
+    host = _hip.MappedHostBuffer(16)
+    sc2 = f32(ws.scalars)
+    ops.loss_finalize(ws.row_part, l1p, ws.n_l1, ws.l0_part, ws.n_wave, f32(ev), f32(ev), f32(ev), sc2, B, n, d,
+                      host=host, seq=7)
+    # grad side, separately
+    sq = ws.sq.clone()
+    gbe, gbd = torch.empty_like(G.b_enc), torch.empty_like(G.b_dec_flat)
+    o = ws.sq_off
+    ops.reduce_rows(ws.gpre_colpart, ws.gpre_colpart.shape[0], h, out_t=gbe, sq_part=sq[o[2]:o[3]])
+    ops.reduce_rows(ws.loss_colpart, ws.loss_colpart.shape[0], n * d, out_t=gbd, sq_part=sq[o[3]:o[4]])
+    clip = torch.empty(8, device=gpu)
+    ops.clip_finalize(sq, o, 1.0, cc.dtype == torch.bfloat16, clip)
+    torch.cuda.synchronize()
+    host.wait(8, 7)
+    for x, y in ((colsum, ws.colsum_acts), (l1p, ws.l1_part), (ev, ws.ev), (ev_a, ws.ev_a), (ev_b, ws.ev_b),
+                 (sc[:6], ws.scalars[:6]), (sq, ws.sq), (gbe, G.b_enc), (gbd, G.b_dec_flat),
+                 (clip[:6], ws.clip_out[:6])):
+        assert torch.equal(x, y)
+    assert torch.equal(torch.from_numpy(host.f32[:6].copy()), sc2[:6].cpu())
+    assert torch.equal(sc2[:6], sc[:6])
 
 
-def test_mapped_loss_scalars_match_copy(gpu):
-    """Trainer.mapped_losses (the loss tail writes the scalars straight into mapped host memory and the
-    host polls a sequence word) gives the same loss dicts and parameters as the copy + event path."""
+def test_two_get_losses_before_one_backward(gpu):
+    """Two get_losses() graphs alive at once (gradient accumulation, `get_losses(a).l2 +
+    get_losses(b).l2`): the second forward must not overwrite the activations the first graph's
+    backward needs.  Gradients = the sum of the oracle's gradients of both batches (fp32)."""
+    r = load("step_b64_n2_d32_h256_fp32")
+    cfg = dict(r["cfg"], device=str(gpu))
+    cc = make_cc(cfg, r["init"], gpu, 2)
+    g = torch.Generator().manual_seed(11)
+    xa, xb = (torch.randn(64, 2, 32, generator=g) * 2 for _ in range(2))
+    la, lb = cc.get_losses(xa.to(gpu)), cc.get_losses(xb.to(gpu))
+    (la.l2_loss + 2.0 * la.l1_loss + lb.l2_loss).backward()
+    P = {k: v.detach().clone().requires_grad_(True) for k, v in r["init"].items()}
+    oa, ob = O.get_losses(xa, P, torch.float32), O.get_losses(xb, P, torch.float32)
+    (oa["l2_loss"] + 2.0 * oa["l1_loss"] + ob["l2_loss"]).backward()
+    assert math.isclose(la.l2_loss.item(), oa["l2_loss"].item(), rel_tol=1e-5)
+    assert math.isclose(lb.l2_loss.item(), ob["l2_loss"].item(), rel_tol=1e-5)
+    for k in O.PARAM_ORDER:
+        assert rel(getattr(cc, k).grad.cpu(), P[k].grad) < 2e-5, k
+
+
+def test_param_access_orders_after_side_stream_adam(gpu):
+    """After Trainer.step() the decoder half of Adam may still run on the side stream: reading the
+    params through any public path (attribute, parameters(), state_dict(), optimizer.state) first
+    orders torch's current stream after it (the arena's pending event is consumed)."""
     B, n, d, h = 512, 2, 128, 1024
     cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
                num_tokens=B * 20, device=str(gpu))
-    out = []
-    for mapped in (True, False):
-        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=2), crosscoder=ca.CrossCoder(cfg))
-        tr.mapped_losses = mapped
-        losses = [tr.step() for _ in range(3)]
-        tr.synchronize()
-        torch.cuda.synchronize()
-        out.append((losses, tr.crosscoder.arena().data.clone()))
-    assert out[0][0] == out[1][0]
-    assert torch.equal(out[0][1], out[1][1])
+    tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=2), crosscoder=ca.CrossCoder(cfg))
+    cc = tr.crosscoder
+    for access in (lambda: cc.W_dec, lambda: list(cc.parameters()), lambda: cc.state_dict(),
+                   lambda: tr.optimizer.state, lambda: cc.b_dec):
+        tr.step()
+        assert cc._arena.pending is not None  # the side-stream Adam of this step
+        access()
+        assert cc._arena.pending is None
+    # and what such a read sees is the finished update: the same bits after a full device sync
+    tr.step()
+    w = cc.W_dec.detach().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(w, cc.W_dec.detach())

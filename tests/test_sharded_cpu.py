@@ -2,6 +2,7 @@
 the same collectives and combine rules the GPU path uses) driven by a torch-CPU backend must
 reproduce the unsharded oracle step."""
 import os
+import pathlib
 import random
 
 import pytest
@@ -169,3 +170,61 @@ def test_shard_range_and_clip_combine():
     s = torch.tensor([1.0, 2.0, 3.0, 4.0])
     assert sharded.clip_sums_for_allreduce(s, 0).tolist() == [1, 2, 3, 4]
     assert sharded.clip_sums_for_allreduce(s, 1).tolist() == [1, 2, 3, 0]
+
+
+def _init_worker(rank, world, port, q, enc_dtype, tmpdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import crosscoder_amd as ca
+        from crosscoder_amd import crosscoder as ccmod
+
+        cfg = {"seed": 49, "dict_size": 96, "d_in": 24, "enc_dtype": enc_dtype, "dec_init_norm": 0.08,
+               "device": "cpu"}
+        lo, hi = sharded.shard_range(cfg["dict_size"], world, rank)
+        cc = sharded.shard_crosscoder(cfg, lo, hi)
+        full = ca.CrossCoder(cfg)
+        # this rank's slice IS the reference init of the whole dictionary, sliced
+        assert torch.equal(cc.W_dec.detach(), full.W_dec.detach()[lo:hi])
+        assert torch.equal(cc.W_enc.detach(), full.W_enc.detach()[:, :, lo:hi])
+        sd = sharded.gather_state_dict(cc, cfg["dict_size"])
+        ref = full.state_dict()
+        assert list(sd) == list(ref)
+        for k in ref:
+            assert torch.equal(sd[k], ref[k]) and sd[k].stride() == ref[k].stride(), k
+        if rank == 0:
+            ccmod.write_checkpoint(sd, cfg, save_dir=pathlib.Path(tmpdir), version=0)
+        dist.barrier()
+        q.put((rank, True))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("enc_dtype", ["fp32", "bf16"])
+def test_sharded_init_is_reference_slice_and_gathers_back(enc_dtype, tmp_path):
+    """ShardedTrainer's default init (shard_crosscoder) gives rank r latents [lo, hi) of exactly the
+    crosscoder the reference builds for the whole dictionary (crosscoder.py:31-62), and
+    gather_state_dict reassembles the reference state_dict (values, key order, W_enc strides); the
+    rank-0 checkpoint is the reference's two-file format (crosscoder.py:132-146)."""
+    world = 2
+    port = 29500 + random.randint(2001, 4000)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_init_worker, args=(r, world, port, q, enc_dtype, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == {0: True, 1: True}
+    import json
+
+    import crosscoder_amd as ca
+
+    cfg = json.load(open(tmp_path / "0_cfg.json"))
+    sd = torch.load(tmp_path / "0.pt", weights_only=True)
+    ref = ca.CrossCoder(cfg).state_dict()
+    for k in ref:
+        assert torch.equal(sd[k], ref[k]) and sd[k].stride() == ref[k].stride(), k

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Experiment build of the library with extra defines (never shipped): tools/build_variant.sh NAME -DFOO=1 ...
-# -> crosscoder-model-diff-replication_amd/exp/NAME.so ; load it with CC_HIP_LIB=<path> (tools only).
+# -> crosscoder-model-diff-replication_amd/exp/NAME.so ; time it with tools/step_ab.py --lib <path> (tools only).
 set -e
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)

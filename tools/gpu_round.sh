@@ -34,7 +34,7 @@ for s in $STEPS; do
     gemm) run gemm_bench 300 python tools/gemm_bench.py crosscoder-model-diff-replication_amd/libcrosscoder_hip.so ;;
     ab) run gemm_ab 400 python tools/gemm_bench.py crosscoder-model-diff-replication_amd/exp/base.so \
           crosscoder-model-diff-replication_amd/libcrosscoder_hip.so ;;
-    stepab) run step_ab 400 python tools/step_ab.py "--only=${STEPAB_ONLY:-default,separate tails}" ;;
+    stepab) run step_ab 400 python tools/step_ab.py --spans ;;
     small) run small_bench 200 python tools/small_bench.py crosscoder-model-diff-replication_amd/exp/base.so \
              crosscoder-model-diff-replication_amd/libcrosscoder_hip.so ;;
     adam) run adam_bench 200 python tools/adam_bench.py crosscoder-model-diff-replication_amd/libcrosscoder_hip.so ;;
