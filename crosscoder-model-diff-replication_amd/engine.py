@@ -259,6 +259,24 @@ def loss_from_recon(ws, P, grad_scale=None):
     loss_finalize(ws)
 
 
+def loss_finalize_beside(ws, side_stream, on_losses=None):
+    """loss_finalize (+ on_losses(ws.scalars), e.g. the host copy) on `side_stream`, after everything
+    queued so far on torch's stream: the backward's G3 does not read the tail's outputs, so it starts
+    right after the loss kernel.  Returns the event the stream must wait for before G4 (whose L1 term
+    reads the tail's activation column sums)."""
+    dev = ws.x.device
+    ready = torch.cuda.Event()
+    ready.record(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side_stream):
+        side_stream.wait_event(ready)
+        loss_finalize(ws)
+        if on_losses is not None:
+            on_losses(ws.scalars)
+        done = torch.cuda.Event()
+        done.record(side_stream)
+    return done
+
+
 def row_chunks(B, n_chunks):
     """Batch slices [r0, r1) for the chunked (comm-overlapped) step: boundaries on 256-row GEMM
     tiles, so each slice's d_acts launch owns whole column-partial rows."""
@@ -280,9 +298,11 @@ def dacts_rows(ws, P, l1_coeff, r0, r1, l1_grad_weight=1.0):
                           colsum_part=ws.gpre_colpart[c0:c1])
 
 
-def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None, sums_out=None, zero_mask=0):
+def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None, sums_out=None, zero_mask=0,
+             tail_done=None):
     """Gradients of l2 + l1_coeff * l1 into the grads Arena G (+ squared-sum partials).
-    dacts_done: G3 already ran per batch slice (dacts_rows).  clip (max_norm, single-GPU step): the
+    dacts_done: G3 already ran per batch slice (dacts_rows).  tail_done: the event of a loss tail
+    running beside (loss_finalize_beside), waited for before G4.  clip (max_norm, single-GPU step): the
     bias-gradient sums and clip_grad_norm_'s coefficient in one launch (clip_and_adam then skips
     its clip_finalize).  sums_out (latent-sharded step): instead, the per-parameter squared sums in
     the same launch (segment_sums semantics, zero_mask), for the all-reduce."""
@@ -290,6 +310,8 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
     l1_scale = float(l1_coeff) * l1_grad_weight / B
     if not dacts_done:
         dacts_rows(ws, P, l1_coeff, 0, B, l1_grad_weight)
+    if tail_done is not None:
+        torch.cuda.current_stream(ws.x.device).wait_event(tail_done)
     with _span("G4G5_wgrad"):
         if ws.tr:
             ops.wgrad_both_t(ws.acts_t, ws.g_recon_t, P.W_dec_hk, ws.inv_norms, ws.colsum_acts, l1_scale,

@@ -108,24 +108,27 @@ class Trainer:
         ws = cc._workspace(raw.shape[0], step=True)
         P = cc.arena()
         opt = self.optimizer
-        engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None)
-        if on_losses is not None:
-            on_losses(ws.scalars)
+        side = self._side_stream()
+        engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None, loss=False)
+        engine.loss_rows(ws, P, 0, ws.B)
+        # the loss scalars (+ their host copy) on the side stream, beside G3
+        tail_done = engine.loss_finalize_beside(ws, side, on_losses)
         l1c = self.get_l1_coeff()
-        engine.backward(ws, P, opt.grads, l1c, clip=1.0)  # clip_grad_norm_(max_norm=1.0), trainer.py:46
+        # clip_grad_norm_(max_norm=1.0), trainer.py:46
+        engine.backward(ws, P, opt.grads, l1c, clip=1.0, tail_done=tail_done)
         g = opt.param_groups[0]
         opt.t += 1
         b1, b2 = g["betas"]
         engine.clip_and_adam(ws, P, opt.grads, opt.exp_avg, opt.exp_avg_sq, g["lr"], b1, b2, g["eps"], opt.t,
-                             side_stream=self._side_stream())
+                             side_stream=side)
         self.scheduler.step()
         self._last_l1c = l1c
         return ws.scalars
 
     def _copy_losses(self, scalars):
-        # the step's single device->host copy, enqueued as soon as the forward has produced the
-        # losses: the host waits for the forward only, and enqueues the next step while this
-        # step's backward / Adam still run (torch's stream orders every later use of the params)
+        # the step's single device->host copy, enqueued (on the side stream) as soon as the forward has
+        # produced the losses: the host waits for the forward only, and enqueues the next step while
+        # this step's backward / Adam still run
         if self._host is None:
             self._host = torch.empty(8, dtype=torch.float32, pin_memory=True)
             self._copied = torch.cuda.Event()
