@@ -8,6 +8,6 @@ at the repository root).
 from .crosscoder import CrossCoder, LossOutput, DTYPES  # noqa: F401
 from .trainer import Trainer  # noqa: F401
 from .buffer import Buffer, SyntheticBuffer  # noqa: F401
-from .analysis import decoder_stats, fold_activation_scaling_factor  # noqa: F401
+from .analysis import decoder_stats, fold_activation_scaling_factor, sae_vis_export  # noqa: F401
 
 __version__ = "0.1.0"

@@ -6,6 +6,10 @@
 * `fold_activation_scaling_factor(cc, *scales)` -- Crosscoder_model_diff.ipynb:35368-35378: fold the
   per-model activation normalisation factors into the weights (W_enc[m] *= s_m, W_dec[:, m] /= s_m,
   b_dec[m] /= s_m) so the crosscoder takes raw residual-stream activations (cc_fold_scaling).
+* `sae_vis_export(cc, *scales)` -- the notebook's latent-dashboard hand-off (:35735-35801): a copy with
+  the scaling factors folded into W_enc only, whose state_dict the sae_vis fork's CrossCoder loads
+  (`load_state_dict(folded_cross_coder.state_dict())`, keys / shapes of the reference), plus the
+  CrossCoderConfig fields that fork is built with.
 """
 import torch
 
@@ -36,3 +40,21 @@ def fold_activation_scaling_factor(cross_coder, *scaling_factors, fold_decoder=T
     ops.fold_scaling(a.W_enc_hk, a.W_dec_hk if fold_decoder else None, a.b_dec_flat if fold_decoder else None, s,
                      a.n, a.d)
     return cross_coder
+
+
+def sae_vis_export(cross_coder, *scaling_factors, dtype=torch.bfloat16):
+    """-> (state_dict on the CPU in `dtype`, sae_vis CrossCoderConfig kwargs).  The crosscoder itself
+    is left untouched (the notebook folds a deep copy, :35752-35763)."""
+    import copy
+
+    a = cross_coder.arena()
+    a.wait_pending()
+    ws, cross_coder._ws = cross_coder._ws, None  # (no copy of the step workspace)
+    try:
+        folded = copy.deepcopy(cross_coder)
+    finally:
+        cross_coder._ws = ws
+    fold_activation_scaling_factor(folded, *scaling_factors, fold_decoder=False)
+    sd = {k: v.detach().to("cpu", dtype) for k, v in folded.state_dict().items()}
+    cfg = {"d_in": cross_coder.cfg["d_in"], "d_hidden": cross_coder.cfg["dict_size"], "apply_b_dec_to_input": False}
+    return sd, cfg

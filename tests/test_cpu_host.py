@@ -112,6 +112,25 @@ def test_loads_reference_checkpoint(tmp_path):
         os.chdir(cwd)
 
 
+def test_load_from_hf_reads_a_local_hub_layout(tmp_path):
+    """crosscoder.py:160-205 minus the download: {local_dir}/{path}/cfg.json + cc_weights.pt (the Hub repo's
+    layout, e.g. blocks.14.hook_resid_pre/) loads through CrossCoder.load_from_hf(local_dir=...), the
+    device override applies, and the weights / strides are the file's."""
+    src = os.path.join(GOLDEN, "ckpt", "version_0")
+    cfg = json.load(open(os.path.join(src, "0_cfg.json")))
+    ref = torch.load(os.path.join(src, "0.pt"), weights_only=True)
+    d = tmp_path / "blocks.14.hook_resid_pre"
+    d.mkdir()
+    json.dump(dict(cfg, device="cuda:7"), open(d / "cfg.json", "w"))  # the override must win
+    torch.save(ref, d / "cc_weights.pt")
+    cc = ca.CrossCoder.load_from_hf(path="blocks.14.hook_resid_pre", device="cpu", local_dir=tmp_path)
+    assert cc.cfg["device"] == "cpu"
+    for k, v in ref.items():
+        assert torch.equal(cc.state_dict()[k], v) and cc.state_dict()[k].stride() == v.stride(), k
+    with pytest.raises(RuntimeError, match="no network"):
+        ca.CrossCoder.load_from_hf()
+
+
 def test_arena_repacks_after_param_replacement():
     cc = ca.CrossCoder(_cfg())
     before = cc.W_dec.detach().clone()

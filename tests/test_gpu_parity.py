@@ -986,3 +986,25 @@ def test_param_access_orders_after_side_stream_adam(gpu):
     w = cc.W_dec.detach().clone()
     torch.cuda.synchronize()
     assert torch.equal(w, cc.W_dec.detach())
+
+
+def test_sae_vis_export_matches_notebook_fold(gpu):
+    """Crosscoder_model_diff.ipynb:35752-35801: the encoder-only fold of the scaling factors into a copy,
+    exported as the state_dict the sae_vis fork loads: same keys / shapes / strides as the reference,
+    W_enc[m] scaled bit-identically to the notebook's torch ops, W_dec / biases unchanged, and the live
+    crosscoder untouched."""
+    r = load("step_b64_n2_d32_h256_bf16")
+    cfg = dict(r["cfg"], device=str(gpu))
+    cc = make_cc(cfg, r["init"], gpu, 2)
+    base, chat = 0.2758961493232058, 0.24422852496546169
+    sd, vcfg = ca.sae_vis_export(cc, base, chat)
+    assert vcfg == {"d_in": 32, "d_hidden": 256, "apply_b_dec_to_input": False}
+    ref = {k: v.clone() for k, v in r["init"].items()}
+    ref["W_enc"][0] = ref["W_enc"][0] * base
+    ref["W_enc"][1] = ref["W_enc"][1] * chat
+    assert list(sd) == list(ref)
+    for k in ref:
+        assert sd[k].dtype == torch.bfloat16 and sd[k].shape == ref[k].shape and sd[k].stride() == ref[k].stride()
+        assert torch.equal(sd[k], ref[k]), k
+    for k, v in r["init"].items():  # the source crosscoder is unchanged
+        assert torch.equal(cc.state_dict()[k].cpu(), v), k

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) short bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
@@ -15,7 +17,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 
 #ifndef G4_NST
-#define G4_NST 4
+#define G4_NST 5
 #endif
 #ifndef G4_GM
 #define G4_GM 4
@@ -47,6 +49,14 @@ __device__ __forceinline__ void tile_of_block(int bid, int nbm, int nbn, int& tm
   int w = wg - g * per_group;
   tm = first + w % gm;
   tn = w / gm;
+}
+
+// MFMA with the accumulator pinned to AGPRs (the compiler otherwise splits the 256 accumulators
+// between the VGPR and AGPR files and copies them around the MFMAs).  Only accumulate chains use
+// the AGPRs inside the loop (D -> C of the next MFMA on the same registers needs no wait states);
+// the epilogue's first read follows a 12-state s_nop.
+__device__ __forceinline__ void mfma_a(f32x4& acc, const bf16x8& b, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
 }
 
 __device__ __forceinline__ unsigned short f2bf(float f) { return __builtin_bit_cast(unsigned short, (__bf16)f); }
@@ -94,29 +104,81 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const void* __restrict__
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // B fragments double-buffered in registers (Bf[cur] for this sub-step, Bf[nxt] filled for the next
+  // one), A fragments streamed one row group ahead (Af[i & 1])
+  bf16x8 Bf[2][8], Af[4];
+  auto frag = [&](int s, int f) {  // f 0..7: A row group f; 8..15: B column group f - 8
+    const char* st = smem + (s % NST) * STAGE;
+    const char* base = f < 8 ? st + wr * 128 * 64 + f * 16 * 64 : st + 256 * 64 + wc * 128 * 64 + (f - 8) * 16 * 64;
+    return *(const bf16x8*)(base + foff);
+  };
+
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s) issue(s);
-
-  for (int s = 0; s < nk; ++s) {
-    wait_vmcnt<8 * (NST - 2)>();  // this wave's DMAs of sub-step s landed
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of sub-step s - 1 are done
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();  // everyone's did, and everyone finished reading sub-step s - 1
-    __builtin_amdgcn_sched_barrier(0);
-    issue(s + NST - 1);            // into the stage sub-step s - 1 used
-    const char* la = smem + (s % NST) * STAGE + wr * 128 * 64;
-    const char* lb = smem + (s % NST) * STAGE + 256 * 64 + wc * 128 * 64;
-    bf16x8 bf[8];
+  wait_vmcnt<8 * (NST - 2)>();
+  __builtin_amdgcn_s_barrier();
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bf[j] = *(const bf16x8*)(lb + j * 16 * 64 + foff);
+  for (int j = 0; j < 8; ++j) Bf[0][j] = frag(0, 8 + j);
+  Af[0] = frag(0, 0);
+  Af[1] = frag(0, 1);
+
+  // sub-step s: row group i = MFMAs A_i x B_0..7, then the reads of A_{i+2} (stage s, or s + 1 past row 5) and
+  // B_i (stage s + 1).  Stage s is read during sub-steps s - 1 (B, A row 0) and s (A rows 1..7).  After row 0
+  // the barrier: stage s + 1 landed everywhere (RAW for the B reads that follow), and every wave is
+  // past sub-step s - 1, the last reader of stage s - 1, which takes the DMAs of sub-step s + NST - 1
+  // (WAR).  Prefetch distance NST - 2 sub-steps.
+  auto substep = [&](auto cur_c, int s) {
+    constexpr int cur = decltype(cur_c)::value, nxt = cur ^ 1;
+    char* dst = dst0 + ((s + NST - 1) % NST) * STAGE;
+    const uint32_t kb = (uint32_t)((s + NST - 1) * 64);
+    const bool live = s + NST - 1 < nk;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const bf16x8 af = *(const bf16x8*)(la + i * 16 * 64 + foff);
+      const bf16x8 a = Af[i & 3];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af, acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 8; ++j) {
+#ifdef G4_ASM_MFMA
+        mfma_a(acc[i][j], Bf[cur][j], a);
+#else
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Bf[cur][j], a, acc[i][j], 0, 0, 0);
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+        // rows 1..4: the 8 DMAs of sub-step s + NST - 1, one after every other MFMA
+        if (i >= 1 && i <= 4 && (j & 3) == 1) {
+          const int q = (i - 1) * 2 + (j >> 2);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (lds_void*)(dst + q * 1024), 16,
+                                                   (int)(live ? voff0 + q * vstep + kb : OOB), 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        // the fragment reads: A two row groups ahead after MFMA 2, B of s + 1 after MFMA 5
+        if (j == 2) {
+          Af[(i + 2) & 3] = i < 6 ? frag(s, i + 2) : frag(s + 1, i - 6);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (j == 5 && i >= 1) {
+          Bf[nxt][i - 1] = frag(s + 1, 8 + i - 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (i == 0) {  // the barrier of sub-step s + 1 (see above)
+        wait_vmcnt<8 * (NST - 3)>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
+    Bf[nxt][7] = frag(s + 1, 15);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  int s = 0;
+  for (; s + 1 < nk; s += 2) {
+    substep(std::integral_constant<int, 0>{}, s);
+    substep(std::integral_constant<int, 1>{}, s + 1);
   }
+  if (s < nk) substep(std::integral_constant<int, 0>{}, s);
   wait_vmcnt<0>();
+#ifdef G4_ASM_MFMA
+  asm volatile("s_nop 11\n\ts_nop 4" ::: "memory");
+#endif
   // epilogue: lane holds row (lane & 15), 4 consecutive columns 4 * (lane >> 4) of each 16 x 16 block
   const __amdgpu_buffer_rsrc_t rc = rsrc((char*)C + ((int64_t)m0 * ldc + n0) * 2,
                                          ((uint64_t)(M - m0 - 1) * ldc + (N - n0)) * 2);

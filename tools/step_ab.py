@@ -1,7 +1,7 @@
-"""Whole-step timing of the shipped schedule, config 2, for in-process or same-box A/B of library
-builds: python tools/step_ab.py [--lib path/to/variant.so] [--spans] [--rounds R]
-(--lib: load this build instead of the in-tree library -- tools only; --spans: per-launch HIP-event
-averages as well).  Earlier scheduling variants and their measurements: DESIGN.md section 8."""
+"""Whole-step timing of config 2 on ONE device, for same-box A/B: schedule variants of the decoder-half
+Adam are defined HERE (monkeypatching engine.adam inside this process) -- the product keeps a single
+schedule -- and library builds via --lib.  Variants run interleaved, 20 steps per sample.
+  python tools/step_ab.py [--lib path/to/variant.so] [--spans] [--rounds R] [--only=a,b]"""
 import argparse
 import os
 import sys
@@ -12,11 +12,51 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def fused_dec_adam(blocks):
+    """Decoder half as the 64x64-tile Adam that also writes W_dec^T + the norm partials (one HBM pass,
+    cc_adam_dec_transposed) with a capped grid, beside the next step's G1."""
+    from crosscoder_amd import engine, ops
+
+    def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None):
+        coef = ws.clip_out[0:1]
+        dev = P.data.device
+        ops.adam_step(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), coef, lr, beta1, beta2, eps, step)
+        enc_done = torch.cuda.Event()
+        enc_done.record(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side_stream):
+            side_stream.wait_event(enc_done)
+            ops.adam_dec_transposed(P.W_dec_hk, G.W_dec_hk, M.W_dec_hk, V.W_dec_hk, coef, lr, beta1, beta2, eps, step,
+                                    ws.W_dec_t, ws.norm_part, max_blocks=blocks)
+            ops.adam_step(P.b_dec_flat, G.b_dec_flat, M.b_dec_flat, V.b_dec_flat, coef, lr, beta1, beta2, eps, step)
+            ops.dec_norms_finalize(ws.norm_part, ws.h, ws.n, ws.d, ws.norms, ws.tn, ws.inv_norms)
+            ws.norms_token = engine._norms_token(P)
+            done = torch.cuda.Event()
+            done.record(side_stream)
+        P.pending = done
+    return adam
+
+
+def flat_dec_adam(blocks):
+    from crosscoder_amd import engine
+
+    shipped = engine.adam
+
+    def adam(*a, **k):
+        old = engine.DEC_ADAM_BLOCKS
+        engine.DEC_ADAM_BLOCKS = blocks
+        try:
+            shipped(*a, **k)
+        finally:
+            engine.DEC_ADAM_BLOCKS = old
+    return adam
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib")
     ap.add_argument("--spans", action="store_true")
     ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--only")
     args = ap.parse_args()
     import crosscoder_amd as ca
 
@@ -29,25 +69,42 @@ def main():
     B, n, d, h = bench.CONFIGS[2]
     cfg = bench.make_cfg(B, n, d, h)
     tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 8, seed=0), crosscoder=ca.CrossCoder(cfg))
-    timer = bench.EventTimer() if args.spans else None
-    for _ in range(5):
-        tr.step()
-    res = []
-    for _ in range(args.rounds):
-        torch.cuda.synchronize()
-        if timer is not None:
-            timer.enabled = True
-            engine.TIMER = timer
-        t0 = time.perf_counter()
-        for _ in range(20):
+    shipped = engine.adam
+    variants = {"shipped": shipped}
+    for b in (64, 96, 128, 192, 256):
+        variants[f"fused dec Adam {b} blocks"] = fused_dec_adam(b)
+    variants["flat dec Adam 512 blocks"] = flat_dec_adam(512)
+    if args.only:
+        keep = args.only.split(",")
+        variants = {k: v for k, v in variants.items() if k in keep}
+    timers = {k: bench.EventTimer() for k in variants} if args.spans else {}
+    res = {k: [] for k in variants}
+    for fn in variants.values():
+        engine.adam = fn
+        for _ in range(3):
             tr.step()
-        torch.cuda.synchronize()
-        engine.TIMER = None
-        res.append((time.perf_counter() - t0) / 20 * 1e3)
-    res.sort()
-    print(f"{args.lib or 'in-tree'}: median {res[len(res) // 2]:.4f} ms/step  min {res[0]:.4f}")
-    if timer is not None:
-        print("   ", {k: round(v, 4) for k, v in timer.averages_ms().items()})
+    for _ in range(args.rounds):
+        for name, fn in variants.items():
+            engine.adam = fn
+            tr.step()  # switch-over step (the previous variant's side-stream work drains)
+            tr.synchronize()
+            torch.cuda.synchronize()
+            if args.spans:
+                timers[name].enabled = True
+                engine.TIMER = timers[name]
+            t0 = time.perf_counter()
+            for _ in range(20):
+                tr.step()
+            torch.cuda.synchronize()
+            engine.TIMER = None
+            res[name].append((time.perf_counter() - t0) / 20 * 1e3)
+    engine.adam = shipped
+    print(f"library: {args.lib or 'in-tree'}")
+    for name, ts in res.items():
+        ts.sort()
+        print(f"{name:28s} median {ts[len(ts) // 2]:.4f} ms/step  min {ts[0]:.4f}")
+        if args.spans:
+            print("   ", {k: round(v, 4) for k, v in timers[name].averages_ms().items()})
 
 
 if __name__ == "__main__":
