@@ -50,19 +50,35 @@ def clip_sums_for_allreduce(sums, rank):
     return out
 
 
+def own_rows(B, world, rank, align=32):
+    """Batch rows [r0, r1) whose loss this rank computes in the reduce-scatter exchange (`align`-row
+    aligned: 32 = the HIP loss kernel's row blocks)."""
+    if B % (align * world):
+        raise ValueError(f"batch {B} must be a multiple of {align} x world ({align * world}) for "
+                         "comm='reduce_scatter'")
+    r = B // world
+    return rank * r, (rank + 1) * r
+
+
 class ShardedStep:
-    def __init__(self, backend, group=None):
+    """comm: how the partial reconstructions are combined.
+      "all_reduce"      fp32 all-reduce of [B, n*d] in batch slices; each slice's loss and d_acts rows
+                        run as it lands (2 x 4*B*n*d*(G-1)/G bytes per rank on the wire)
+      "reduce_scatter"  fp32 reduce-scatter by batch rows -> loss on this rank's B/G rows -> bf16
+                        all-gather of g_recon (+ the small loss partial slabs) -> d_acts on the whole
+                        batch (4*B*n*d*(G-1)/G + 2*B*n*d*(G-1)/G bytes: 25 % fewer)."""
+
+    def __init__(self, backend, group=None, comm="all_reduce"):
+        if comm not in ("all_reduce", "reduce_scatter"):
+            raise ValueError(f"comm must be 'all_reduce' or 'reduce_scatter', got {comm!r}")
         self.b = backend
         self.group = group
+        self.comm = comm
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
 
-    def step(self, raw, factor, l1c, lr, betas, eps, t, max_norm=1.0, on_losses=None):
-        """One step -> (scalars, red): the loss scalars (l1 / l0 of this rank's latents only) and the
-        all-reduced [4 squared-gradient sums, l1, l0].  on_losses(scalars, red) is called once both
-        are final on the device (before the clip / Adam launches)."""
+    def _combine_all_reduce(self, recon, l1c):
         b = self.b
-        recon = b.forward_partial(raw, factor)
         chunks = b.row_chunks()
         # every slice's all-reduce is queued at once on the collective stream; the compute stream
         # waits for slice c only when it needs it
@@ -71,6 +87,27 @@ class ShardedStep:
         for (r0, r1), w in zip(chunks, works):
             w.wait()
             b.rows_ready(r0, r1, l1c)                # loss rows + g_recon + d_acts rows of the slice
+
+    def _combine_reduce_scatter(self, recon, l1c):
+        b = self.b
+        r0, r1 = own_rows(recon.shape[0], self.world, self.rank, getattr(b, "row_align", 32))
+        mine = b.own_recon_buffer(r1 - r0)
+        dist.reduce_scatter_tensor(mine, recon, op=dist.ReduceOp.SUM, group=self.group)
+        b.loss_own_rows(mine, r0, r1)                # this rank's loss rows: g_recon rows, row terms
+        for out, inp in b.gather_pairs(r0, r1, self.world):
+            dist.all_gather_into_tensor(out, inp, group=self.group)
+        b.after_gather(l1c)                          # the whole batch's g_recon (+^T) -> d_acts (G3)
+
+    def step(self, raw, factor, l1c, lr, betas, eps, t, max_norm=1.0, on_losses=None):
+        """One step -> (scalars, red): the loss scalars (l1 / l0 of this rank's latents only) and the
+        all-reduced [4 squared-gradient sums, l1, l0].  on_losses(scalars, red) is called once both
+        are final on the device (before the clip / Adam launches)."""
+        b = self.b
+        recon = b.forward_partial(raw, factor)
+        if self.comm == "all_reduce":
+            self._combine_all_reduce(recon, l1c)
+        else:
+            self._combine_reduce_scatter(recon, l1c)
         red = b.reduce_buffer()                      # [6]: 4 clip sums + l1, l0 (latent-local)
         scalars = b.loss_finalize(red)               # [l2, l1, l0, ev, ev_a, ev_b, ...]; red[4:6] = local l1, l0
         # l1 / l0 over all ranks first (8 bytes, async on the collective stream): the losses are final
@@ -116,6 +153,39 @@ class HipShardBackend:
         engine.loss_rows(self.ws, P, r0, r1)
         engine.dacts_rows(self.ws, P, l1c, r0, r1)
 
+    # ---- comm="reduce_scatter"
+    def own_recon_buffer(self, rows):
+        ws = self.ws
+        if getattr(ws, "rs_recon", None) is None or ws.rs_recon.shape[0] != rows:
+            ws.rs_recon = torch.empty(rows, ws.K, dtype=torch.float32, device=ws.x.device)
+        return ws.rs_recon
+
+    def loss_own_rows(self, mine, r0, r1):
+        ws = self.ws
+        ws.recon[r0:r1].copy_(mine)
+        engine.loss_rows(ws, self.cc.arena(), r0, r1)  # g_recon rows, row terms, db_dec partial rows
+
+    def gather_pairs(self, r0, r1, world):
+        """(output, input) pairs for all_gather_into_tensor: g_recon rows (bf16), the db_dec partial rows
+        (fp32, one per 32 batch rows) and the loss row terms (fp32 [2, n*ncb, B] slab, by columns)."""
+        ws = self.ws
+        p0, p1 = r0 // 32, r1 // 32
+        rp = ws.row_part
+        # gathered concatenated along dim 0 ([world * 2, n*ncb, rows]; gloo takes only that form)
+        self._rp_all = torch.empty(world * rp.shape[0], rp.shape[1], r1 - r0, device=rp.device)
+        return [(ws.g_recon, ws.g_recon[r0:r1].clone()),
+                (ws.loss_colpart, ws.loss_colpart[p0:p1].clone()),
+                (self._rp_all, rp[:, :, r0:r1].contiguous())]
+
+    def after_gather(self, l1c):
+        ws = self.ws
+        rp = ws.row_part
+        rp.copy_(self._rp_all.view(-1, rp.shape[0], rp.shape[1], self._rp_all.shape[2]).permute(1, 2, 0, 3)
+                 .reshape(rp.shape))
+        if ws.tr:
+            ops.transpose(ws.g_recon, out=ws.g_recon_t)
+        engine.dacts_rows(ws, self.cc.arena(), l1c, 0, ws.B)
+
     def loss_finalize(self, red):
         engine.loss_finalize(self.ws, l1l0_out=red[4:6])
         return self.ws.scalars
@@ -150,7 +220,7 @@ class ShardedTrainer:
     """Trainer.step contract over latent shards (the whole job is one crosscoder with
     cfg["dict_size"] latents; this rank trains its slice)."""
 
-    def __init__(self, cfg, buffer, group=None, crosscoder=None, recon_chunks=None, logger=None):
+    def __init__(self, cfg, buffer, group=None, crosscoder=None, recon_chunks=None, logger=None, comm="all_reduce"):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -164,7 +234,7 @@ class ShardedTrainer:
         self.buffer = buffer
         chunks = recon_chunks if recon_chunks is not None else cfg.get("recon_chunks", 4)
         self.backend = HipShardBackend(crosscoder, recon_chunks=chunks)
-        self.engine = ShardedStep(self.backend, group)
+        self.engine = ShardedStep(self.backend, group, comm=comm)
         self.total_steps = cfg["num_tokens"] // cfg["batch_size"]
         self.step_counter = 0
         self.t = 0

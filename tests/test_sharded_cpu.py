@@ -23,6 +23,8 @@ class CpuShardBackend:
         self.P = {k: torch.nn.Parameter(v.detach().clone()) for k, v in P.items()}
         self.m = {k: torch.zeros_like(v) for k, v in self.P.items()}
         self.v = {k: torch.zeros_like(v) for k, v in self.P.items()}
+        self.rs = False
+        self.row_align = 1
 
     def forward_partial(self, raw, factor):
         self.x = O.buffer_next(raw, factor)
@@ -41,9 +43,40 @@ class CpuShardBackend:
         return torch.zeros(6)
 
     def loss_finalize(self, red):
-        scalars = self.loss_from_full_recon()
+        scalars = self.rs_scalars() if self.rs else self.loss_from_full_recon()
         red[4:6] = scalars[1:3]
         return scalars
+
+    # ---- comm="reduce_scatter": loss on this rank's rows, then the gathered g_recon drives the backward
+    def own_recon_buffer(self, rows):
+        self.rs = True
+        return torch.empty(rows, N_MODELS, D)
+
+    def loss_own_rows(self, mine, r0, r1):
+        with torch.no_grad():
+            x = self.x
+            diff = mine + self.P["b_dec"] - x[r0:r1]
+            self.g_rows = (2.0 * diff / x.shape[0]).contiguous()
+            l2_rows = diff.pow(2).sum(dim=(1, 2))
+            tv_rows = (x[r0:r1] - x.mean(0)).pow(2).sum(dim=(1, 2))
+            self.terms = torch.stack([l2_rows, 1 - l2_rows / (tv_rows + 1e-8)])
+            self.dbd = self.g_rows.sum(0, keepdim=True)
+
+    def gather_pairs(self, r0, r1, world):
+        B = self.x.shape[0]
+        self.g_full = torch.empty(B, N_MODELS, D)
+        self.terms_all = torch.empty(world * 2, r1 - r0)  # (concatenated along dim 0: gloo's form)
+        self.dbd_all = torch.empty(world, N_MODELS, D)
+        return [(self.g_full, self.g_rows), (self.terms_all, self.terms), (self.dbd_all, self.dbd)]
+
+    def after_gather(self, l1c):
+        self.l1 = (self.acts * self.P["W_dec"].norm(dim=-1).sum(1)[None]).sum(-1).mean(0)
+
+    def rs_scalars(self):
+        t = self.terms_all.view(-1, 2, self.terms_all.shape[1]).permute(1, 0, 2).reshape(2, -1)
+        l0 = (self.acts > 0).float().sum(-1).mean()
+        ev = t[1].mean()
+        return torch.stack([t[0].mean(), self.l1.detach(), l0, ev, ev, ev])
 
     def loss_from_full_recon(self):
         self.R = self.recon.clone().requires_grad_(True)
@@ -62,9 +95,13 @@ class CpuShardBackend:
     def backward(self, l1c, red, rank):
         for p in self.P.values():
             p.grad = None
-        gl2 = torch.autograd.grad(self.l2, [self.R, self.P["b_dec"]], retain_graph=True)
-        (self.partial * gl2[0]).sum().add(l1c * self.l1).backward()
-        self.P["b_dec"].grad = gl2[1]
+        if self.rs:  # d(l2)/d(recon) = the gathered g_recon; d(l2)/d(b_dec) = the ranks' row sums
+            (self.partial * self.g_full).sum().add(l1c * self.l1).backward()
+            self.P["b_dec"].grad = self.dbd_all.sum(0)
+        else:
+            gl2 = torch.autograd.grad(self.l2, [self.R, self.P["b_dec"]], retain_graph=True)
+            (self.partial * gl2[0]).sum().add(l1c * self.l1).backward()
+            self.P["b_dec"].grad = gl2[1]
         sums = torch.stack([self.P[k].grad.pow(2).sum() for k in O.PARAM_ORDER])
         red[0:4] = sharded.clip_sums_for_allreduce(sums, rank)
 
@@ -87,7 +124,7 @@ def _setup():
     return cfg, P, raws, factor
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, comm):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -97,7 +134,7 @@ def _worker(rank, world, port, q):
         Ps = {"W_enc": P["W_enc"][:, :, lo:hi], "W_dec": P["W_dec"][lo:hi], "b_enc": P["b_enc"][lo:hi],
               "b_dec": P["b_dec"]}
         backend = CpuShardBackend(Ps)
-        step = sharded.ShardedStep(backend)
+        step = sharded.ShardedStep(backend, comm=comm)
         outs = []
         seen = []
 
@@ -118,12 +155,15 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("comm", ["all_reduce", "reduce_scatter"])
 @pytest.mark.parametrize("world", [2])
-def test_sharded_step_matches_unsharded(world):
+def test_sharded_step_matches_unsharded(world, comm):
+    """Both exchanges of the partial reconstructions: the sliced all-reduce, and the
+    reduce-scatter by batch rows -> loss on B/G rows -> all-gather of g_recon and the row terms."""
     port = 29500 + random.randint(0, 2000)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, comm)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}

@@ -143,9 +143,10 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const void* __restrict__
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Bf[cur][j], a, acc[i][j], 0, 0, 0);
 #endif
         __builtin_amdgcn_sched_barrier(0);
-        // rows 1..4: the 8 DMAs of sub-step s + NST - 1, one after every other MFMA
-        if (i >= 1 && i <= 4 && (j & 3) == 1) {
-          const int q = (i - 1) * 2 + (j >> 2);
+        // the 8 DMAs of sub-step s + NST - 1 spread one per row group (two in row 1) after the
+        // barrier: an LDS-DMA piece costs ~60 issue cycles, hidden only behind ~4 queued MFMAs
+        if (i >= 1 && (j == 3 || (i == 1 && j == 7))) {
+          const int q = (i == 1 && j == 7) ? 0 : i;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (lds_void*)(dst + q * 1024), 16,
                                                    (int)(live ? voff0 + q * vstep + kb : OOB), 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);

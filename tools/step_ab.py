@@ -51,6 +51,36 @@ def flat_dec_adam(blocks):
     return adam
 
 
+class G2FromWdec:
+    """Variant: G2 reads W_dec directly (MN operand, cc_decode_fwd_ws) and the side stream computes only
+    the decoder norms -- no W_dec^T pass (302 MB of HBM traffic less per step)."""
+
+    def __init__(self, tr):
+        from crosscoder_amd import engine, ops
+        self.engine, self.ops, self.tr = engine, ops, tr
+        self.saved = (ops.decode_partial_t, engine._decoder_derived)
+
+    def on(self):
+        engine, ops, tr = self.engine, self.ops, self.tr
+        P = tr.crosscoder.arena()
+        plain_decode = self.saved[0].__globals__["decode_partial"]
+
+        def decode_partial_t(acts, W_dec_t, recon, ws=None):
+            plain_decode(acts, P.W_dec_hk, recon, ws)
+
+        def decoder_derived(ws, P_):
+            with engine._span("dec_norms"):
+                ops.dec_norms(P_.W_dec_hk, ws.h, ws.n, ws.d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
+
+        ops.decode_partial_t = decode_partial_t
+        engine._decoder_derived = decoder_derived
+        tr.crosscoder._ws.norms_token = None
+
+    def off(self):
+        self.ops.decode_partial_t, self.engine._decoder_derived = self.saved
+        self.tr.crosscoder._ws.norms_token = None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib")
@@ -70,22 +100,42 @@ def main():
     cfg = bench.make_cfg(B, n, d, h)
     tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 8, seed=0), crosscoder=ca.CrossCoder(cfg))
     shipped = engine.adam
-    variants = {"shipped": shipped}
+    tr.step()
+    g2mn = G2FromWdec(tr)
+    # name -> (adam function, setup, teardown)
+    variants = {"shipped": (shipped, None, None)}
     for b in (64, 96, 128, 192, 256):
-        variants[f"fused dec Adam {b} blocks"] = fused_dec_adam(b)
-    variants["flat dec Adam 512 blocks"] = flat_dec_adam(512)
+        variants[f"fused dec Adam {b} blocks"] = (fused_dec_adam(b), None, None)
+    variants["flat dec Adam 512 blocks"] = (flat_dec_adam(512), None, None)
+    variants["G2 from W_dec (no W_dec^T pass)"] = (shipped, g2mn.on, g2mn.off)
     if args.only:
         keep = args.only.split(",")
         variants = {k: v for k, v in variants.items() if k in keep}
     timers = {k: bench.EventTimer() for k in variants} if args.spans else {}
     res = {k: [] for k in variants}
-    for fn in variants.values():
+
+    def use(v):
+        fn, setup, _ = v
+        tr.synchronize()
+        torch.cuda.synchronize()
         engine.adam = fn
+        if setup:
+            setup()
+
+    def drop(v):
+        tr.synchronize()
+        torch.cuda.synchronize()
+        if v[2]:
+            v[2]()
+
+    for v in variants.values():
+        use(v)
         for _ in range(3):
             tr.step()
+        drop(v)
     for _ in range(args.rounds):
-        for name, fn in variants.items():
-            engine.adam = fn
+        for name, v in variants.items():
+            use(v)
             tr.step()  # switch-over step (the previous variant's side-stream work drains)
             tr.synchronize()
             torch.cuda.synchronize()
@@ -98,6 +148,7 @@ def main():
             torch.cuda.synchronize()
             engine.TIMER = None
             res[name].append((time.perf_counter() - t0) / 20 * 1e3)
+            drop(v)
     engine.adam = shipped
     print(f"library: {args.lib or 'in-tree'}")
     for name, ts in res.items():
