@@ -93,6 +93,20 @@ CC_DEV void load8f(const float* base, int64_t idx, float v[8]) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
 }
+CC_DEV void load8f_nt(const float* base, int64_t idx, float v[8]) {
+  const f32x4* p = (const f32x4*)(base + idx);
+  f32x4 a = __builtin_nontemporal_load(p), b = __builtin_nontemporal_load(p + 1);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+}
+// cache policy chosen at compile time: NT = non-temporal (read / written once in the step: keep the
+// Infinity Cache for operands that are read again soon)
+template <int DT, bool NT> CC_DEV void ld8(const void* b, int64_t i, float v[8]) {
+  if constexpr (NT) load8_nt<DT>(b, i, v); else load8<DT>(b, i, v);
+}
+template <int DT, bool NT> CC_DEV void st8(void* b, int64_t i, const float v[8]) {
+  if constexpr (NT) store8_nt<DT>(b, i, v); else store8<DT>(b, i, v);
+}
 
 CC_DEV float wave_sum(float v) {
 #pragma unroll

@@ -43,6 +43,13 @@ CC_DEV void tile_store_transposed(const char* lds, void* out_t, int64_t ldt, int
   }
 }
 
+#ifndef CC_PREP_RAW_NT  // the raw batch is read once per step
+#define CC_PREP_RAW_NT 0
+#endif
+#ifndef CC_LOSS_RECON_NT  // the fp32 reconstruction is read once
+#define CC_LOSS_RECON_NT 0
+#endif
+
 // ---------------------------------------------------------------------------------------
 // x_out = dtype(x_in * factor[model]);  colsum_part[rb][k] = sum over the block's rows.
 // grid: (ceil(K/512), ceil(B/64)); block 256 = 4 waves; lane -> 8 columns, wave -> 16 rows.
@@ -71,7 +78,7 @@ __global__ __launch_bounds__(256) void prep_kernel(const void* __restrict__ x_in
         float v[8][8];
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-          if (base + wave + 4 * k < B) load8<DIN>(x_in, (int64_t)(base + wave + 4 * k) * K + col, v[k]);
+          if (base + wave + 4 * k < B) ld8<DIN, CC_PREP_RAW_NT>(x_in, (int64_t)(base + wave + 4 * k) * K + col, v[k]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const int r = base + wave + 4 * k;
@@ -269,7 +276,8 @@ __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ rec
 #pragma unroll
       for (int u = 0; u < 2; ++u)
         if (ra + 4 * u < row_end) {
-          load8f(recon, (int64_t)(ra + 4 * u) * K + col, rv[u]);
+          if constexpr (CC_LOSS_RECON_NT) load8f_nt(recon, (int64_t)(ra + 4 * u) * K + col, rv[u]);
+          else load8f(recon, (int64_t)(ra + 4 * u) * K + col, rv[u]);
           load8<DT>(x, (int64_t)(ra + 4 * u) * K + col, xv[u]);
         }
     }
@@ -638,6 +646,13 @@ CC_DEV void adam_elem(const AdamArgs& a, float coef, float& p, float g, float& m
 #ifndef CC_ADAM_U
 #define CC_ADAM_U 1
 #endif
+// cache policy of the bulk (encoder-half / whole-arena) Adam: 0 every access temporal, 1 g / m / v
+// non-temporal and p temporal (the updated weights stay in the Infinity Cache for the next GEMM that
+// reads them), 2 every access non-temporal
+#ifndef CC_ADAM_BULK_NT
+#define CC_ADAM_BULK_NT 1
+#endif
+
 // Bulk of the arena: U 8-element chunks per thread, all 4*U loads issued before any math, one
 // pass over the grid (no grid-stride loop).  U = 1 measured fastest (390 us for the 151 M-element
 // config-2 arena = 5.4 TB/s; U = 2: 398 us; the grid-stride loop: 431 us).
@@ -650,7 +665,9 @@ __global__ __launch_bounds__(256) void adam_bulk_kernel(const AdamArgs a, int64_
   for (int u = 0; u < U; ++u) {
     const int64_t c = c0 + u * 256;
     if (c < nchunks) {
-      load8<DT>(a.p, c * 8, p[u]); load8<DT>(a.g, c * 8, g[u]); load8<DT>(a.m, c * 8, m[u]); load8<DT>(a.v, c * 8, v[u]);
+      constexpr bool PN = CC_ADAM_BULK_NT == 2, SN = CC_ADAM_BULK_NT >= 1;
+      ld8<DT, PN>(a.p, c * 8, p[u]); ld8<DT, SN>(a.g, c * 8, g[u]); ld8<DT, SN>(a.m, c * 8, m[u]);
+      ld8<DT, SN>(a.v, c * 8, v[u]);
     }
   }
 #pragma unroll
@@ -659,7 +676,8 @@ __global__ __launch_bounds__(256) void adam_bulk_kernel(const AdamArgs a, int64_
     if (c < nchunks) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) adam_elem<DT>(a, coef, p[u][j], g[u][j], m[u][j], v[u][j]);
-      store8<DT>(a.p, c * 8, p[u]); store8<DT>(a.m, c * 8, m[u]); store8<DT>(a.v, c * 8, v[u]);
+      constexpr bool PN = CC_ADAM_BULK_NT == 2, SN = CC_ADAM_BULK_NT >= 1;
+      st8<DT, PN>(a.p, c * 8, p[u]); st8<DT, SN>(a.m, c * 8, m[u]); st8<DT, SN>(a.v, c * 8, v[u]);
     }
   }
 }
@@ -702,7 +720,12 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
       p[j] = pj; m[j] = mj; v[j] = vj;
     }
     if (full) {
-      store8_nt<DT>(a.p, i, p); store8_nt<DT>(a.m, i, m); store8_nt<DT>(a.v, i, v);
+#if CC_ADAM_SIDE_PT  // experiment: the updated weights stored temporal (kept in the Infinity Cache)
+      store8<DT>(a.p, i, p);
+#else
+      store8_nt<DT>(a.p, i, p);
+#endif
+      store8_nt<DT>(a.m, i, m); store8_nt<DT>(a.v, i, v);
     } else {
       for (int j = 0; j < 8 && i + j < a.numel; ++j) {
         ((typename E::T*)a.p)[i + j] = E::from_f(p[j]);
