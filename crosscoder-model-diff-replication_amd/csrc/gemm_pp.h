@@ -273,13 +273,25 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
   }
 
   // issue phase p's DMAs for step T (target buffer T & 1)
-  // TAIL: the step may lie past the end (prologue and the last two K steps only: the steady-state
-  // loop stays free of the branch)
+  // tail: 1 = the step may lie past the end (prologue and the last two K steps only: the steady-state
+  // loop stays free of the branch); 0 = steady state; 2 = steady state of a K % 64 == 0 contraction:
+  // every lane's step lies inside K, so the K advance rides in the scalar offset (no per-DMA VALU)
   auto issue_t = [&](auto tail, int p, int T) {
+    constexpr int TL = decltype(tail)::value;
     const bool isA = p < 2;
     const int k0 = (kb0 + T) * 64;
     char* dst = smem + (T & 1) * BUF + (isA ? 0 : TILE);
-    if (decltype(tail)::value && pf && T >= nk) {  // W_dec quarter 0 (B, T = nk), 1 (A, T = nk) or 2 (B, T = nk + 1)
+    if constexpr (TL == 2) {
+      const int64_t ld = isA ? args.lda : args.ldb;
+      const bool kc = isA ? AKC : BKC;
+      const int kadd = (int)(kc ? (int64_t)k0 * 2 : (int64_t)k0 * ld * 2);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)  // (vo[p][q] == OOB lanes stay past the record count)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? ra : rb, (lds_void*)(dst + pp_ci(p, q, wave) * 1024), 16,
+                                                 (int)vo[p][q], kadd, 0, 0);
+      return;
+    }
+    if (TL == 1 && pf && T >= nk) {  // W_dec quarter 0 (B, T = nk), 1 (A, T = nk) or 2 (B, T = nk + 1)
       const int quarter = isA ? 1 : (T == nk ? 0 : 2);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -305,7 +317,7 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
                                                (int)off, 0, 0, 0);
     }
   };
-  auto issue = [&](int p, int T) { issue_t(std::true_type{}, p, T); };
+  auto issue = [&](int p, int T) { issue_t(std::integral_constant<int, 1>{}, p, T); };
 
   // fragment lane offsets
   int kc_off[2], mn_off[4];
@@ -429,8 +441,15 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
     }
   };
   int t = 0;
-  for (; t < nk - 2; ++t) kstep(std::false_type{}, t);  // steady state: every DMA is an operand DMA
-  for (; t < nk; ++t) kstep(std::true_type{}, t);       // last two steps: DMAs past the end prefetch W_dec
+#ifndef CC_PP_SOFF
+#define CC_PP_SOFF 1
+#endif
+  // steady state: every DMA is an operand DMA
+  if (CC_PP_SOFF && K % 64 == 0)
+    for (; t < nk - 2; ++t) kstep(std::integral_constant<int, 2>{}, t);
+  else
+    for (; t < nk - 2; ++t) kstep(std::integral_constant<int, 0>{}, t);
+  for (; t < nk; ++t) kstep(std::integral_constant<int, 1>{}, t);  // last two steps: DMAs past the end prefetch W_dec
   if (wr == 0) __builtin_amdgcn_s_barrier();
   // the epilogue's column vectors fly while the last (zero-fill) DMAs drain
   const FragGeom<256> fg(args, m0, n0, wr, wc, lane);
