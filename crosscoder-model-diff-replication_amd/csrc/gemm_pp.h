@@ -181,6 +181,9 @@ CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char
   const LdsIO io(smem, qb, wr, wc, lane);
   epilogue_core<CC_BF16, EPI, 256>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, ecols, cw);
   __syncthreads();
+#ifdef CC_EXP_NOSTORE  // timing-only experiment build (never shipped): no output tile stores
+  return;
+#endif
   if (args.out) {
     const __amdgpu_buffer_rsrc_t rout = tile_rsrc(args.out, args.ldo, m0, n0, args.M, args.N, 2);
 #pragma unroll

@@ -742,6 +742,8 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
 // (8 sequential fma per lane, xor-1/2/4 butterfly) -- one HBM pass instead of Adam + a
 // transpose/norms pass.  Persistent grid over the tiles, rows fast; every element gets
 // adam_elem, so p / m / v are the bits cc_adam_step produces.
+// (64 VGPRs: one half-tile's 4 x 8 elements per thread at a time, so it fits beside a 2-wave-per-SIMD
+// ping-pong GEMM's 208)
 __global__ __launch_bounds__(256) void adam_dec_tr_kernel(const AdamArgs a, int h, int K, char* __restrict__ wt,
                                                           float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) char tile[64 * 128];
@@ -751,30 +753,23 @@ __global__ __launch_bounds__(256) void adam_dec_tr_kernel(const AdamArgs a, int 
   const int g4 = lane >> 4, i = lane & 15, q4 = i >> 2, p4 = i & 3;
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int r0 = (t % nr) * 64, c0 = (t / nr) * 64;
-    float p[2][8], g[2][8], m[2][8], v[2][8];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int idx = threadIdx.x + 256 * k, r = idx >> 3, ch = idx & 7;
-      if (r0 + r < h) {
-        const int64_t e = (int64_t)(r0 + r) * K + c0 + 8 * ch;
-        load8_nt<CC_BF16>(a.p, e, p[k]); load8_nt<CC_BF16>(a.g, e, g[k]);
-        load8_nt<CC_BF16>(a.m, e, m[k]); load8_nt<CC_BF16>(a.v, e, v[k]);
-      }
-    }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int idx = threadIdx.x + 256 * k, r = idx >> 3, ch = idx & 7;
       float qs = 0.f;
       if (r0 + r < h) {
+        float p[8], g[8], m[8], v[8];
         const int64_t e = (int64_t)(r0 + r) * K + c0 + 8 * ch;
+        load8_nt<CC_BF16>(a.p, e, p); load8_nt<CC_BF16>(a.g, e, g);
+        load8_nt<CC_BF16>(a.m, e, m); load8_nt<CC_BF16>(a.v, e, v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) adam_elem<CC_BF16>(a, coef, p[k][j], g[k][j], m[k][j], v[k][j]);
-        store8_nt<CC_BF16>(a.p, e, p[k]); store8_nt<CC_BF16>(a.m, e, m[k]); store8_nt<CC_BF16>(a.v, e, v[k]);
+        for (int j = 0; j < 8; ++j) adam_elem<CC_BF16>(a, coef, p[j], g[j], m[j], v[j]);
+        store8_nt<CC_BF16>(a.p, e, p); store8_nt<CC_BF16>(a.m, e, m); store8_nt<CC_BF16>(a.v, e, v);
         bf16x8 b;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          b[j] = (short)f2bf(p[k][j]);
-          qs = __fmaf_rn(p[k][j], p[k][j], qs);
+          b[j] = (short)f2bf(p[j]);
+          qs = __fmaf_rn(p[j], p[j], qs);
         }
         *(bf16x8*)(tile + r * 128 + ((ch ^ (r & 7)) << 4)) = b;
       }

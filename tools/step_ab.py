@@ -104,9 +104,10 @@ def main():
     g2mn = G2FromWdec(tr)
     # name -> (adam function, setup, teardown)
     variants = {"shipped": (shipped, None, None)}
-    for b in (64, 96, 128, 192, 256):
+    for b in (64, 96, 128, 192, 256, 384, 512, 768, 1024, 2048):
         variants[f"fused dec Adam {b} blocks"] = (fused_dec_adam(b), None, None)
-    variants["flat dec Adam 512 blocks"] = (flat_dec_adam(512), None, None)
+    for b in (512, 1024):
+        variants[f"flat dec Adam {b} blocks"] = (flat_dec_adam(b), None, None)
     variants["G2 from W_dec (no W_dec^T pass)"] = (shipped, g2mn.on, g2mn.off)
     if args.only:
         keep = args.only.split(",")
