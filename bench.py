@@ -199,12 +199,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 flow on a one-GPU box (never a measurement): every rank on cuda:0, gloo
+    # collectives (RCCL refuses two ranks on one device)
+    one_device = os.environ.get("CC_BENCH_ONE_DEVICE") == "1"
+    if one_device:
+        local = 0
     torch.cuda.set_device(local)
     sharded_path = world > 1 or args.force_sharded
     if sharded_path:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), rank=rank, world_size=world)
+        if one_device:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), rank=rank, world_size=world)
     config = args.config if args.config is not None else (2 if world == 1 else 3)
     B, n, d, h_total = CONFIGS[config]
     B = args.batch or B

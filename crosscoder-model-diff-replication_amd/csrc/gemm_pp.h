@@ -226,6 +226,9 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
   {
     const char* a = (const char*)args.A;
     const char* b = (const char*)args.B;
+#ifdef CC_EXP_SAMEPANEL  // timing-only experiment build (never shipped): every tile reads tile (0, 0)'s panels
+    const int m0 = 0, n0 = 0;
+#endif
     if constexpr (AKC) {
       a += (int64_t)m0 * args.lda * 2;
       ra = make_rsrc(a, (uint64_t)(M - m0) * args.lda * 2);
