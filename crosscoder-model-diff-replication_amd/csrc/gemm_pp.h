@@ -33,6 +33,9 @@
 #ifndef CC_PP_ORDER
 #define CC_PP_ORDER 1
 #endif
+#ifndef CC_PP_STAMPS_EPI  // (CC_PP_STAMPS builds) 1: stamp the epilogue's phases instead of the tile's
+#define CC_PP_STAMPS_EPI 0
+#endif
 #ifndef CC_PP_PRIO_BASE  // experiment: wave priority of the whole GEMM (vs concurrent side-stream kernels)
 #define CC_PP_PRIO_BASE 0
 #endif
@@ -157,6 +160,15 @@ template <int EPI>
 CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char* smem, const int (&qb)[4],
                             bool input_staged, int tm, int m0, int n0, int wr, int wc, int lane, int wave,
                             int wave_slot, const FragGeom<256>& fg, const EpiCols<CC_BF16, 256>& ecols) {
+#if defined(CC_EXP_NOEPI) || defined(CC_EXP_NOEPICORE)  // timing-only experiment builds (never shipped)
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+#endif
+#ifdef CC_EXP_NOEPI
+  return;
+#endif
   const int rows = args.M - m0, cols = args.N - n0, ldo = (int)args.ldo;
   const void* in = EPI == EPI_DACTS ? args.mask_src : (EPI == EPI_WGDEC && args.scale0 != 0.f ? args.w_src : nullptr);
   float cw[8][4];  // dW_dec L1-term factors (EPI_WGDEC only)
@@ -179,7 +191,13 @@ CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char
     __builtin_amdgcn_s_barrier();
   }
   const LdsIO io(smem, qb, wr, wc, lane);
+#ifndef CC_EXP_NOEPICORE
   epilogue_core<CC_BF16, EPI, 256>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, ecols, cw);
+#endif
+#if defined(CC_PP_STAMPS) && CC_PP_STAMPS_EPI
+  if (threadIdx.x == 0 && args.dbg)
+    ((uint64_t*)args.dbg)[(int64_t)args.stamp_base + (int64_t)(wave_slot / 8) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
   __syncthreads();
 #ifdef CC_EXP_NOSTORE  // timing-only experiment build (never shipped): no output tile stores
   return;
@@ -459,11 +477,13 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
   if (wr == 0) __builtin_amdgcn_s_barrier();
   // the epilogue's column vectors fly while the last (zero-fill) DMAs drain
   const FragGeom<256> fg(args, m0, n0, wr, wc, lane);
-  EpiCols<CC_BF16, 256> cols;
-  if constexpr (EPI != EPI_F32 && EPI != EPI_DEC) load_epi_cols<CC_BF16, EPI, 256>(cols, args, fg, n0);
+  EpiCols<CC_BF16, 256> evec;
+  if constexpr (EPI != EPI_F32 && EPI != EPI_DEC) load_epi_cols<CC_BF16, EPI, 256>(evec, args, fg, n0);
   wait_vmcnt<0>();
 #ifdef CC_PP_STAMPS  // diagnostic build only: per-block wall-clock timeline (100 MHz counter)
-  if (threadIdx.x == 0 && args.dbg) ((uint64_t*)args.dbg)[(int64_t)args.stamp_base + bid * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+  // (CC_PP_STAMPS_EPI: [main-loop end, epilogue core end, end, hw id] instead)
+  if (threadIdx.x == 0 && args.dbg)
+    ((uint64_t*)args.dbg)[(int64_t)args.stamp_base + bid * 4 + (CC_PP_STAMPS_EPI ? 0 : 1)] = __builtin_amdgcn_s_memrealtime();
 #endif
 
   if constexpr (EPI == EPI_SPLIT) {  // split-K partial: accumulator fragments stored as they are (1 KB each)
@@ -476,7 +496,7 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
     gemm_epilogue<CC_BF16, EPI, 256>(args, acc, tm, m0, n0, wr, wc, lane, bid * 8 + wave);
   } else {  // (the host routes N % 8 != 0 to gemm_kernel)
     __builtin_amdgcn_s_barrier();  // every wave's zero-fill DMAs landed: the LDS is free
-    pp_epilogue_lds<EPI>(args, acc, smem, qb, pf, tm, m0, n0, wr, wc, lane, wave, bid * 8 + wave, fg, cols);
+    pp_epilogue_lds<EPI>(args, acc, smem, qb, pf, tm, m0, n0, wr, wc, lane, wave, bid * 8 + wave, fg, evec);
   }
 }
 
@@ -487,7 +507,7 @@ CC_DEV void pp_stamp_end(const GemmArgs& a, int bid, uint64_t t0) {
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0 && a.dbg) {
     uint64_t* o = (uint64_t*)a.dbg + a.stamp_base + (int64_t)bid * 4;
-    o[0] = t0;
+    if (!CC_PP_STAMPS_EPI) o[0] = t0;
     o[2] = t1;
     o[3] = (uint64_t)__builtin_amdgcn_s_getreg(0xF804) | ((uint64_t)__builtin_amdgcn_s_getreg(0xF814) << 32);
   }

@@ -1,7 +1,7 @@
 """Power and clock of each step kernel run alone, back to back for ~3 s, sampled with rocm-smi in a
 background thread: tells which kernels hold the chip at its package power cap (then the clock drops
 and energy per kernel, not cycles, sets its time).  Config-2 shapes, random operands.
-Usage: python tools/kernel_power.py"""
+Usage: python tools/kernel_power.py [name-substring ...]"""
 import ctypes
 import os
 import re
@@ -63,9 +63,14 @@ def main():
         "G3 d_acts": lambda: ops.dacts_bwd_t(g_recon, W2, acts, tn, 1e-4, g_pre_t, colsum_part=parts),
         "G4+G5 wgrad": lambda: ops.wgrad_both_t(actsT, grT, W2, norms, colsum, 1e-4, gW, parts, gpT, xT, gW2, parts2, n, d),
         "adam (75M params)": lambda: ops.adam_step(P[0], P[1], P[2], P[3], coef, 5e-5, 0.9, 0.999, 1e-8, 3),
+        "hipBLASLt G1 shape (plain)": lambda: torch.matmul(x, W.t(), out=acts),
+        "ours G1 plain (bias+relu)": lambda: ops.encode_fwd(x, W, b_enc, acts, True),
         "idle": None,
     }
+    only = sys.argv[1:]
     for name, fn in cases.items():
+        if only and not any(o in name for o in only):
+            continue
         torch.cuda.synchronize()
         stop, out = threading.Event(), []
         th = threading.Thread(target=sample, args=(stop, out))

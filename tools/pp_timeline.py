@@ -1,6 +1,6 @@
 """Diagnostic: per-block wall-clock timeline of the ping-pong GEMM kernels from a CC_PP_STAMPS build
 (records [start, main-loop end, end, hw id] per block, 100 MHz s_memrealtime).
-Usage: python tools/pp_timeline.py path/to/ppstamps.so"""
+Usage: python tools/pp_timeline.py path/to/ppstamps.so [case-substring ...]"""
 import ctypes
 import os
 import sys
@@ -104,7 +104,14 @@ def main():
     cases["G4+G5 dual (KC/KC, batch-contiguous operands)"] = (
         lambda: L.cc_wgrad_both_t(P(aT), P(grT), P(W), P(norms), P(colsum), 1e-4, P(gW), P(parts), P(gpT), P(xT),
                                   P(gW2), P(parts2), B, h, n, d, 1, st), (h // 256) * (K // 256))
+    aT2 = torch.empty(h, B, device=dev, dtype=bf)
+    cases["G1 encode + acts^T (as in the step)"] = (
+        lambda: L.cc_encode_fwd_t(P(x), P(W), P(b_enc), P(tn), P(acts), P(aT2), 1, P(parts), P(parts), P(parts), B, K,
+                                  h, 1, st), None)
+    only = sys.argv[2:]
     for name, (fn, nb0) in cases.items():
+        if only and not any(o in name for o in only):
+            continue
         for _ in range(20):  # warm clocks
             assert fn() == 0
         buf.zero_()
