@@ -113,6 +113,16 @@ CC_DEV float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// sum over each aligned group of 16 lanes (a DPP row), the same bits as the xor-1/2/4/8 butterfly
+// (every lane gets the sum); DPP moves instead of ds_bpermute: no LDS round trips.  xor 4 / xor 8
+// become row_half_mirror / row_mirror, which pair the same quads / half-rows.  EXEC must be full.
+CC_DEV float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
 // sum over each aligned group of 8 lanes (xor-1/2/4 butterfly: every lane of the group gets the
 // same bits)
 CC_DEV float block8_sum(float v) {

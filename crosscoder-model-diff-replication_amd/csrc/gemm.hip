@@ -677,6 +677,9 @@ static int launch(GemmArgs a, hipStream_t st) {
   return CC_OK;
 }
 
+#ifndef CC_PP_FAST  // the epilogue fast form for whole-tile ReLU launches (0: general form, A/B)
+#define CC_PP_FAST 1
+#endif
 template <bool AKC, bool BKC, int EPI>
 static int launch_pp(GemmArgs a, hipStream_t st) {
 #ifdef CC_PP_STAMPS
@@ -684,6 +687,13 @@ static int launch_pp(GemmArgs a, hipStream_t st) {
 #endif
   a.nbm = (a.M + BM - 1) / BM;
   a.nbn = (a.N + 255) / 256;
+  if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
+    if (CC_PP_FAST && a.M % BM == 0 && a.N % 256 == 0 && (EPI == EPI_DACTS || a.flag)) {  // whole tiles, ReLU on
+      hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI, true>), dim3(a.nbm * a.nbn), dim3(NTHR), 0, st, a);
+      CC_LAUNCH_CHECK();
+      return CC_OK;
+    }
+  }
   hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI>), dim3(a.nbm * a.nbn), dim3(NTHR), 0, st, a);
   CC_LAUNCH_CHECK();
   return CC_OK;

@@ -14,6 +14,10 @@
 //            transfers.
 // N % 4 == 0 (host check): a lane's 4 columns are all in range or all out.
 
+#ifndef CC_EPI_DPP  // column sums of the epilogue by DPP row reductions (0: ds_bpermute shuffles, A/B)
+#define CC_EPI_DPP 1
+#endif
+
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
@@ -85,6 +89,9 @@ struct RegIO {
   }
   CC_DEV typename V4<DT>::T in4(int i, int j) const { return bld4<DT>(rin, fg.boff(i, j, ES)); }
   CC_DEV void out4(int i, int j, const float v[4]) const { bst4<DT>(rout, fg.boff(i, j, ES), v); }
+  CC_DEV void out4p(int i, int j, bf16x4 p) const {  // (bf16 only) already-converted outputs
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, p), rout, (int)fg.boff(i, j, 2), 0, 0);
+  }
 };
 
 // Per-fragment factor of dW_dec's L1 term: (l1_scale * sum_b acts[b, row]) * (1 / ||W_dec[row, model]||),
@@ -140,10 +147,107 @@ CC_DEV void load_epi_cols(EpiCols<DT, BNT>& c, const GemmArgs& args, const FragG
   if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) c.load(args, fg, n0, EPI == EPI_ENC && args.bias);
 }
 
+// EPI_ENC / EPI_DACTS element-wise part (see epilogue_core).  FAST (bf16): every fragment in range, ReLU on.
+template <int DT, int EPI, int BNT, bool FAST, class IO>
+CC_DEV void enc_dacts_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN],
+                           const FragGeom<BNT>& fg, const IO& io, int tm, int n0, int wr, int lane, int wave_slot,
+                           const EpiCols<DT, BNT>& cols) {
+#pragma clang fp contract(off)  // (acc + tn * l1_scale: two roundings in every variant; the l1 sum fuses)
+  using E = Elem<DT>;
+  using WG = WaveGeom<BNT>;
+  const int N = args.N;
+  constexpr int JB = EPB<DT, BNT>::JB_M;
+  float s_l1 = 0.f, s_l0 = 0.f;
+  int l0i = 0;  // FAST: this lane's count of positive outputs
+  typename V4<DT>::T mraw[EPI == EPI_DACTS ? WG::TM : 1][JB];
+#pragma unroll
+  for (int j = 0; j < WG::TN; ++j) {
+    if constexpr (EPI == EPI_DACTS) {
+      if (j % JB == 0) {  // the mask vectors of JB column groups, all in flight together
+#pragma unroll
+        for (int jj = 0; jj < JB; ++jj)
+#pragma unroll
+          for (int i = 0; i < WG::TM; ++i) mraw[i][jj] = io.in4(i, j + jj);
+      }
+    }
+    float add[4], tnc[4], csum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if constexpr (EPI == EPI_ENC) {
+        add[e] = V4<DT>::get(cols.bias[j], e);
+        tnc[e] = cols.tn[j][e];
+      } else {
+        add[e] = cols.tn[j][e] * args.scale0;
+        tnc[e] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < WG::TM; ++i) {
+      const bool ok = FAST || fg.ok(i, j);
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = acc[i][j][e] + add[e];
+        if constexpr (EPI == EPI_ENC) {
+          if (FAST || args.flag) t = fmaxf(t, 0.f);
+        } else {
+          t = V4<DT>::get(mraw[i][j % JB], e) > 0.f ? t : 0.f;
+        }
+        v[e] = FAST ? t : (ok ? E::round(t) : 0.f);
+      }
+      if constexpr (FAST) {
+        const bf16x4 p = pack4<CC_BF16>(v);  // the bf16 rounding, once
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = V4<CC_BF16>::get(p, e);
+        io.out4p(i, j, p);
+      } else {
+        io.out4(i, j, v);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        csum[e] += v[e];
+        if constexpr (EPI == EPI_ENC) {
+          s_l1 = __builtin_fmaf(v[e], tnc[e], s_l1);
+          if constexpr (FAST) l0i += v[e] > 0.f;
+          else s_l0 += v[e] > 0.f ? 1.f : 0.f;
+        }
+      }
+    }
+    if (args.col_part) {  // reduce over the 16 lanes (rows) that share these 4 columns
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#if CC_EPI_DPP
+        csum[e] = row16_sum(csum[e]);
+#else
+        float s = csum[e];
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        s += __shfl_xor(s, 4, 64);
+        s += __shfl_xor(s, 8, 64);
+        csum[e] = s;
+#endif
+      }
+      if ((lane & 15) == 0 && fg.cv[j])
+        st4<CC_F32>(args.col_part, (int64_t)(tm * WG::WARPS_M + wr) * N + n0 + fg.c0 + 16 * j, csum);
+    }
+  }
+  if constexpr (EPI == EPI_ENC) {
+    if (args.wave_part0) {
+      float t = wave_sum(s_l1);
+      if (lane == 0) args.wave_part0[wave_slot] = t;
+    }
+    if (args.wave_part1) {
+      // (integer-valued floats below 2^24: the per-lane counts sum exactly either way)
+      float t = wave_sum(FAST ? (float)l0i : s_l0);
+      if (lane == 0) args.wave_part1[wave_slot] = t;
+    }
+  }
+}
+
 // cols: EpiCols loaded by the caller (EPI_ENC / EPI_DACTS; otherwise unread).
 // cw: dW_dec L1-term factors loaded by the caller (wgdec_factors; EPI_WGDEC with l1_scale != 0
 // only, otherwise unread).  Passed by reference so they stay in registers.
-template <int DT, int EPI, int BNT, class IO>
+template <int DT, int EPI, int BNT, bool FAST = false, class IO>
 CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN],
                           const FragGeom<BNT>& fg, const IO& io, int tm, int m0, int n0, int wr, int lane,
                           int wave_slot, const EpiCols<DT, BNT>& cols,
@@ -152,75 +256,10 @@ CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
   using WG = WaveGeom<BNT>;
   const int N = args.N;
   if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
-    constexpr int JB = EPB<DT, BNT>::JB_M;
-    float s_l1 = 0.f, s_l0 = 0.f;
-    typename V4<DT>::T mraw[EPI == EPI_DACTS ? WG::TM : 1][JB];
-#pragma unroll
-    for (int j = 0; j < WG::TN; ++j) {
-      if constexpr (EPI == EPI_DACTS) {
-        if (j % JB == 0) {  // the mask vectors of JB column groups, all in flight together
-#pragma unroll
-          for (int jj = 0; jj < JB; ++jj)
-#pragma unroll
-            for (int i = 0; i < WG::TM; ++i) mraw[i][jj] = io.in4(i, j + jj);
-        }
-      }
-      float add[4], tnc[4], csum[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if constexpr (EPI == EPI_ENC) {
-          add[e] = V4<DT>::get(cols.bias[j], e);
-          tnc[e] = cols.tn[j][e];
-        } else {
-          add[e] = cols.tn[j][e] * args.scale0;
-          tnc[e] = 0.f;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < WG::TM; ++i) {
-        const bool ok = fg.ok(i, j);
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float t = acc[i][j][e] + add[e];
-          if constexpr (EPI == EPI_ENC) {
-            if (args.flag) t = fmaxf(t, 0.f);
-          } else {
-            t = V4<DT>::get(mraw[i][j % JB], e) > 0.f ? t : 0.f;
-          }
-          v[e] = ok ? E::round(t) : 0.f;
-          csum[e] += v[e];
-          if constexpr (EPI == EPI_ENC) {
-            s_l1 += v[e] * tnc[e];
-            s_l0 += v[e] > 0.f ? 1.f : 0.f;
-          }
-        }
-        io.out4(i, j, v);
-      }
-      if (args.col_part) {  // reduce over the 16 lanes (rows) that share these 4 columns
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float s = csum[e];
-          s += __shfl_xor(s, 1, 64);
-          s += __shfl_xor(s, 2, 64);
-          s += __shfl_xor(s, 4, 64);
-          s += __shfl_xor(s, 8, 64);
-          csum[e] = s;
-        }
-        if ((lane & 15) == 0 && fg.cv[j])
-          st4<CC_F32>(args.col_part, (int64_t)(tm * WG::WARPS_M + wr) * N + n0 + fg.c0 + 16 * j, csum);
-      }
-    }
-    if constexpr (EPI == EPI_ENC) {
-      if (args.wave_part0) {
-        float t = wave_sum(s_l1);
-        if (lane == 0) args.wave_part0[wave_slot] = t;
-      }
-      if (args.wave_part1) {
-        float t = wave_sum(s_l0);
-        if (lane == 0) args.wave_part1[wave_slot] = t;
-      }
-    }
+    // FAST (a kernel variant the host picks when every tile lies inside the matrix and the ReLU is on,
+    // as in the step's G1 / G3): no range selects, one bf16 conversion per output, an integer l0
+    // count.  Same bits as the general form.
+    enc_dacts_core<DT, EPI, BNT, FAST && DT == CC_BF16>(args, acc, fg, io, tm, n0, wr, lane, wave_slot, cols);
   } else if constexpr (EPI == EPI_WGDEC || EPI == EPI_WGENC) {
     constexpr int JB = EPB<DT, BNT>::JB_W;
     const bool l1term = EPI == EPI_WGDEC && args.scale0 != 0.f;

@@ -113,6 +113,7 @@ struct LdsIO {
   CC_DEV char* at(int i, int j) const { return (i < 4 ? lo : hi) + off[j] + (i & 3) * 16 * 512; }
   CC_DEV bf16x4 in4(int i, int j) const { return *(const bf16x4*)at(i, j); }
   CC_DEV void out4(int i, int j, const float v[4]) const { *(bf16x4*)at(i, j) = pack4<CC_BF16>(v); }
+  CC_DEV void out4p(int i, int j, bf16x4 p) const { *(bf16x4*)at(i, j) = p; }
 };
 
 // Source/destination offset (bytes, in a tile-anchored descriptor) of this lane's 16 B of 1-KB
@@ -156,7 +157,7 @@ CC_DEV void pp_store_transposed(const GemmArgs& args, const char* smem, const in
   }
 }
 
-template <int EPI>
+template <int EPI, bool FAST>
 CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char* smem, const int (&qb)[4],
                             bool input_staged, int tm, int m0, int n0, int wr, int wc, int lane, int wave,
                             int wave_slot, const FragGeom<256>& fg, const EpiCols<CC_BF16, 256>& ecols) {
@@ -192,7 +193,7 @@ CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char
   }
   const LdsIO io(smem, qb, wr, wc, lane);
 #ifndef CC_EXP_NOEPICORE
-  epilogue_core<CC_BF16, EPI, 256>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, ecols, cw);
+  epilogue_core<CC_BF16, EPI, 256, FAST>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, ecols, cw);
 #endif
 #if defined(CC_PP_STAMPS) && CC_PP_STAMPS_EPI
   if (threadIdx.x == 0 && args.dbg)
@@ -223,8 +224,9 @@ constexpr int PP_LDS_W = PP_LDS + 256 * 128;
 constexpr int PP_LDS_W = PP_LDS;
 #endif
 
-// One output tile of one GEMM; bid = the tile's block index within that GEMM's grid.
-template <bool AKC, bool BKC, int EPI>
+// One output tile of one GEMM; bid = the tile's block index within that GEMM's grid.  FAST: every tile
+// of the launch lies inside the matrix and the ReLU is on (EPI_ENC / EPI_DACTS epilogue fast form).
+template <bool AKC, bool BKC, int EPI, bool FAST = false>
 CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
   using WG = WaveGeom<256>;
   static_assert(WG::TM == 8 && WG::TN == 4, "ping-pong geometry");
@@ -496,7 +498,7 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
     gemm_epilogue<CC_BF16, EPI, 256>(args, acc, tm, m0, n0, wr, wc, lane, bid * 8 + wave);
   } else {  // (the host routes N % 8 != 0 to gemm_kernel)
     __builtin_amdgcn_s_barrier();  // every wave's zero-fill DMAs landed: the LDS is free
-    pp_epilogue_lds<EPI>(args, acc, smem, qb, pf, tm, m0, n0, wr, wc, lane, wave, bid * 8 + wave, fg, evec);
+    pp_epilogue_lds<EPI, FAST>(args, acc, smem, qb, pf, tm, m0, n0, wr, wc, lane, wave, bid * 8 + wave, fg, evec);
   }
 }
 
@@ -514,13 +516,13 @@ CC_DEV void pp_stamp_end(const GemmArgs& a, int bid, uint64_t t0) {
 }
 #endif
 
-template <bool AKC, bool BKC, int EPI>
+template <bool AKC, bool BKC, int EPI, bool FAST = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(16))) char smem[EPI == EPI_WGDEC ? PP_LDS_W : PP_LDS];
 #ifdef CC_PP_STAMPS
   const uint64_t t0 = pp_stamp_start();
 #endif
-  pp_tile<AKC, BKC, EPI>(args, smem, blockIdx.x);
+  pp_tile<AKC, BKC, EPI, FAST>(args, smem, blockIdx.x);
 #ifdef CC_PP_STAMPS
   pp_stamp_end(args, blockIdx.x, t0);
 #endif
