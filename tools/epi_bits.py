@@ -47,9 +47,17 @@ def main():
         gpT = torch.empty(h, B, device=dev, dtype=bf)
         colp3 = torch.zeros(1 << 20, device=dev)
         assert L.cc_dacts_bwd_t(P(g_recon), P(W), P(acts), P(tn), 1e-4, P(gpT), B, P(colp3), B, K, h, 1, st) == 0
+        norms = torch.rand(h, n, device=dev, generator=torch.Generator(device=dev).manual_seed(1)) + 0.5
+        colsum = torch.rand(h, device=dev, generator=torch.Generator(device=dev).manual_seed(2))
+        gW, gW2 = torch.empty(h, K, device=dev, dtype=bf), torch.empty(h, K, device=dev, dtype=bf)
+        sq1, sq2 = torch.zeros(1 << 20, device=dev), torch.zeros(1 << 20, device=dev)
+        grT, xT = g_recon.t().contiguous(), x.t().contiguous()
+        assert L.cc_wgrad_both_t(P(actsT), P(grT), P(W), P(norms), P(colsum), 1e-4, P(gW), P(sq1), P(gpT), P(xT),
+                                 P(gW2), P(sq2), B, h, n, d, 1, st) == 0
         torch.cuda.synchronize()
-        outs.append((acts, actsT, colp, l1p, l0p, gpT, colp3))
-    names = ["acts", "acts^T", "G1 colsum partials", "l1 partials", "l0 partials", "g_pre^T", "G3 colsum partials"]
+        outs.append((acts, actsT, colp, l1p, l0p, gpT, colp3, gW, sq1, gW2, sq2))
+    names = ["acts", "acts^T", "G1 colsum partials", "l1 partials", "l0 partials", "g_pre^T", "G3 colsum partials",
+             "dW_dec", "dW_dec sq partials", "dW_enc", "dW_enc sq partials"]
     for nm, a, b in zip(names, outs[0], outs[1]):
         same = torch.equal(a.view(torch.int16) if a.dtype == bf else a.view(torch.int32),
                            b.view(torch.int16) if b.dtype == bf else b.view(torch.int32))
