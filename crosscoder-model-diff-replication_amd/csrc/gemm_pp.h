@@ -519,8 +519,11 @@ CC_DEV void pp_stamp_end(const GemmArgs& a, int bid, uint64_t t0) {
 template <bool AKC, bool BKC, int EPI, bool FAST = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(16))) char smem[EPI == EPI_WGDEC ? PP_LDS_W : PP_LDS];
-#ifdef CC_EXP_STAGGER  // timing-only experiment build (never shipped): odd first-round blocks start ~CC_EXP_STAGGER x 4 us late
-  if ((blockIdx.x & 1) && blockIdx.x < 256)
+#ifdef CC_EXP_STAGGER  // timing-only experiment build (never shipped): half the first-round blocks start ~CC_EXP_STAGGER x 4 us
+#ifndef CC_EXP_STAGGER_XCD  // late: every other block of each XCD (0), or the odd XCDs' blocks (1)
+#define CC_EXP_STAGGER_XCD 0
+#endif
+  if ((CC_EXP_STAGGER_XCD ? (blockIdx.x & 1) : ((blockIdx.x >> 3) & 1)) && blockIdx.x < 256)
     for (int i = 0; i < CC_EXP_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
 #endif
 #ifdef CC_PP_STAMPS
