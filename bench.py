@@ -77,8 +77,8 @@ class EventTimer:
 SPAN_EVERY = 4  # timed steps per roofline-kernel sample (events around the launch)
 
 # span name -> kernel-name prefix in the rocprofv3 traces
-SPAN_KERNEL = {"G1_encode": "gemm_pp_kernel<true, true, 1>", "G2_decode": "gemm_pp_kernel<true, false, 2>",
-               "G3_dacts": "gemm_pp_kernel<true, true, 3>", "G4G5_wgrad": "gemm_pp_dual_kernel<true, true, 4, 5>",
+SPAN_KERNEL = {"G1_encode": "gemm_pp_kernel<true, true, 1", "G2_decode": "gemm_pp_kernel<true, false, 2",
+               "G3_dacts": "gemm_pp_kernel<true, true, 3", "G4G5_wgrad": "gemm_pp_dual_kernel<true, true, 4, 5>",
                "adam": "adam_bulk_kernel"}
 
 

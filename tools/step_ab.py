@@ -36,6 +36,31 @@ def fused_dec_adam(blocks):
     return adam
 
 
+def serial_adam(norms_beside):
+    """The whole Adam as one flat launch on the main stream (no decoder half beside G1); the next step's
+    W_dec^T + decoder norms then either on the side stream beside prep / G1 (norms_beside) or on the main
+    stream before G2 (forward's decoder_norms)."""
+    from crosscoder_amd import engine
+
+    def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None):
+        coef = ws.clip_out[0:1]
+        from crosscoder_amd import ops
+        with engine._span("adam"):
+            ops.adam_step(P.data, G.data, M.data, V.data, coef, lr, beta1, beta2, eps, step)
+        if not norms_beside:
+            return
+        dev = P.data.device
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side_stream):
+            side_stream.wait_event(ev)
+            engine.norms_for_next(ws, P)
+            done = torch.cuda.Event()
+            done.record(side_stream)
+        P.pending = done
+    return adam
+
+
 def flat_dec_adam(blocks):
     from crosscoder_amd import engine
 
@@ -108,6 +133,8 @@ def main():
         variants[f"fused dec Adam {b} blocks"] = (fused_dec_adam(b), None, None)
     for b in (512, 1024):
         variants[f"flat dec Adam {b} blocks"] = (flat_dec_adam(b), None, None)
+    variants["serial Adam + norms beside G1"] = (serial_adam(True), None, None)
+    variants["serial Adam + norms before G2"] = (serial_adam(False), None, None)
     variants["G2 from W_dec (no W_dec^T pass)"] = (shipped, g2mn.on, g2mn.off)
     if args.only:
         keep = args.only.split(",")
