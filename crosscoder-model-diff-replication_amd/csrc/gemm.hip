@@ -680,6 +680,8 @@ static int launch(GemmArgs a, hipStream_t st) {
 #ifndef CC_PP_FAST  // the epilogue fast form for whole-tile ReLU launches (0: general form, A/B)
 #define CC_PP_FAST 1
 #endif
+static int g_pp_fast = CC_PP_FAST;  // cc_debug_set_pp_fast: in-process check that both forms give the same bits
+extern "C" void cc_debug_set_pp_fast(int on) { g_pp_fast = on; }
 template <bool AKC, bool BKC, int EPI>
 static int launch_pp(GemmArgs a, hipStream_t st) {
 #ifdef CC_PP_STAMPS
@@ -688,7 +690,7 @@ static int launch_pp(GemmArgs a, hipStream_t st) {
   a.nbm = (a.M + BM - 1) / BM;
   a.nbn = (a.N + 255) / 256;
   if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
-    if (CC_PP_FAST && a.M % BM == 0 && a.N % 256 == 0 && (EPI == EPI_DACTS || a.flag)) {  // whole tiles, ReLU on
+    if (g_pp_fast && a.M % BM == 0 && a.N % 256 == 0 && (EPI == EPI_DACTS || a.flag)) {  // whole tiles, ReLU on
       hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI, true>), dim3(a.nbm * a.nbn), dim3(NTHR), 0, st, a);
       CC_LAUNCH_CHECK();
       return CC_OK;

@@ -712,6 +712,42 @@ def test_decode_split_schedule(gpu, shape):
         assert torch.equal(r_split[:, :col0], r_one[:, :col0])
 
 
+@pytest.mark.parametrize("B,h,K", [(512, 512, 256), (4096, 16384, 4608)])
+def test_whole_tile_epilogue_matches_general_form(gpu, B, h, K):
+    """G1 / G3 on whole 256 x 256 tiles with the ReLU on take the epilogue's fast kernel form (no range
+    selects, one bf16 conversion, integer l0 count): every output and partial slab bit-identical to the
+    general form (cc_debug_set_pp_fast(0)), which partial tiles use."""
+    g = torch.Generator().manual_seed(11)
+    bf = torch.bfloat16
+    x = torch.randn(B, K, generator=g).to(bf).to(gpu)
+    W = (torch.randn(h, K, generator=g) * 0.05).to(bf).to(gpu)
+    b_enc = (torch.randn(h, generator=g) * 0.1).to(bf).to(gpu)
+    tn = torch.rand(h, generator=g).to(gpu)
+    g_recon = (torch.randn(B, K, generator=g) * 1e-3).to(bf).to(gpu)
+    lib = ops.lib()
+
+    def run():
+        acts, acts_t = torch.empty(B, h, device=gpu, dtype=bf), torch.empty(h, B, device=gpu, dtype=bf)
+        colp = torch.zeros(ops.col_part_rows(B), h, device=gpu)
+        l0p = torch.zeros(1 << 16, device=gpu)
+        ops.encode_fwd_t(x, W, b_enc, acts, acts_t, True, colsum_part=colp, l0_part=l0p)
+        gp_t = torch.empty(h, B, device=gpu, dtype=bf)
+        colp3 = torch.zeros(ops.col_part_rows(B), h, device=gpu)
+        ops.dacts_bwd_t(g_recon, W, acts, tn, 1e-4, gp_t, colsum_part=colp3)
+        torch.cuda.synchronize()
+        return acts, acts_t, colp, l0p, gp_t, colp3
+
+    fast = run()
+    lib.cc_debug_set_pp_fast(0)
+    try:
+        general = run()
+    finally:
+        lib.cc_debug_set_pp_fast(1)
+    for a, b in zip(fast, general):
+        assert torch.equal(a.view(torch.int16) if a.dtype == bf else a, b.view(torch.int16) if b.dtype == bf else b)
+    assert fast[0].float().max() > 0 and (fast[4] != 0).any()
+
+
 # ----------------------------------------------------------------------------- around the step (§8f)
 def test_buffer_matches_reference_with_fake_lms(gpu):
     """Buffer (buffer.py:12-125) with deterministic fake LMs: normalisation factors and every next()

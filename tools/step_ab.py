@@ -61,6 +61,21 @@ def serial_adam(norms_beside):
     return adam
 
 
+class NoLoss:
+    """Timing-only variant: the loss kernel skipped (g_recon keeps the last values): the upper bound of what
+    folding the loss into G2's epilogue could save."""
+
+    def __init__(self):
+        from crosscoder_amd import engine
+        self.engine, self.saved = engine, engine.loss_rows
+
+    def on(self):
+        self.engine.loss_rows = lambda *a, **k: None
+
+    def off(self):
+        self.engine.loss_rows = self.saved
+
+
 def flat_dec_adam(blocks):
     from crosscoder_amd import engine
 
@@ -133,6 +148,8 @@ def main():
         variants[f"fused dec Adam {b} blocks"] = (fused_dec_adam(b), None, None)
     for b in (512, 1024):
         variants[f"flat dec Adam {b} blocks"] = (flat_dec_adam(b), None, None)
+    nl = NoLoss()
+    variants["no loss kernel (timing only)"] = (shipped, nl.on, nl.off)
     variants["serial Adam + norms beside G1"] = (serial_adam(True), None, None)
     variants["serial Adam + norms before G2"] = (serial_adam(False), None, None)
     variants["G2 from W_dec (no W_dec^T pass)"] = (shipped, g2mn.on, g2mn.off)
