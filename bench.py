@@ -192,6 +192,10 @@ def main():
     ap.add_argument("--d-model", type=int)
     ap.add_argument("--dict-size", type=int, help="the WHOLE dictionary (split over the ranks when N > 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--comm", choices=("all_reduce", "reduce_scatter"), default="all_reduce",
+                    help="latent-sharded step: the partial-reconstruction exchange")
+    ap.add_argument("--recon-chunks", type=int, default=None,
+                    help="latent-sharded step: batch slices the exchange is overlapped by (default 4)")
     ap.add_argument("--force-sharded", action="store_true",
                     help="diagnostic: run the latent-sharded step even on one rank (1-rank RCCL group)")
     args = ap.parse_args()
@@ -232,7 +236,7 @@ def main():
         from crosscoder_amd import sharded
 
         buf = ca.SyntheticBuffer(cfg, rows=B * 8, n_models=n, seed=0)  # same seed on every rank: replicated batch
-        tr = sharded.ShardedTrainer(cfg, buffer=buf)
+        tr = sharded.ShardedTrainer(cfg, buffer=buf, comm=args.comm, recon_chunks=args.recon_chunks)
 
     timer = EventTimer()
     engine.TIMER = timer
