@@ -61,6 +61,28 @@ def serial_adam(norms_beside):
     return adam
 
 
+def dec_adam_side_norms_main():
+    """Decoder-half Adam on the side stream as shipped, but W_dec^T + the decoder norms on the main stream
+    before G2 (forward's decoder_norms), after the wait for the side stream."""
+    from crosscoder_amd import engine, ops
+
+    def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None):
+        coef = ws.clip_out[0:1]
+        dev = P.data.device
+        with engine._span("adam"):
+            ops.adam_step(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), coef, lr, beta1, beta2, eps, step)
+        enc_done = torch.cuda.Event()
+        enc_done.record(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side_stream):
+            side_stream.wait_event(enc_done)
+            ops.adam_step(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), coef, lr, beta1, beta2, eps, step,
+                          max_blocks=engine.DEC_ADAM_BLOCKS)
+            done = torch.cuda.Event()
+            done.record(side_stream)
+        P.pending = done
+    return adam
+
+
 class NoLoss:
     """Timing-only variant: the loss kernel skipped (g_recon keeps the last values): the upper bound of what
     folding the loss into G2's epilogue could save."""
@@ -148,6 +170,7 @@ def main():
         variants[f"fused dec Adam {b} blocks"] = (fused_dec_adam(b), None, None)
     for b in (512, 1024):
         variants[f"flat dec Adam {b} blocks"] = (flat_dec_adam(b), None, None)
+    variants["dec Adam beside G1 + norms on main"] = (dec_adam_side_norms_main(), None, None)
     nl = NoLoss()
     variants["no loss kernel (timing only)"] = (shipped, nl.on, nl.off)
     variants["serial Adam + norms beside G1"] = (serial_adam(True), None, None)
