@@ -63,6 +63,12 @@ SIGNATURES = {
                                _p, _p]),
     "cc_loss_tail": (_i, [_p, _i64, _i64, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _i64,
                           _i64, _i64, _p, _p]),
+    "cc_loss_tail_nb": (_i, [_p, _i64, _i64, _p, _p, _p, _p, _i64, _p, _i64, _p, _p, _p, _p, _p, _p, ctypes.c_uint32,
+                             _i64, _i64, _i64, _p, _p]),
+    "cc_loss_finalize_nb": (_i, [_p, _i64, _p, _i64, _p, _i64, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _i64, _i64,
+                                 _i64, _p]),
+    "cc_decode_loss_ncb": (_i64, [_i64, _i64, _i64, _i64, _i]),
+    "cc_decode_loss_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_transposed_ok": (_i, [_i64, _i64, _i64, _i]),
     "cc_encode_fwd_t": (_i, [_p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_dacts_bwd_t": (_i, [_p, _p, _p, _p, _f, _p, _i64, _p, _i64, _i64, _i64, _i, _p]),

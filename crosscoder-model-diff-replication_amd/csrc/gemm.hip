@@ -32,7 +32,7 @@ constexpr int BM = 256, NTHR = 512;
 constexpr uint32_t OOB = 0x7ffffff0u;  // voffset that the range check always rejects
 constexpr uint32_t MAX_RECORDS = 0x7fffffe0u;
 
-enum Epi { EPI_F32 = 0, EPI_ENC = 1, EPI_DEC = 2, EPI_DACTS = 3, EPI_WGDEC = 4, EPI_WGENC = 5, EPI_SPLIT = 6 };
+enum Epi { EPI_F32 = 0, EPI_ENC = 1, EPI_DEC = 2, EPI_DACTS = 3, EPI_WGDEC = 4, EPI_WGENC = 5, EPI_SPLIT = 6, EPI_DLOSS = 7 };
 
 struct GemmArgs {
   const void* A;
@@ -60,6 +60,7 @@ struct GemmArgs {
   int k_step0, k_steps; // ping-pong split-K: contraction steps [k_step0, k_step0 + k_steps) (0 steps: all)
   void* out_t;          // ping-pong bf16 epilogue: also store the tile transposed, out_t[n][m] (ld ldt)
   int64_t ldt;
+  float* row_part;      // EPI_DLOSS: loss row terms [2][n * d/64][M]
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -852,9 +853,8 @@ __global__ __launch_bounds__(256) void reduce_splits_kernel(const float* __restr
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= (int64_t)nbm * nbn * 8 * 32 * 64) return;
   const int lane = (int)(t & 63), f = (int)((t >> 6) & 31), wave = (int)((t >> 11) & 7);
-  const int tile = (int)(t >> 14);
-  int tm, tn;
-  tile_of_block(tile, nbm, nbn, tm, tn);
+  const int tile = (int)(t >> 14);  // slab tile index tm * nbn + tn (EPI_SPLIT)
+  const int tm = tile / nbn, tn = tile - tm * nbn;
   const int row = tm * BM + (wave >> 2) * 128 + 16 * (f >> 2) + (lane & 15);
   const int col = tn * 256 + (wave & 3) * 64 + 16 * (f & 3) + 4 * (lane >> 4);
   if (row >= M || col >= N) return;
@@ -956,6 +956,170 @@ int cc_decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, floa
 int cc_decode_fwd_ws_t(const void* acts, const void* W_dec_t, float* recon_f32, float* ws, int64_t ws_floats,
                        int64_t B, int64_t h, int64_t K, int dtype, void* stream) {
   return decode_fwd_ws<true>(acts, W_dec_t, recon_f32, ws, ws_floats, B, h, K, dtype, (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+// ---- G2 + the reconstruction loss in one pass (bf16) ----
+// The whole-contraction tiles run the loss as their epilogue (EPI_DLOSS: the fp32 reconstruction never
+// reaches HBM); the split-K leftover columns are summed here in the fixed order of reduce_splits_kernel
+// and run the same per-element arithmetic (loss_kernel's): g_recon is bit-identical to decode + loss.
+// Block: 128 rows x 64 columns of the leftover region (tail-relative column ct0 = 64 * blockIdx.x), 16
+// waves: lane -> 8 columns (lane & 7) of row 8 * wave + (lane >> 3).  Row terms per 64-column block
+// (row_part[2][n * d/64][B]), column sums of g_recon per 128-row group (col_part[B/128][K]), g_recon^T
+// through an LDS tile.  B % 8 == 0, d % 64 == 0.
+struct LossSplitArgs {
+  const float* part;
+  int S, t_nbn, col0, B, K, n, d;
+  int64_t split_stride;
+  const bf16_t* b_dec;
+  const bf16_t* x;
+  const float* x_mean;
+  float gs;
+  bf16_t* g_recon;
+  bf16_t* g_t;
+  float* row_part;
+  float* col_part;
+};
+constexpr int LSPLIT_THREADS = 1024;
+__global__ __launch_bounds__(LSPLIT_THREADS) void loss_split_kernel(const LossSplitArgs a) {
+  constexpr int TP = 128 + 8;  // padded LDS row (rows of one column of the transposed tile)
+  constexpr int NW = LSPLIT_THREADS / 64;
+  __shared__ __attribute__((aligned(16))) bf16_t tt[64 * TP];
+  __shared__ float red[NW][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cq = lane & 7;
+  const int ct = blockIdx.x * 64 + cq * 8;  // tail-relative column of this lane's 8
+  const int c = a.col0 + ct;                // global column
+  const int r0 = blockIdx.y * 128;
+  const int cblk = a.col0 + blockIdx.x * 64;
+  const int m = cblk / a.d, ncb = a.d / 64, cb = (cblk - m * a.d) / 64;
+  const int rl = w * 8 + (lane >> 3);
+  const int r = r0 + rl;
+  float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (r0 + w * 8 < a.B) {  // wave-uniform (B % 8 == 0)
+    // slab coordinates of (r, ct): tile (tm, tn), wave, fragment (i, j), lane (lr + 16 lg)
+    const int tn = ct >> 8, cc2 = ct & 255;
+    const int tm = r >> 8, rr2 = r & 255;
+    const int wave = (rr2 >> 7) * 4 + (cc2 >> 6), i = (rr2 & 127) >> 4, j = (cc2 & 63) >> 4;
+    const int lr = rr2 & 15, lg = (cc2 & 15) >> 2;
+    const int64_t off = ((int64_t)(tm * a.t_nbn + tn) * 8 + wave) * 8192 + ((i * 4 + j) * 64 + lr + 16 * lg) * 4;
+    float bd[8], mu[8], xv[8];
+    load8<CC_BF16>(a.b_dec, c, bd);
+    load8f(a.x_mean, c, mu);
+    load8<CC_BF16>(a.x, (int64_t)r * a.K + c, xv);
+    f32x4 u = *(const f32x4*)(a.part + off), v = *(const f32x4*)(a.part + off + 64);
+    for (int s = 1; s < a.S; ++s) {  // reduce_splits' order
+      u += *(const f32x4*)(a.part + s * a.split_stride + off);
+      v += *(const f32x4*)(a.part + s * a.split_stride + off + 64);
+    }
+    float l2 = 0.f, tv = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float rv = e < 4 ? u[e] : v[e - 4];
+      const float diff = (rv + bd[e]) - xv[e];
+      l2 += diff * diff;
+      const float q = xv[e] - mu[e];
+      tv += q * q;
+      g[e] = Elem<CC_BF16>::round(a.gs * diff);
+      tt[(cq * 8 + e) * TP + rl] = f2bf(g[e]);
+    }
+    store8<CC_BF16>(a.g_recon, (int64_t)r * a.K + c, g);
+    l2 = block8_sum(l2);
+    tv = block8_sum(tv);
+    if (cq == 0) {
+      const int64_t plane = (int64_t)a.n * ncb * a.B;
+      a.row_part[(int64_t)(m * ncb + cb) * a.B + r] = l2;
+      a.row_part[plane + (int64_t)(m * ncb + cb) * a.B + r] = tv;
+    }
+  }
+  // column sums over the block's 128 rows: the 8 row lanes of each column group, then the waves
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float s = g[e];
+    s += __shfl_xor(s, 8, 64);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    if (lane < 8) red[w][cq * 8 + e] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int t = threadIdx.x;
+    float s = red[0][t];
+    for (int q = 1; q < NW; ++q) s += red[q][t];
+    a.col_part[(int64_t)blockIdx.y * a.K + cblk + t] = s;
+  }
+  // g_recon^T: column cblk + cc gets rows [r0, r0 + 128) as 16 chunks of 16 B (one per thread)
+  const int cc = threadIdx.x >> 4, ch = threadIdx.x & 15;
+  if (r0 + ch * 8 < a.B)
+    *(u32x4*)(a.g_t + (int64_t)(cblk + cc) * a.B + r0 + ch * 8) = *(const u32x4*)(tt + cc * TP + ch * 8);
+}
+
+extern "C" {
+
+// Row-term column blocks per model of cc_decode_loss_t's row_part (d / 64), or 0 when the fused entry
+// does not serve the shape (then: cc_decode_fwd_ws_t + cc_loss_fwd_bwd_rows_t).
+int64_t cc_decode_loss_ncb(int64_t B, int64_t h, int64_t n, int64_t d, int dtype) {
+  const int64_t K = n * d;
+  if (dtype != CC_BF16 || B <= 0 || h <= 0 || n <= 0 || d <= 0) return 0;
+  if (B % 8 || h % 8 || d % 64 || !use_pp(K, true, true, dtype)) return 0;
+  return d / 64;
+}
+
+int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, const void* x, const float* x_mean,
+                     float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
+                     int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
+  if (!acts || !W_dec_t || !b_dec || !x || !x_mean || !g_recon || !g_recon_t || !row_part || !col_part)
+    return CC_ERR_NULL;
+  if (!cc_decode_loss_ncb(B, h, n, d, dtype)) return CC_ERR_SHAPE;
+  if (!al16(x) || !al16(g_recon) || !al16(g_recon_t) || !al16(x_mean) || !al16(b_dec)) return CC_ERR_ALIGN;
+  const int64_t K = n * d;
+  hipStream_t st = (hipStream_t)stream;
+  DecPlan p;
+  const bool split = dec_plan(B, h, K, dtype, p);
+  GemmArgs a = {};
+  a.A = acts; a.lda = h; a.B = W_dec_t; a.ldb = h;
+  a.M = (int)B; a.N = split ? p.nbn_main * 256 : (int)K; a.K = (int)h;
+  a.out = g_recon; a.ldo = K; a.out_t = g_recon_t; a.ldt = B;
+  a.mask_src = x; a.bias = b_dec; a.tn = x_mean; a.scale0 = grad_scale;
+  a.col_part = col_part; a.row_part = row_part; a.d_model = (int)d; a.n_models = (int)n;
+  int rc = check_gemm(a, dtype, true, true);
+  if (rc) return rc;
+  a.nbm = (a.M + BM - 1) / BM;
+  a.nbn = (a.N + 255) / 256;
+  const bool fast = B % BM == 0 && a.N % 256 == 0;
+  if (!split) {
+    if (fast) hipLaunchKernelGGL((gemm_pp_kernel<true, true, EPI_DLOSS, true>), dim3(a.nbm * a.nbn), dim3(NTHR), 0, st, a);
+    else hipLaunchKernelGGL((gemm_pp_kernel<true, true, EPI_DLOSS>), dim3(a.nbm * a.nbn), dim3(NTHR), 0, st, a);
+    CC_LAUNCH_CHECK();
+    return CC_OK;
+  }
+  if (!ws) return CC_ERR_NULL;
+  const int64_t split_stride = split_stride_of(B, p);
+  if (ws_floats < (int64_t)p.nsplit * split_stride) return CC_ERR_SHAPE;
+  if (!al16(ws)) return CC_ERR_ALIGN;
+  GemmArgs t = {};
+  t.A = acts; t.lda = h; t.B = (const bf16_t*)W_dec_t + (int64_t)p.nbn_main * 256 * h; t.ldb = h;
+  t.M = (int)B; t.N = p.tail_cols; t.K = (int)h;
+  t.out = ws; t.ldo = p.tail_cols;
+  t.nbm = (t.M + BM - 1) / BM;
+  t.nbn = (t.N + 255) / 256;
+  const dim3 grid(a.nbm * a.nbn + p.nsplit * t.nbm * t.nbn);
+  if (fast) hipLaunchKernelGGL((gemm_pp_main_splitk_kernel<true, true, EPI_DLOSS, true>), grid, dim3(NTHR), 0, st, a, t,
+                               p.steps_per, p.nk, split_stride);
+  else hipLaunchKernelGGL((gemm_pp_main_splitk_kernel<true, true, EPI_DLOSS>), grid, dim3(NTHR), 0, st, a, t,
+                          p.steps_per, p.nk, split_stride);
+  CC_LAUNCH_CHECK();
+  LossSplitArgs l = {};
+  l.part = ws; l.S = p.nsplit; l.t_nbn = t.nbn; l.col0 = p.nbn_main * 256; l.B = (int)B; l.K = (int)K; l.n = (int)n;
+  l.d = (int)d; l.split_stride = split_stride;
+  l.b_dec = (const bf16_t*)b_dec; l.x = (const bf16_t*)x; l.x_mean = x_mean; l.gs = grad_scale;
+  l.g_recon = (bf16_t*)g_recon; l.g_t = (bf16_t*)g_recon_t; l.row_part = row_part; l.col_part = col_part;
+  hipLaunchKernelGGL(loss_split_kernel, dim3((unsigned)(p.tail_cols / 64), (unsigned)((B + 127) / 128)),
+                     dim3(LSPLIT_THREADS), 0,
+                     st, l);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
 }
 
 int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,

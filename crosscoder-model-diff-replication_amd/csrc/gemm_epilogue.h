@@ -145,6 +145,7 @@ struct EpiCols {
 template <int DT, int EPI, int BNT>
 CC_DEV void load_epi_cols(EpiCols<DT, BNT>& c, const GemmArgs& args, const FragGeom<BNT>& fg, int n0) {
   if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) c.load(args, fg, n0, EPI == EPI_ENC && args.bias);
+  if constexpr (EPI == EPI_DLOSS) c.load(args, fg, n0, true);  // b_dec, x_mean
 }
 
 // EPI_ENC / EPI_DACTS element-wise part (see epilogue_core).  FAST (bf16): every fragment in range, ReLU on.
@@ -244,6 +245,77 @@ CC_DEV void enc_dacts_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT
   }
 }
 
+// EPI_DLOSS (bf16, ping-pong LDS epilogue only): G2's reconstruction loss + its gradient on a whole-
+// contraction tile (crosscoder.py:104-121 and the autograd of :104-106), the arithmetic of loss_kernel:
+//   diff = (recon + b_dec) - x;  g_recon = bf16(grad_scale * diff)   (the same bits as loss_kernel)
+//   row terms l2 = sum diff^2, tv = sum (x - x_mean)^2 per row and 64-column wave block
+//   column sums of g_recon per 128-row wave half (the b_dec gradient's partial rows)
+// io.in4 = the x tile (staged in LDS), io.out4p writes g_recon in place; cols.bias = b_dec,
+// cols.tn = x_mean.  Row terms go to row_part[2][n * d/64][B] (d % 64 == 0: a wave's 64 columns lie in
+// one model); rows past M are masked (FAST: every row of the launch is inside the matrix).
+template <int BNT, bool FAST, class IO>
+CC_DEV void dloss_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN],
+                       const FragGeom<BNT>& fg, const IO& io, int tm, int m0, int n0, int wr, int lane,
+                       const EpiCols<CC_BF16, BNT>& cols) {
+  using WG = WaveGeom<BNT>;
+  const float gs = args.scale0;
+  // rows outer (a row's terms complete after its 4 column groups: 2 live sums instead of 16)
+  float csum[WG::TN][4];
+#pragma unroll
+  for (int j = 0; j < WG::TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) csum[j][e] = 0.f;
+  const int gc = n0 + fg.c0 - 4 * (lane >> 4);  // first column of this wave's 64-column block
+  const int d = args.d_model, ncb = d / 64, B = args.M;
+  const int m = gc / d, cb = (gc - m * d) / 64;
+  float* rp = args.row_part + (int64_t)(m * ncb + cb) * B;
+  const int64_t plane = (int64_t)args.n_models * ncb * B;
+  const bool rows_out = lane < 16 && gc < args.N;
+#pragma unroll
+  for (int i = 0; i < WG::TM; ++i) {
+    float l2 = 0.f, tv = 0.f;
+#pragma unroll
+    for (int j = 0; j < WG::TN; ++j) {
+      const bf16x4 xr = io.in4(i, j);
+      float g[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xv = V4<CC_BF16>::get(xr, e);
+        const float diff = (acc[i][j][e] + V4<CC_BF16>::get(cols.bias[j], e)) - xv;
+        l2 += diff * diff;
+        const float c = xv - cols.tn[j][e];
+        tv += c * c;
+        g[e] = gs * diff;
+      }
+      const bf16x4 p = pack4<CC_BF16>(g);  // the bf16 rounding, once
+      io.out4p(i, j, p);
+      if (FAST || fg.rv[i]) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) csum[j][e] += V4<CC_BF16>::get(p, e);
+      }
+    }
+    // the row's terms: sum over the 4 lane groups that hold its 64 columns
+    l2 += __shfl_xor(l2, 16, 64);
+    l2 += __shfl_xor(l2, 32, 64);
+    tv += __shfl_xor(tv, 16, 64);
+    tv += __shfl_xor(tv, 32, 64);
+    const int r = m0 + fg.r0 + 16 * i;
+    if (rows_out && (FAST || r < B)) {
+      rp[r] = l2;
+      rp[plane + r] = tv;
+    }
+  }
+  if (args.col_part) {  // reduce over the 16 lanes (rows) that share these 4 columns
+#pragma unroll
+    for (int j = 0; j < WG::TN; ++j) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) csum[j][e] = row16_sum(csum[j][e]);
+      if ((lane & 15) == 0 && fg.cv[j])
+        st4<CC_F32>(args.col_part, (int64_t)(tm * WG::WARPS_M + wr) * args.ldo + n0 + fg.c0 + 16 * j, csum[j]);
+    }
+  }
+}
+
 // cols: EpiCols loaded by the caller (EPI_ENC / EPI_DACTS; otherwise unread).
 // cw: dW_dec L1-term factors loaded by the caller (wgdec_factors; EPI_WGDEC with l1_scale != 0
 // only, otherwise unread).  Passed by reference so they stay in registers.
@@ -260,6 +332,9 @@ CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
     // as in the step's G1 / G3): no range selects, one bf16 conversion per output, an integer l0
     // count.  Same bits as the general form.
     enc_dacts_core<DT, EPI, BNT, FAST && DT == CC_BF16>(args, acc, fg, io, tm, n0, wr, lane, wave_slot, cols);
+  } else if constexpr (EPI == EPI_DLOSS) {
+    static_assert(DT == CC_BF16, "the fused decode + loss epilogue is bf16 only");
+    dloss_core<BNT, FAST>(args, acc, fg, io, tm, m0, n0, wr, lane, cols);
   } else if constexpr (EPI == EPI_WGDEC || EPI == EPI_WGENC) {
     constexpr int JB = EPB<DT, BNT>::JB_W;
     const bool l1term = EPI == EPI_WGDEC && args.scale0 != 0.f;

@@ -171,7 +171,9 @@ CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char
   return;
 #endif
   const int rows = args.M - m0, cols = args.N - n0, ldo = (int)args.ldo;
-  const void* in = EPI == EPI_DACTS ? args.mask_src : (EPI == EPI_WGDEC && args.scale0 != 0.f ? args.w_src : nullptr);
+  const void* in = EPI == EPI_DACTS || EPI == EPI_DLOSS
+                       ? args.mask_src
+                       : (EPI == EPI_WGDEC && args.scale0 != 0.f ? args.w_src : nullptr);
   float cw[8][4];  // dW_dec L1-term factors (EPI_WGDEC only)
   if (in) {
     if (!input_staged) {
@@ -489,7 +491,8 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
 #endif
 
   if constexpr (EPI == EPI_SPLIT) {  // split-K partial: accumulator fragments stored as they are (1 KB each)
-    float* o = (float*)args.out + ((int64_t)bid * 8 + wave) * 32 * 256;
+    // slab tile index tm * nbn + tn (row-major over the tiles, whatever the block order)
+    float* o = (float*)args.out + ((int64_t)(tm * args.nbn + tn) * 8 + wave) * 32 * 256;
 #pragma unroll
     for (int i = 0; i < WG::TM; ++i)
 #pragma unroll
@@ -557,14 +560,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_kernel(const GemmArgs a0
 // split-K units of the leftover tiles (t, as gemm_pp_splitk_kernel).  The split units are dispatched
 // as the first main tiles finish, instead of after the slowest one (the two-launch form waits for
 // the whole main wave to drain at the kernel boundary).
-template <bool AKC, bool BKC, int EPI>
+template <bool AKC, bool BKC, int EPI, bool FAST = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_main_splitk_kernel(const GemmArgs a0, const GemmArgs t,
                                                                     int steps_per, int nk_total,
                                                                     int64_t split_stride) {
   __shared__ __attribute__((aligned(16))) char smem[PP_LDS];
   const int nb0 = a0.nbm * a0.nbn;
   if ((int)blockIdx.x < nb0) {
-    pp_tile<AKC, BKC, EPI>(a0, smem, blockIdx.x);
+    pp_tile<AKC, BKC, EPI, FAST>(a0, smem, blockIdx.x);
     return;
   }
   const int b = blockIdx.x - nb0;

@@ -346,9 +346,23 @@ CC_DEV void ev_phase1(const EvSeg& a, int blk, int t, float (*red)[4]) {
     float l2 = 0.f, tv = 0.f, l2m[2] = {0, 0}, tvm[2] = {0, 0};
     for (int m = 0; m < n; ++m) {
       float s = 0.f, u = 0.f;
-      for (int cb = 0; cb < ncb; ++cb) {
-        s += a.row_part[(int64_t)(m * ncb + cb) * B + r];
-        u += a.row_part[plane + (int64_t)(m * ncb + cb) * B + r];
+      // 8 column blocks' loads in flight per trip (clamped index, no branch around a load), then the
+      // in-order adds: the sequential sum's bits with one memory latency per 8 blocks
+      for (int cb0 = 0; cb0 < ncb; cb0 += 8) {
+        float vs[8], vu[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int cb = cb0 + q < ncb ? cb0 + q : ncb - 1;
+          vs[q] = a.row_part[(int64_t)(m * ncb + cb) * B + r];
+          vu[q] = a.row_part[plane + (int64_t)(m * ncb + cb) * B + r];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          if (cb0 + q < ncb) {
+            s += vs[q];
+            u += vu[q];
+          }
+        }
       }
       l2 += s;
       tv += u;
@@ -968,10 +982,17 @@ int cc_loss_finalize(const float* row_part, const float* l1_part, int64_t n_l1, 
 int cc_loss_finalize_mapped(const float* row_part, const float* l1_part, int64_t n_l1, const float* l0_part,
                             int64_t n_l0, float* ev, float* ev_a, float* ev_b, float* scalars, float* l1l0_out,
                             float* host_out, uint32_t seq, int64_t B, int64_t n, int64_t d, void* stream) {
+  return cc_loss_finalize_nb(row_part, cc_loss_col_blocks(d), l1_part, n_l1, l0_part, n_l0, ev, ev_a, ev_b, scalars,
+                             l1l0_out, host_out, seq, B, n, d, stream);
+}
+
+int cc_loss_finalize_nb(const float* row_part, int64_t ncb_rows, const float* l1_part, int64_t n_l1,
+                        const float* l0_part, int64_t n_l0, float* ev, float* ev_a, float* ev_b, float* scalars,
+                        float* l1l0_out, float* host_out, uint32_t seq, int64_t B, int64_t n, int64_t d, void* stream) {
   if (!row_part || !scalars) return CC_ERR_NULL;
-  if (B <= 0 || n <= 0 || d <= 0) return CC_ERR_SHAPE;
+  if (B <= 0 || n <= 0 || d <= 0 || ncb_rows <= 0) return CC_ERR_SHAPE;
   // the per-block partials of the row terms use the tail of `scalars` (cc_loss_scalars_len)
-  int ncb = (int)cc_loss_col_blocks(d);
+  int ncb = (int)ncb_rows;
   int nblk = (int)((B + 255) / 256);
   float* ev_part = scalars + 8;
   hipStream_t st = (hipStream_t)stream;
@@ -1147,15 +1168,23 @@ int cc_loss_tail(const float* acts_colpart, int64_t R, int64_t h, float* colsum_
                  float* l1_part, const float* row_part, const float* l0_part, int64_t n_l0, float* ev, float* ev_a,
                  float* ev_b, float* scalars, float* l1l0_out, float* host_out, uint32_t seq, int64_t B, int64_t n,
                  int64_t d, uint32_t* counter, void* stream) {
+  return cc_loss_tail_nb(acts_colpart, R, h, colsum_acts, tn, l1_part, row_part, cc_loss_col_blocks(d), l0_part, n_l0,
+                         ev, ev_a, ev_b, scalars, l1l0_out, host_out, seq, B, n, d, counter, stream);
+}
+
+int cc_loss_tail_nb(const float* acts_colpart, int64_t R, int64_t h, float* colsum_acts, const float* tn,
+                    float* l1_part, const float* row_part, int64_t ncb, const float* l0_part, int64_t n_l0, float* ev,
+                    float* ev_a, float* ev_b, float* scalars, float* l1l0_out, float* host_out, uint32_t seq,
+                    int64_t B, int64_t n, int64_t d, uint32_t* counter, void* stream) {
   if (!acts_colpart || !colsum_acts || !tn || !l1_part || !row_part || !scalars || !counter) return CC_ERR_NULL;
-  if (R <= 0 || h <= 0 || B <= 0 || n <= 0 || d <= 0) return CC_ERR_SHAPE;
+  if (R <= 0 || h <= 0 || B <= 0 || n <= 0 || d <= 0 || ncb <= 0) return CC_ERR_SHAPE;
   TailArgs a = {};
   const int nred = (int)((h + RED_COLS - 1) / RED_COLS);
   const int nblk = (int)((B + 255) / 256);
   float* ev_part = scalars + 8;  // as cc_loss_finalize (cc_loss_scalars_len)
   a.red[0] = {acts_colpart, (int)R, (int)h, h, 1.f, colsum_acts, nullptr, nullptr, tn, l1_part};
   a.red_blocks[0] = nred;
-  a.ev = {row_part, (int)B, (int)n, (int)cc_loss_col_blocks(d), ev, ev_a, ev_b, ev_part};
+  a.ev = {row_part, (int)B, (int)n, (int)ncb, ev, ev_a, ev_b, ev_part};
   a.ev_blocks = nblk;
   a.finalize = 1;
   a.scal = {ev_part, nblk, l1_part, nred, l0_part, n_l0, (int)B, scalars, l1l0_out, host_out, (unsigned)seq};

@@ -132,8 +132,16 @@ class StepWorkspace:
         self.g_recon = E(B, K, dt=dtype)
         self.g_recon_t = E(K, B, dt=dtype) if self.tr else None
         self.ncb = ops.loss_col_blocks(d)
-        self.row_part = E(2, n * self.ncb, B)
+        # G2 + loss in one pass (decode_loss_t) when it serves the shape: its row terms come per 64-column
+        # block and its b_dec-gradient partials per 128-row group; one storage holds either layout
+        self.fused_ncb = ops.decode_loss_ncb(B, h, n, d, dtype) if self.tr else 0
+        rp = E(2 * n * max(self.ncb, self.fused_ncb) * B)
+        self.row_part = rp[:2 * n * self.ncb * B].view(2, n * self.ncb, B)  # loss_fwd_bwd's layout
+        self.row_part_fused = rp[:2 * n * self.fused_ncb * B].view(2, n * self.fused_ncb, B) if self.fused_ncb \
+            else None
         self.loss_colpart = E(ops.loss_part_rows(B), K)
+        self.row_ncb = None         # layout of the row terms last written (None: loss_fwd_bwd's)
+        self.loss_col_rows = ops.loss_part_rows(B)  # rows of loss_colpart last written
         self.ev = E(B)
         self.ev_a = E(B)
         self.ev_b = E(B)
@@ -202,10 +210,12 @@ def decoder_norms(ws, P):
     _decoder_derived(ws, P)
 
 
-def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True):
+def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True, finalize=True):
     """Forward + reconstruction-loss gradient.  P: params Arena.  x_in [B, n, d] any of
     fp32/bf16, factor [n] or None.  Leaves losses in ws.scalars / ws.ev*, g_recon ready
-    (loss=False: stops at the fp32 reconstruction, for loss_rows / loss_finalize by slices)."""
+    (loss=False: stops at the fp32 reconstruction, for loss_rows / loss_finalize by slices;
+    finalize=False: stops after the loss rows, for loss_finalize_beside).  Where the fused entry
+    serves the shape, G2 and the loss rows are one pass (decode_loss_t; no fp32 reconstruction)."""
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
     with _span("prep"):
         ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart, out_t=ws.x_t)
@@ -222,6 +232,12 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
     P.wait_pending()
     decoder_norms(ws, P)  # (+ W_dec^T), unless launched already after the last Adam
+    if loss and ws.fused_ncb:
+        decode_loss(ws, P, grad_scale)
+        ws.acts_pending = True
+        if finalize:
+            loss_finalize(ws)
+        return
     with _span("G2_decode"):
         if ws.tr:
             ops.decode_partial_t(ws.acts, ws.W_dec_t, ws.recon, ws.dec_ws)
@@ -231,7 +247,19 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     # the loss finaliser's launch (loss_tail)
     ws.acts_pending = True
     if loss:
-        loss_from_recon(ws, P, grad_scale)
+        loss_rows(ws, P, 0, ws.B, grad_scale)
+        if finalize:
+            loss_finalize(ws)
+
+
+def decode_loss(ws, P, grad_scale=None):
+    """G2 + loss rows + g_recon (and g_recon^T) in one pass over the whole batch (decode_loss_t)."""
+    gs = 2.0 / ws.B if grad_scale is None else grad_scale
+    with _span("G2_decode"):
+        ops.decode_loss_t(ws.acts, ws.W_dec_t, P.b_dec_flat, ws.x, ws.x_mean, gs, ws.g_recon, ws.g_recon_t,
+                          ws.row_part_fused, ws.loss_colpart, ws.dec_ws, ws.n, ws.d)
+    ws.row_ncb = ws.fused_ncb
+    ws.loss_col_rows = ops.col_part_rows(ws.B)
 
 
 def loss_rows(ws, P, r0, r1, grad_scale=None):
@@ -240,22 +268,39 @@ def loss_rows(ws, P, r0, r1, grad_scale=None):
     with _span("loss"):
         ops.loss_fwd_bwd(ws.recon, P.b_dec_flat, ws.x, ws.x_mean, ws.g_recon, ws.row_part, ws.loss_colpart, gs, ws.B,
                          ws.n, ws.d, row0=r0, rows=r1 - r0, g_recon_t=ws.g_recon_t)
+    ws.row_ncb = None
+    ws.loss_col_rows = ops.loss_part_rows(ws.B)
+
+
+def _row_part(ws):
+    return ws.row_part if ws.row_ncb is None else ws.row_part_fused
+
+
+def loss_colpart(ws):
+    """The b_dec-gradient partial rows the last loss producer wrote."""
+    return ws.loss_colpart[:ws.loss_col_rows]
 
 
 def loss_finalize(ws, l1l0_out=None):
     """Loss scalars / EV vectors.  After a forward (which deferred the activation column sums) one
     launch does both (cc_loss_tail); a re-formed loss (same activations) only the finaliser."""
     if ws.acts_pending:
-        ops.loss_tail(ws.acts_colpart, ws.h, ws.colsum_acts, ws.tn, ws.l1_part, ws.row_part, ws.l0_part, ws.n_wave,
-                      ws.ev, ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], l1l0_out=l1l0_out)
+        ops.loss_tail(ws.acts_colpart, ws.h, ws.colsum_acts, ws.tn, ws.l1_part, _row_part(ws), ws.l0_part, ws.n_wave,
+                      ws.ev, ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], l1l0_out=l1l0_out,
+                      ncb=ws.row_ncb)
         ws.acts_pending = False
         return
-    ops.loss_finalize(ws.row_part, ws.l1_part, ws.n_l1, ws.l0_part, ws.n_wave, ws.ev, ws.ev_a, ws.ev_b, ws.scalars,
-                      ws.B, ws.n, ws.d, l1l0_out=l1l0_out)
+    ops.loss_finalize(_row_part(ws), ws.l1_part, ws.n_l1, ws.l0_part, ws.n_wave, ws.ev, ws.ev_a, ws.ev_b, ws.scalars,
+                      ws.B, ws.n, ws.d, l1l0_out=l1l0_out, ncb=ws.row_ncb)
 
 
 def loss_from_recon(ws, P, grad_scale=None):
-    loss_rows(ws, P, 0, ws.B, grad_scale)
+    """Re-form g_recon (+ the loss slabs) for another grad_scale, from the forward's operands: after the
+    fused pass (no fp32 reconstruction kept) G2 runs again on the same acts / W_dec^T."""
+    if ws.row_ncb is not None:
+        decode_loss(ws, P, grad_scale)
+    else:
+        loss_rows(ws, P, 0, ws.B, grad_scale)
     loss_finalize(ws)
 
 
@@ -320,16 +365,16 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
             ops.wgrad_both(ws.acts, ws.g_recon, P.W_dec_hk, ws.inv_norms, ws.colsum_acts, l1_scale, G.W_dec_hk,
                            ws.sq_slice(1), ws.g_pre, ws.x, G.W_enc_hk, ws.sq_slice(0), n, d)
     if sums_out is not None:
-        ops.grad_tail_sums(ws.gpre_colpart, G.b_enc, ws.sq_slice(2), ws.loss_colpart, G.b_dec_flat, ws.sq_slice(3),
+        ops.grad_tail_sums(ws.gpre_colpart, G.b_enc, ws.sq_slice(2), loss_colpart(ws), G.b_dec_flat, ws.sq_slice(3),
                            ws.sq, ws.sq_off, sums_out, ws.tail_ctr[1:2], zero_mask=zero_mask)
         return
     if clip is not None:
-        ops.grad_tail(ws.gpre_colpart, G.b_enc, ws.sq_slice(2), ws.loss_colpart, G.b_dec_flat, ws.sq_slice(3), ws.sq,
+        ops.grad_tail(ws.gpre_colpart, G.b_enc, ws.sq_slice(2), loss_colpart(ws), G.b_dec_flat, ws.sq_slice(3), ws.sq,
                       ws.sq_off, clip, ws.dtype == torch.bfloat16, ws.clip_out, ws.tail_ctr[1:2])
         ws.clip_ready = True
         return
     ops.reduce_rows(ws.gpre_colpart, ws.gpre_colpart.shape[0], h, out_t=G.b_enc, sq_part=ws.sq_slice(2))
-    ops.reduce_rows(ws.loss_colpart, ws.loss_colpart.shape[0], K, out_t=G.b_dec_flat, sq_part=ws.sq_slice(3))
+    ops.reduce_rows(loss_colpart(ws), ws.loss_col_rows, K, out_t=G.b_dec_flat, sq_part=ws.sq_slice(3))
 
 
 # workgroups of the decoder-half Adam that runs beside the next step's G1 (128 / 192 / 384 measured

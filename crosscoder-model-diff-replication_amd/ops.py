@@ -176,6 +176,20 @@ def decode_partial_t(acts, W_dec_t, recon_f32, ws=None):
                                    0 if ws is None else ws.numel(), B, h, K, dtype_code(acts.dtype), _stream(acts)))
 
 
+def decode_loss_ncb(B, h, n, d, dtype):
+    """Row-term column blocks per model of decode_loss_t's row_part (d / 64), 0 if it does not serve the shape."""
+    return int(lib().cc_decode_loss_ncb(B, h, n, d, dtype_code(dtype)))
+
+
+def decode_loss_t(acts, W_dec_t, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t, row_part, col_part, ws, n, d):
+    """G2 + the reconstruction loss in one pass (cc_decode_loss_t): g_recon / g_recon_t bit-identical to
+    decode_partial_t + loss_fwd_bwd(g_recon_t=...); row_part [2, n * d/64, B], col_part [B/128, K]."""
+    B, h = acts.shape
+    check(lib().cc_decode_loss_t(_ptr(acts), _ptr(W_dec_t), _ptr(b_dec), _ptr(x), _ptr(x_mean), grad_scale,
+                                 _ptr(g_recon), _ptr(g_recon_t), _ptr(row_part), _ptr(col_part), _ptr(ws),
+                                 0 if ws is None else ws.numel(), B, h, n, d, dtype_code(acts.dtype), _stream(acts)))
+
+
 def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_scale, B, n, d, row0=0, rows=None,
                  g_recon_t=None):
     """Loss terms + g_recon for batch rows [row0, row0 + rows) (default: all B rows);
@@ -194,8 +208,15 @@ def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_
 
 
 def loss_finalize(row_part, l1_part, n_l1, l0_part, n_l0, ev, ev_a, ev_b, scalars, B, n, d, l1l0_out=None,
-                  host=None, seq=0):
-    """host (optional): a _hip.MappedHostBuffer that also receives scalars[0:8] and then `seq` in word 8."""
+                  host=None, seq=0, ncb=None):
+    """host (optional): a _hip.MappedHostBuffer that also receives scalars[0:8] and then `seq` in word 8.
+    ncb: row_part's column blocks per model when it is not loss_fwd_bwd's layout (decode_loss_t's)."""
+    if ncb is not None:
+        check(lib().cc_loss_finalize_nb(_ptr(row_part), ncb, _ptr(l1_part), n_l1, _ptr(l0_part), n_l0, _ptr(ev),
+                                        _ptr(ev_a), _ptr(ev_b), _ptr(scalars), _ptr(l1l0_out),
+                                        host.device_ptr if host is not None else None, seq, B, n, d,
+                                        _stream(row_part)))
+        return
     if host is not None:
         check(lib().cc_loss_finalize_mapped(_ptr(row_part), _ptr(l1_part), n_l1, _ptr(l0_part), n_l0, _ptr(ev),
                                             _ptr(ev_a), _ptr(ev_b), _ptr(scalars), _ptr(l1l0_out), host.device_ptr,
@@ -206,8 +227,15 @@ def loss_finalize(row_part, l1_part, n_l1, l0_part, n_l0, ev, ev_a, ev_b, scalar
 
 
 def loss_tail(acts_colpart, h, colsum_acts, tn, l1_part, row_part, l0_part, n_l0, ev, ev_a, ev_b, scalars, B, n, d,
-              counter, l1l0_out=None, host=None, seq=0):
+              counter, l1l0_out=None, host=None, seq=0, ncb=None):
     """reduce_rows(acts_colpart, dot_w=tn, dot_part=l1_part) + loss_finalize as one launch (same bits)."""
+    if ncb is not None:
+        check(lib().cc_loss_tail_nb(_ptr(acts_colpart), acts_colpart.shape[0], h, _ptr(colsum_acts), _ptr(tn),
+                                    _ptr(l1_part), _ptr(row_part), ncb, _ptr(l0_part), n_l0, _ptr(ev), _ptr(ev_a),
+                                    _ptr(ev_b), _ptr(scalars), _ptr(l1l0_out),
+                                    host.device_ptr if host is not None else None, seq, B, n, d, _ptr(counter),
+                                    _stream(acts_colpart)))
+        return
     check(lib().cc_loss_tail(_ptr(acts_colpart), acts_colpart.shape[0], h, _ptr(colsum_acts), _ptr(tn), _ptr(l1_part),
                              _ptr(row_part), _ptr(l0_part), n_l0, _ptr(ev), _ptr(ev_a), _ptr(ev_b), _ptr(scalars),
                              _ptr(l1l0_out), host.device_ptr if host is not None else None, seq, B, n, d,

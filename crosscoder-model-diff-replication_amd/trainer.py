@@ -109,8 +109,8 @@ class Trainer:
         P = cc.arena()
         opt = self.optimizer
         side = self._side_stream()
-        engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None, loss=False)
-        engine.loss_rows(ws, P, 0, ws.B)
+        # prep, G1, G2 + the loss rows (one pass where decode_loss_t serves the shape)
+        engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None, finalize=False)
         # the loss scalars (+ their host copy) on the side stream, beside G3
         tail_done = engine.loss_finalize_beside(ws, side, on_losses)
         l1c = self.get_l1_coeff()

@@ -150,6 +150,21 @@ int cc_loss_fwd_bwd_rows_t(const float* recon_f32, const void* b_dec, const void
                            void* g_recon, void* g_recon_t, float* row_part, float* col_part, float grad_scale,
                            int64_t row0, int64_t rows, int64_t B, int64_t n, int64_t d, int dtype, void* stream);
 
+/* G2 + the reconstruction loss in one pass (crosscoder.py:82-89 then :104-121 and their autograd),
+ * the fused form of cc_decode_fwd_ws_t + cc_loss_fwd_bwd_rows_t over all rows: the whole-contraction
+ * tiles run the loss as their GEMM epilogue (the fp32 reconstruction never reaches HBM), the split-K
+ * leftover columns are summed in cc_decode_fwd_ws's fixed order and then run the same arithmetic.
+ * g_recon / g_recon_t are bit-identical to the two-call form; the partial slabs use other blocks:
+ *   row_part [2][n * ncb][B], ncb = cc_decode_loss_ncb(..) = d / 64 column blocks per model
+ *   col_part [cc_col_part_rows(B)][K] (column sums of g_recon per 128-row group)
+ * so their sums agree to fp32 reassociation (cc_loss_tail_nb / cc_loss_finalize_nb take ncb; the b_dec
+ * gradient sums cc_col_part_rows(B) rows).  ws: cc_decode_ws_floats(B, h, n*d, dtype) floats.
+ * bf16, B % 8 == 0, d % 64 == 0; cc_decode_loss_ncb returns 0 for shapes this entry does not serve. */
+int64_t cc_decode_loss_ncb(int64_t B, int64_t h, int64_t n, int64_t d, int dtype);
+int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, const void* x, const float* x_mean,
+                     float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
+                     int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream);
+
 /* Loss reduction (crosscoder.py:106-128, trainer.py:51-61): per-row explained variances
  * ev/ev_a/ev_b [B] (fp32) and scalars[0:8] = {l2, l1, l0, mean ev, mean ev_a, mean ev_b, 0, 0};
  * `scalars` holds cc_loss_scalars_len(B) floats (the tail is workspace).
@@ -177,6 +192,17 @@ int cc_loss_tail(const float* acts_colpart, int64_t R, int64_t h, float* colsum_
                  float* l1_part, const float* row_part, const float* l0_part, int64_t n_l0, float* ev, float* ev_a,
                  float* ev_b, float* scalars, float* l1l0_out, float* host_out, uint32_t seq, int64_t B, int64_t n,
                  int64_t d, uint32_t* counter, void* stream);
+
+/* cc_loss_finalize_mapped / cc_loss_tail over a row_part of `ncb` column blocks per model (the
+ * producer's layout: cc_loss_col_blocks(d) for cc_loss_fwd_bwd*, cc_decode_loss_ncb for
+ * cc_decode_loss_t).  host_out may be NULL. */
+int cc_loss_finalize_nb(const float* row_part, int64_t ncb, const float* l1_part, int64_t n_l1,
+                        const float* l0_part, int64_t n_l0, float* ev, float* ev_a, float* ev_b, float* scalars,
+                        float* l1l0_out, float* host_out, uint32_t seq, int64_t B, int64_t n, int64_t d, void* stream);
+int cc_loss_tail_nb(const float* acts_colpart, int64_t R, int64_t h, float* colsum_acts, const float* tn,
+                    float* l1_part, const float* row_part, int64_t ncb, const float* l0_part, int64_t n_l0, float* ev,
+                    float* ev_a, float* ev_b, float* scalars, float* l1l0_out, float* host_out, uint32_t seq,
+                    int64_t B, int64_t n, int64_t d, uint32_t* counter, void* stream);
 
 /* Backward through decode + L1 + ReLU (autograd of crosscoder.py:77,84-89,126):
  * g_pre[B,h] = (g_recon . W_dec^T + l1_scale * tn[h]) * (acts > 0),  l1_scale = l1_coeff / B.

@@ -67,6 +67,23 @@ def test_argument_validation_without_gpu():
                             2, 32, null, null) == 1                                              # no counter
     assert lib.cc_loss_tail(fake, 16, 256, fake, fake, fake, fake, fake, 8, fake, fake, fake, fake, null, null, 0, 0,
                             2, 32, fake, null) == 3                                              # empty batch
+    assert lib.cc_loss_tail_nb(fake, 16, 256, fake, fake, fake, fake, 0, fake, 8, fake, fake, fake, fake, null, null,
+                               0, 64, 2, 32, fake, null) == 3                                    # ncb = 0
+    assert lib.cc_loss_finalize_nb(null, 36, fake, 8, fake, 8, fake, fake, fake, fake, null, null, 0, 64, 2, 32,
+                                   null) == 1
+    # G2 + loss in one pass (cc_decode_loss_t): served shapes, checks before any launch
+    assert lib.cc_decode_loss_ncb(4096, 16384, 2, 2304, 1) == 36      # config 2: d / 64 row-term blocks
+    assert lib.cc_decode_loss_ncb(4096, 16384, 2, 2304, 2) == 0       # fp32: two-pass form
+    assert lib.cc_decode_loss_ncb(4096, 16384, 2, 200, 1) == 0        # d % 64
+    assert lib.cc_decode_loss_ncb(4100, 16384, 2, 2304, 1) == 0       # B % 8
+    args = [fake] * 10 + [fake, 0, 4096, 16384, 2, 2304, 1, null]
+    args[5] = ctypes.c_float(2.0 / 4096)
+    bad = list(args)
+    bad[3] = null
+    assert lib.cc_decode_loss_t(*bad) == 1                            # no x
+    bad = list(args)
+    bad[15] = 200
+    assert lib.cc_decode_loss_t(*bad) == 3                            # d % 64
 
 
 def _cfg(dtype="bf16", h=256, d=32, device="cpu"):

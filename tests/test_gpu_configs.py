@@ -61,11 +61,11 @@ def test_baseline_config_full_size_trainer_step(gpu, name):
     assert rel(D(ws.acts[rows]), pre.clamp_min(0)) < 1e-2
     flips = ((ws.acts[rows] > 0) != (pre > 0)).float().mean().item()
     assert flips <= 2e-3, flips
-    # G2: fp32 partial reconstruction rows (no bias), crosscoder.py:82-89
+    # G2 (+ the loss in its epilogue): g_recon rows = bf16(2 (acts W_dec + b_dec - x) / B), crosscoder.py:82-89
     acts = D(ws.acts)
-    assert rel(D(ws.recon[rows]), acts[rows] @ Wd0) < 1e-5
+    recon = acts @ Wd0 + bd0  # fp64 reconstruction of the step's own activations
+    assert rel(D(ws.g_recon[rows]), 2 * (recon[rows] - x[rows]) / B) < 8e-3
     # loss scalars vs fp64 reductions of the step's own tensors (crosscoder.py:104-128)
-    recon = D(ws.recon) + bd0
     l2_row = (recon - x).pow(2).sum(1)
     tn = Wd0.view(h, n, d).norm(dim=-1).sum(-1)
     assert math.isclose(loss["l2_loss"], l2_row.mean().item(), rel_tol=1e-4)

@@ -442,6 +442,58 @@ def test_full_size_step_deterministic(gpu, full_size_case):
 
 
 # ----------------------------------------------------------------------------- batch slices / sharded
+@pytest.mark.parametrize("B,n,d,h", [(4096, 2, 2304, 1024),   # config-2 columns: 256 main tiles + 8-way split
+                                     (4000, 2, 2304, 512),    # split, ragged last row block
+                                     (1000, 2, 256, 1024),    # whole-tile grid only, ragged rows
+                                     (512, 4, 64, 384)])      # n = 4, d = 64
+def test_fused_decode_loss_matches_two_pass(gpu, B, n, d, h):
+    """G2 + loss in one pass (cc_decode_loss_t: the loss as the GEMM epilogue, the split-K leftover summed
+    in reduce_splits' order) vs the two-pass form (cc_decode_fwd_ws_t + cc_loss_fwd_bwd_rows_t):
+    g_recon / g_recon^T and everything downstream of them (g_pre, W gradients) bit for bit; the
+    per-row loss terms, EV, loss scalars and the b_dec gradient to fp32 reassociation."""
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16", seed=5,
+               device=str(gpu))
+    cc = ca.CrossCoder(cfg, n_models=n)
+    g = torch.Generator().manual_seed(B + d)
+    raw = (torch.randn(B, n, d, generator=g) * 3).to(gpu)
+    factor = torch.tensor([0.7, 1.3, 0.9, 1.1][:n]).to(torch.bfloat16).to(gpu)
+    a = cc.arena()
+    res = []
+    for fused in (True, False):
+        ws = engine.StepWorkspace(B, n, d, h, torch.bfloat16, gpu)
+        assert ws.fused_ncb == d // 64
+        G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+        ws.g_recon.fill_(float("nan"))
+        ws.g_recon_t.fill_(float("nan"))
+        if fused:
+            engine.forward(ws, a, raw, factor)
+            assert ws.row_ncb == d // 64
+        else:
+            engine.forward(ws, a, raw, factor, loss=False)
+            engine.loss_rows(ws, a, 0, B)
+            engine.loss_finalize(ws)
+        engine.backward(ws, a, G, 2.0, clip=1.0)
+        torch.cuda.synchronize()
+        rp = engine._row_part(ws)
+        per_row = rp.view(2, n, -1, B).sum(2)  # [l2 / tv][model][row]
+        res.append(dict(g_recon=ws.g_recon.clone(), g_recon_t=ws.g_recon_t.clone(), g_pre_t=ws.g_pre_t.clone(),
+                        W=G.data[:2 * h * n * d + h].clone(), b_dec=G.b_dec_flat.clone(), per_row=per_row.clone(),
+                        ev=torch.stack([ws.ev, ws.ev_a, ws.ev_b]).clone(), scalars=ws.scalars[:6].clone(),
+                        clip=ws.clip_out[:2].clone()))
+    f, t = res
+    assert not bool(torch.isnan(f["g_recon"]).any())
+    for k in ("g_recon", "g_recon_t", "g_pre_t", "W"):
+        assert torch.equal(f[k], t[k]), k
+    assert torch.equal(f["g_recon_t"], f["g_recon"].t())
+    assert rel(f["per_row"], t["per_row"]) < 1e-5
+    assert (f["ev"] - t["ev"]).abs().max().item() < 1e-5
+    assert rel(f["scalars"], t["scalars"]) < 1e-6
+    # b_dec.grad = bf16(column sums of g_recon): at most one bf16 rounding apart
+    db = (f["b_dec"].float() - t["b_dec"].float()).abs()
+    assert bool((db <= t["b_dec"].float().abs() * 2 ** -7 + 1e-30).all())
+    assert rel(f["clip"], t["clip"]) < 1e-2
+
+
 @pytest.mark.parametrize("B", [1024, 1000])
 def test_sliced_loss_and_dacts_match_whole_batch(gpu, B):
     """The sharded step's per-slice loss rows + d_acts (run as each slice's all-reduce lands)
@@ -467,8 +519,10 @@ def test_sliced_loss_and_dacts_match_whole_batch(gpu, B):
                 engine.dacts_rows(ws, a, 2.0, r0, r1)
             engine.loss_finalize(ws)
             engine.backward(ws, a, G, 2.0, dacts_done=True)
-        else:
-            engine.forward(ws, a, raw, factor)
+        else:  # the whole batch through the same two-pass decode + loss kernels
+            engine.forward(ws, a, raw, factor, loss=False)
+            engine.loss_rows(ws, a, 0, B)
+            engine.loss_finalize(ws)
             engine.backward(ws, a, G, 2.0)
         torch.cuda.synchronize()
         outs.append([t.clone() for t in (ws.g_recon, ws.g_pre, ws.row_part, ws.loss_colpart, ws.scalars[:6],
@@ -493,6 +547,7 @@ def test_transposed_wgrad_step_matches_batch_major(gpu, B):
     for tr in (True, False):
         ws = engine.StepWorkspace(B, n, d, h, torch.bfloat16, gpu, transposed=tr)
         assert ws.tr == tr
+        ws.fused_ncb = 0  # both through the two-pass decode + loss (the fused form has its own test)
         G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
         engine.forward(ws, a, raw, factor)
         engine.backward(ws, a, G, 2.0)
@@ -915,8 +970,10 @@ def test_baseline_config_shapes_spot_check(gpu, B, n, d, h):
     # G1: acts rows
     pre = x[rows] @ We.t() + be
     assert rel(acts[rows], pre.clamp_min(0)) < 1e-2
-    # G2: fp32 partial reconstruction rows (split-K leftover columns included)
-    assert rel(D(ws.recon)[rows], acts[rows] @ Wd) < 1e-5
+    # G2 + loss (one pass): g_recon rows = bf16(2 (acts W_dec + b_dec - x) / B), split-K leftover columns
+    # included (crosscoder.py:82-89, 104-106)
+    recon = acts[rows] @ Wd + D(a.b_dec_flat)
+    assert rel(grec[rows], 2.0 * (recon - x[rows]) / B) < 8e-3
     # G3: g_pre rows = (g_recon W_dec^T + l1c tn / B) * [acts > 0]
     ref3 = (grec[rows] @ Wd.t() + 2.0 * tn / B) * (acts[rows] > 0)
     assert rel(gpre[rows], ref3) < 1e-2
@@ -959,17 +1016,18 @@ def test_fused_tails_match_separate_launches(gpu, enc_dtype, B, n, d, h):
     colsum, l1p = f32(ws.colsum_acts), f32(ws.l1_part)
     ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=colsum, dot_w=ws.tn, dot_part=l1p)
     ev, ev_a, ev_b, sc = f32(ws.ev), f32(ws.ev_a), f32(ws.ev_b), f32(ws.scalars)
-    ops.loss_finalize(ws.row_part, l1p, ws.n_l1, ws.l0_part, ws.n_wave, ev, ev_a, ev_b, sc, B, n, d)
+    rp = engine._row_part(ws)  # (the layout of the pass that wrote the row terms)
+    ops.loss_finalize(rp, l1p, ws.n_l1, ws.l0_part, ws.n_wave, ev, ev_a, ev_b, sc, B, n, d, ncb=ws.row_ncb)
     host = _hip.MappedHostBuffer(16)
     sc2 = f32(ws.scalars)
-    ops.loss_finalize(ws.row_part, l1p, ws.n_l1, ws.l0_part, ws.n_wave, f32(ev), f32(ev), f32(ev), sc2, B, n, d,
-                      host=host, seq=7)
+    ops.loss_finalize(rp, l1p, ws.n_l1, ws.l0_part, ws.n_wave, f32(ev), f32(ev), f32(ev), sc2, B, n, d,
+                      host=host, seq=7, ncb=ws.row_ncb)
     # grad side, separately
     sq = ws.sq.clone()
     gbe, gbd = torch.empty_like(G.b_enc), torch.empty_like(G.b_dec_flat)
     o = ws.sq_off
     ops.reduce_rows(ws.gpre_colpart, ws.gpre_colpart.shape[0], h, out_t=gbe, sq_part=sq[o[2]:o[3]])
-    ops.reduce_rows(ws.loss_colpart, ws.loss_colpart.shape[0], n * d, out_t=gbd, sq_part=sq[o[3]:o[4]])
+    ops.reduce_rows(engine.loss_colpart(ws), ws.loss_col_rows, n * d, out_t=gbd, sq_part=sq[o[3]:o[4]])
     clip = torch.empty(8, device=gpu)
     ops.clip_finalize(sq, o, 1.0, cc.dtype == torch.bfloat16, clip)
     torch.cuda.synchronize()

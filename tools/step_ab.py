@@ -83,19 +83,19 @@ def dec_adam_side_norms_main():
     return adam
 
 
-class NoLoss:
-    """Timing-only variant: the loss kernel skipped (g_recon keeps the last values): the upper bound of what
-    folding the loss into G2's epilogue could save."""
+class TwoPassLoss:
+    """Variant: G2 to the fp32 reconstruction, then the separate loss kernel (cc_decode_fwd_ws_t +
+    cc_loss_fwd_bwd_rows_t: the round-2 form) instead of the loss in G2's epilogue (cc_decode_loss_t)."""
 
-    def __init__(self):
-        from crosscoder_amd import engine
-        self.engine, self.saved = engine, engine.loss_rows
+    def __init__(self, tr):
+        self.tr = tr
 
     def on(self):
-        self.engine.loss_rows = lambda *a, **k: None
+        ws = self.tr.crosscoder._ws
+        self.saved, ws.fused_ncb = ws.fused_ncb, 0
 
     def off(self):
-        self.engine.loss_rows = self.saved
+        self.tr.crosscoder._ws.fused_ncb = self.saved
 
 
 def flat_dec_adam(blocks):
@@ -171,8 +171,8 @@ def main():
     for b in (512, 1024):
         variants[f"flat dec Adam {b} blocks"] = (flat_dec_adam(b), None, None)
     variants["dec Adam beside G1 + norms on main"] = (dec_adam_side_norms_main(), None, None)
-    nl = NoLoss()
-    variants["no loss kernel (timing only)"] = (shipped, nl.on, nl.off)
+    tp = TwoPassLoss(tr)
+    variants["two-pass decode + loss"] = (shipped, tp.on, tp.off)
     variants["serial Adam + norms beside G1"] = (serial_adam(True), None, None)
     variants["serial Adam + norms before G2"] = (serial_adam(False), None, None)
     variants["G2 from W_dec (no W_dec^T pass)"] = (shipped, g2mn.on, g2mn.off)
