@@ -304,11 +304,24 @@ def loss_from_recon(ws, P, grad_scale=None):
     loss_finalize(ws)
 
 
+def acts_colsum(ws):
+    """Sum_b acts (G4's L1 term reads it) and the l1 dot partials against the decoder norms, on torch's
+    stream (the reduction half of the loss tail, same bits): loss_finalize_beside's side-stream launch is
+    then read by nothing on torch's stream, which never waits for it (a cross-stream wait costs ~17 us
+    even on a completed event, profiles/r02_step_ab_prep_ahead.txt)."""
+    if not ws.acts_pending:
+        return
+    ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], ws.h, out_f32=ws.colsum_acts, dot_w=ws.tn,
+                    dot_part=ws.l1_part)
+    ws.acts_pending = False
+
+
 def loss_finalize_beside(ws, side_stream, on_losses=None):
     """loss_finalize (+ on_losses(ws.scalars), e.g. the host copy) on `side_stream`, after everything
     queued so far on torch's stream: the backward's G3 does not read the tail's outputs, so it starts
-    right after the loss kernel.  Returns the event the stream must wait for before G4 (whose L1 term
-    reads the tail's activation column sums)."""
+    right after the loss kernel.  Returns the event the stream must wait for before G4 when the tail
+    also forms the activation column sums (G4's L1 term reads them), else None (acts_colsum ran)."""
+    needed = ws.acts_pending
     dev = ws.x.device
     ready = torch.cuda.Event()
     ready.record(torch.cuda.current_stream(dev))
@@ -319,7 +332,7 @@ def loss_finalize_beside(ws, side_stream, on_losses=None):
             on_losses(ws.scalars)
         done = torch.cuda.Event()
         done.record(side_stream)
-    return done
+    return done if needed else None
 
 
 def row_chunks(B, n_chunks):
