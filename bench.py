@@ -15,7 +15,8 @@ real number of activations (batch rows) trained per second by the whole job; `la
 
 The JSON line also carries `roofline` (dominant kernel's achieved TFLOP/s from HIP events around its
 launches inside the timed region, vs the bf16 dense MFMA peak), `hbm` (achieved GB/s of the
-streaming kernels: Adam halves, input prep, loss, W_dec^T pass, from an untimed attribution pass) and
+streaming kernels: Adam halves, input prep, W_dec^T pass -- and the loss kernel where G2 does not carry the
+loss in its epilogue -- from an untimed attribution pass) and
 `cpu_baseline` (the oracle CPU step timed on this host, rank 0, N = 1 only).
 """
 import argparse
@@ -77,7 +78,7 @@ class EventTimer:
 SPAN_EVERY = 4  # timed steps per roofline-kernel sample (events around the launch)
 
 # span name -> kernel-name prefix in the rocprofv3 traces
-SPAN_KERNEL = {"G1_encode": "gemm_pp_kernel<true, true, 1", "G2_decode": "gemm_pp_kernel<true, false, 2",
+SPAN_KERNEL = {"G1_encode": "gemm_pp_kernel<true, true, 1", "G2_decode": "gemm_pp_main_splitk_kernel<true, true, 7",
                "G3_dacts": "gemm_pp_kernel<true, true, 3", "G4G5_wgrad": "gemm_pp_dual_kernel<true, true, 4, 5>",
                "adam": "adam_bulk_kernel"}
 
@@ -288,7 +289,7 @@ def main():
     # algorithmic operand/output bytes of the dominant launch (each input read once, output written once)
     es = 2  # bf16
     alg = {"G1_encode": (B * K + h_local * K + 2 * B * h_local) * es,
-           "G2_decode": (B * h_local + h_local * K) * es + B * K * 4,
+           "G2_decode": (B * h_local + h_local * K + 3 * B * K) * es,  # + x in, g_recon / g_recon^T out (fused loss)
            "G3_dacts": (B * K + h_local * K + 2 * B * h_local) * es,
            "G4G5_wgrad": (2 * B * h_local + 2 * B * K + 3 * h_local * K) * es}
     dom_alg_bytes = alg.get(dom)
