@@ -1176,7 +1176,7 @@ int cc_loss_tail_nb(const float* acts_colpart, int64_t R, int64_t h, float* cols
                     float* l1_part, const float* row_part, int64_t ncb, const float* l0_part, int64_t n_l0, float* ev,
                     float* ev_a, float* ev_b, float* scalars, float* l1l0_out, float* host_out, uint32_t seq,
                     int64_t B, int64_t n, int64_t d, uint32_t* counter, void* stream) {
-  if (!acts_colpart || !colsum_acts || !tn || !l1_part || !row_part || !scalars || !counter) return CC_ERR_NULL;
+  if (!acts_colpart || !tn || !l1_part || !row_part || !scalars || !counter) return CC_ERR_NULL;  // colsum_acts optional
   if (R <= 0 || h <= 0 || B <= 0 || n <= 0 || d <= 0 || ncb <= 0) return CC_ERR_SHAPE;
   TailArgs a = {};
   const int nred = (int)((h + RED_COLS - 1) / RED_COLS);

@@ -230,6 +230,9 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     # x.mean(0) is first read by the loss kernel: reduced here it runs while the stream would
     # otherwise idle waiting for the side stream's decoder-half Adam (G1 starts 8 us earlier)
     ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
+    # sum_b acts (G4's L1 term, crosscoder.py:126) likewise, in the same wait; the l1 dots against the
+    # decoder norms (not known before the side stream's pass) stay in the loss tail
+    ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts)
     P.wait_pending()
     decoder_norms(ws, P)  # (+ W_dec^T), unless launched already after the last Adam
     if loss and ws.fused_ncb:
@@ -243,8 +246,8 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
             ops.decode_partial_t(ws.acts, ws.W_dec_t, ws.recon, ws.dec_ws)
         else:
             ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
-    # sum_b acts (for dL1/dW_dec) and B * l1 = sum_h colsum_acts[h] * tn[h] (crosscoder.py:126) ride in
-    # the loss finaliser's launch (loss_tail)
+    # B * l1 = sum_h colsum_acts[h] * tn[h] (crosscoder.py:126) rides in the loss finaliser's launch
+    # (loss_tail)
     ws.acts_pending = True
     if loss:
         loss_rows(ws, P, 0, ws.B, grad_scale)
@@ -285,7 +288,7 @@ def loss_finalize(ws, l1l0_out=None):
     """Loss scalars / EV vectors.  After a forward (which deferred the activation column sums) one
     launch does both (cc_loss_tail); a re-formed loss (same activations) only the finaliser."""
     if ws.acts_pending:
-        ops.loss_tail(ws.acts_colpart, ws.h, ws.colsum_acts, ws.tn, ws.l1_part, _row_part(ws), ws.l0_part, ws.n_wave,
+        ops.loss_tail(ws.acts_colpart, ws.h, None, ws.tn, ws.l1_part, _row_part(ws), ws.l0_part, ws.n_wave,
                       ws.ev, ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], l1l0_out=l1l0_out,
                       ncb=ws.row_ncb)
         ws.acts_pending = False
@@ -304,24 +307,12 @@ def loss_from_recon(ws, P, grad_scale=None):
     loss_finalize(ws)
 
 
-def acts_colsum(ws):
-    """Sum_b acts (G4's L1 term reads it) and the l1 dot partials against the decoder norms, on torch's
-    stream (the reduction half of the loss tail, same bits): loss_finalize_beside's side-stream launch is
-    then read by nothing on torch's stream, which never waits for it (a cross-stream wait costs ~17 us
-    even on a completed event, profiles/r02_step_ab_prep_ahead.txt)."""
-    if not ws.acts_pending:
-        return
-    ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], ws.h, out_f32=ws.colsum_acts, dot_w=ws.tn,
-                    dot_part=ws.l1_part)
-    ws.acts_pending = False
-
-
 def loss_finalize_beside(ws, side_stream, on_losses=None):
     """loss_finalize (+ on_losses(ws.scalars), e.g. the host copy) on `side_stream`, after everything
     queued so far on torch's stream: the backward's G3 does not read the tail's outputs, so it starts
-    right after the loss kernel.  Returns the event the stream must wait for before G4 when the tail
-    also forms the activation column sums (G4's L1 term reads them), else None (acts_colsum ran)."""
-    needed = ws.acts_pending
+    right after the loss kernel, and nothing on torch's stream reads the tail's outputs (G4's activation
+    column sums come from forward(); a cross-stream wait costs the waiting stream ~17-24 us even on a
+    completed event, profiles/r02_step_ab_prep_ahead.txt).  Returns the event that marks the tail's end."""
     dev = ws.x.device
     ready = torch.cuda.Event()
     ready.record(torch.cuda.current_stream(dev))
@@ -332,7 +323,7 @@ def loss_finalize_beside(ws, side_stream, on_losses=None):
             on_losses(ws.scalars)
         done = torch.cuda.Event()
         done.record(side_stream)
-    return done if needed else None
+    return done
 
 
 def row_chunks(B, n_chunks):

@@ -228,7 +228,8 @@ def loss_finalize(row_part, l1_part, n_l1, l0_part, n_l0, ev, ev_a, ev_b, scalar
 
 def loss_tail(acts_colpart, h, colsum_acts, tn, l1_part, row_part, l0_part, n_l0, ev, ev_a, ev_b, scalars, B, n, d,
               counter, l1l0_out=None, host=None, seq=0, ncb=None):
-    """reduce_rows(acts_colpart, dot_w=tn, dot_part=l1_part) + loss_finalize as one launch (same bits)."""
+    """reduce_rows(acts_colpart, dot_w=tn, dot_part=l1_part) + loss_finalize as one launch (same bits);
+    colsum_acts None: the column sums are not stored (already formed), only the l1 dot partials."""
     if ncb is not None:
         check(lib().cc_loss_tail_nb(_ptr(acts_colpart), acts_colpart.shape[0], h, _ptr(colsum_acts), _ptr(tn),
                                     _ptr(l1_part), _ptr(row_part), ncb, _ptr(l0_part), n_l0, _ptr(ev), _ptr(ev_a),

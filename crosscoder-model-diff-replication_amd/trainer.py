@@ -111,12 +111,11 @@ class Trainer:
         side = self._side_stream()
         # prep, G1, G2 + the loss rows (one pass where decode_loss_t serves the shape)
         engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None, finalize=False)
-        engine.acts_colsum(ws)  # sum_b acts for G4 on this stream: G4 then never waits for the side stream
-        # the loss scalars (+ their host copy) on the side stream, beside G3
-        tail_done = engine.loss_finalize_beside(ws, side, on_losses)
+        # the loss scalars (+ their host copy) on the side stream, beside G3 (read by nothing on this stream)
+        engine.loss_finalize_beside(ws, side, on_losses)
         l1c = self.get_l1_coeff()
         # clip_grad_norm_(max_norm=1.0), trainer.py:46
-        engine.backward(ws, P, opt.grads, l1c, clip=1.0, tail_done=tail_done)
+        engine.backward(ws, P, opt.grads, l1c, clip=1.0)
         g = opt.param_groups[0]
         opt.t += 1
         b1, b2 = g["betas"]

@@ -187,7 +187,9 @@ int cc_loss_finalize_mapped(const float* row_part, const float* l1_part, int64_t
  * -- bit-identical to cc_reduce_rows(.., dot_w = tn, dot_part = l1_part) followed by
  * cc_loss_finalize[_mapped](.., n_l1 = cc_reduce_parts(h), ..).  The last block to finish runs the
  * scalar finaliser; `counter` is one device uint32, zero before the first call, left zero by
- * every call (launches sharing a counter must be ordered, e.g. one stream).  host_out may be NULL. */
+ * every call (launches sharing a counter must be ordered, e.g. one stream).  host_out may be NULL;
+ * colsum_acts may be NULL (the column sums already formed by cc_reduce_rows: only the l1 dot
+ * partials, the same bits). */
 int cc_loss_tail(const float* acts_colpart, int64_t R, int64_t h, float* colsum_acts, const float* tn,
                  float* l1_part, const float* row_part, const float* l0_part, int64_t n_l0, float* ev, float* ev_a,
                  float* ev_b, float* scalars, float* l1l0_out, float* host_out, uint32_t seq, int64_t B, int64_t n,

@@ -98,21 +98,6 @@ class TwoPassLoss:
         self.tr.crosscoder._ws.fused_ncb = self.saved
 
 
-class TailAll:
-    """Variant: Sum_b acts + l1 dots inside the side-stream loss tail (round-2 schedule; G4 waits for its
-    event) instead of a reduce_rows on the main stream before it (engine.acts_colsum)."""
-
-    def __init__(self):
-        from crosscoder_amd import engine
-        self.engine, self.saved = engine, engine.acts_colsum
-
-    def on(self):
-        self.engine.acts_colsum = lambda ws: None
-
-    def off(self):
-        self.engine.acts_colsum = self.saved
-
-
 def flat_dec_adam(blocks):
     from crosscoder_amd import engine
 
@@ -188,8 +173,6 @@ def main():
     variants["dec Adam beside G1 + norms on main"] = (dec_adam_side_norms_main(), None, None)
     tp = TwoPassLoss(tr)
     variants["two-pass decode + loss"] = (shipped, tp.on, tp.off)
-    ta = TailAll()
-    variants["acts colsum in the side tail"] = (shipped, ta.on, ta.off)
     variants["serial Adam + norms beside G1"] = (serial_adam(True), None, None)
     variants["serial Adam + norms before G2"] = (serial_adam(False), None, None)
     variants["G2 from W_dec (no W_dec^T pass)"] = (shipped, g2mn.on, g2mn.off)
