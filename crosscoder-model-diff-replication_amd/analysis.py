@@ -22,6 +22,8 @@ def decoder_stats(cc, shared_range=(0.3, 0.7)):
     a = cc.arena()
     a.wait_pending()
     norms, rel, cos = ops.decoder_stats(a.W_dec_hk, a.n, a.d)
+    if a.padded:  # (the padding columns are zero: the padding latents are dropped)
+        norms, rel, cos = norms[:a.h_ref], rel[:a.h_ref], cos[:a.h_ref]
     lo, hi = shared_range
     return {"norms": norms, "relative_norms": rel, "shared_latent_mask": (rel < hi) & (rel > lo),
             "cosine_sims": cos}
@@ -55,6 +57,6 @@ def sae_vis_export(cross_coder, *scaling_factors, dtype=torch.bfloat16):
     finally:
         cross_coder._ws = ws
     fold_activation_scaling_factor(folded, *scaling_factors, fold_decoder=False)
-    sd = {k: v.detach().to("cpu", dtype) for k, v in folded.state_dict().items()}
+    sd = {k: v.detach().to("cpu", dtype) for k, v in folded.reference_state_dict().items()}
     cfg = {"d_in": cross_coder.cfg["d_in"], "d_hidden": cross_coder.cfg["dict_size"], "apply_b_dec_to_input": False}
     return sd, cfg

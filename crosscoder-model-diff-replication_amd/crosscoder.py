@@ -73,7 +73,10 @@ class CrossCoder(nn.Module):
             raise TypeError("crosscoder_amd kernels support enc_dtype 'bf16' and 'fp32'")
         device = torch.device(cfg["device"])
         W_dec = reference_init(cfg, self.n_models) if init_W_dec is None else init_W_dec.to(self.dtype)
-        self._arena = engine.Arena(d_hidden, self.n_models, d_in, self.dtype, device)
+        # kernel dims: dict_size / d_in rounded up to multiples of 8 (zero padding latents / columns that
+        # stay zero, engine.padded_dims); the parameters are the reference-shaped views
+        self._hp, self._dp = engine.padded_dims(d_hidden, d_in)
+        self._arena = engine.Arena(self._hp, self.n_models, self._dp, self.dtype, device, ref=(d_hidden, d_in))
         with torch.no_grad():
             self._arena.W_dec().copy_(W_dec)
             self._arena.W_enc().copy_(W_dec.permute(1, 2, 0))
@@ -131,7 +134,7 @@ class CrossCoder(nn.Module):
             self._arena.wait_pending()  # the old arena's decoder half may still be written
             prm = self._parameters
             dev = prm["W_dec"].device
-            new = engine.Arena(self.d_hidden, self.n_models, self.cfg["d_in"], self.dtype, dev)
+            new = engine.Arena(self._hp, self.n_models, self._dp, self.dtype, dev, ref=(self.d_hidden, self.cfg["d_in"]))
             with torch.no_grad():
                 for name, dst in new.views().items():
                     dst.copy_(prm[name].data)
@@ -152,14 +155,21 @@ class CrossCoder(nn.Module):
         ws = self._ws
         if (ws is None or ws.B != B or ws.x.device != a.data.device
                 or (ws.busy is not None and ws.busy() is not None)):
-            ws = engine.StepWorkspace(B, self.n_models, self.cfg["d_in"], self.d_hidden, self.dtype, a.data.device)
+            ws = engine.StepWorkspace(B, self.n_models, self._dp, self._hp, self.dtype, a.data.device)
             self._ws = ws
         return ws
 
-    def _flat_x(self, x):
-        x = x.contiguous()
+    def _check_x(self, x):
         if x.dim() != 3 or x.shape[1] != self.n_models or x.shape[2] != self.cfg["d_in"]:
             raise ValueError(f"expected x of shape [batch, {self.n_models}, {self.cfg['d_in']}], got {tuple(x.shape)}")
+
+    def pad_input(self, x):
+        """x [batch, n, d_in] -> [batch, n, kernel d] (zero columns appended when d_in % 8 != 0)."""
+        return x if self._dp == x.shape[-1] else torch.nn.functional.pad(x, (0, self._dp - x.shape[-1]))
+
+    def _flat_x(self, x):
+        self._check_x(x)
+        x = self.pad_input(x).contiguous()
         if x.dtype == self.dtype:
             return x.view(x.shape[0], -1)
         return ops.prep_input(x, None, self.dtype)
@@ -169,19 +179,23 @@ class CrossCoder(nn.Module):
         """x [batch, n_models, d_model] -> acts [batch, d_hidden] (crosscoder.py:69-80)."""
         a = self.arena()
         xf = self._flat_x(x)
-        acts = torch.empty(xf.shape[0], self.d_hidden, dtype=self.dtype, device=xf.device)
+        acts = torch.empty(xf.shape[0], self._hp, dtype=self.dtype, device=xf.device)
         ops.encode_fwd(xf, a.W_enc_hk, a.b_enc, acts, apply_relu)
-        return acts
+        return acts[:, :self.d_hidden].contiguous() if self._hp != self.d_hidden else acts
 
     def decode(self, acts):
         """acts [batch, d_hidden] -> [batch, n_models, d_model] incl. b_dec (crosscoder.py:82-89)."""
         a = self.arena()
         a.wait_pending()
-        acts = acts.to(self.dtype).contiguous()
+        acts = acts.to(self.dtype)
+        if self._hp != self.d_hidden:  # zero activations of the padding latents
+            acts = torch.nn.functional.pad(acts, (0, self._hp - acts.shape[-1]))
+        acts = acts.contiguous()
         B = acts.shape[0]
-        out = torch.empty(B, self.n_models * self.cfg["d_in"], dtype=self.dtype, device=acts.device)
+        out = torch.empty(B, self.n_models * self._dp, dtype=self.dtype, device=acts.device)
         ops.decode_fwd(acts, a.W_dec_hk, a.b_dec_flat, recon_t=out)
-        return out.view(B, self.n_models, self.cfg["d_in"])
+        out = out.view(B, self.n_models, self._dp)
+        return out[:, :, :self.cfg["d_in"]].contiguous() if self._dp != self.cfg["d_in"] else out
 
     def forward(self, x):
         return self.decode(self.encode(x))
@@ -209,8 +223,19 @@ class CrossCoder(nn.Module):
     def save(self):
         if self.save_dir is None:
             self.create_save_dir()
-        self.save_dir, self.save_version = write_checkpoint(self.state_dict(), self.cfg, self.save_dir,
+        self.save_dir, self.save_version = write_checkpoint(self.reference_state_dict(), self.cfg, self.save_dir,
                                                             self.save_version)
+
+    def reference_state_dict(self):
+        """state_dict() in the reference's own tensor layout: the views themselves, or -- when the kernel
+        dims are padded -- compact copies with the reference strides (W_enc [n, d, h] strides (d, 1, n*d))."""
+        sd = self.state_dict()
+        if not self._arena.padded:
+            return sd
+        out = type(sd)()
+        for k, v in sd.items():
+            out[k] = v.permute(2, 0, 1).contiguous().permute(1, 2, 0) if k == "W_enc" else v.contiguous()
+        return out
 
     def _load_checked(self, state_dict):
         self.load_state_dict(state_dict)
@@ -259,9 +284,10 @@ class _LossFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, cc, x, arena_data, W_enc, W_dec, b_enc, b_dec):
+        cc._check_x(x)
         ws = cc._workspace(x.shape[0])
         a = cc.arena()
-        engine.forward(ws, a, x.contiguous(), None)
+        engine.forward(ws, a, cc.pad_input(x).contiguous(), None)
         s = ws.scalars
         dt = cc.dtype
         out = (s[0].clone(), s[1].to(dt, copy=True), s[2].clone(), ws.ev.clone(), ws.ev_a.to(dt, copy=True),
@@ -282,7 +308,7 @@ class _LossFn(torch.autograd.Function):
         w1 = 0.0 if g_l1 is None else float(g_l1)
         if w2 != 1.0:  # g_recon was formed for d(l2)=1; re-form it for this upstream weight
             engine.loss_from_recon(ws, a, grad_scale=2.0 * w2 / ws.B)
-        G = engine.Arena(cc.d_hidden, cc.n_models, cc.cfg["d_in"], cc.dtype, a.data.device)
+        G = a.like()
         engine.backward(ws, a, G, l1_coeff=w1)
         ws.busy = None
         v = G.views()

@@ -42,13 +42,25 @@ def _span(name):
     return TIMER.span(name) if TIMER is not None else contextlib.nullcontext()
 
 
+def padded_dims(h, d):
+    """Kernel dims (h, d) of a crosscoder with dict_size h and d_in d: both rounded up to a multiple of 8
+    (the kernels move 16-byte rows).  The padding latents / columns are zero in every arena and stay
+    zero through the step (their pre-activations, reconstructions, gradients and Adam updates are 0),
+    so the reference-shaped views see exactly the reference crosscoder."""
+    return -(-h // 8) * 8, -(-d // 8) * 8
+
+
 class Arena:
     """Flat storage for the four parameters (or their grads / Adam moments):
     [ W_enc h-major [h][K] | b_enc [h] | W_dec [h][K] | b_dec [K] ] -- the encoder half and the
-    decoder half are contiguous, so Adam can update them as two launches (enc_part / dec_part)."""
+    decoder half are contiguous, so Adam can update them as two launches (enc_part / dec_part).
+    h, d are the kernel dims (padded_dims); ref = (dict_size, d_in) of the reference-shaped views
+    when they differ."""
 
-    def __init__(self, h, n, d, dtype, device, data=None):
+    def __init__(self, h, n, d, dtype, device, data=None, ref=None):
         self.h, self.n, self.d = h, n, d
+        self.h_ref, self.d_ref = ref if ref is not None else (h, d)
+        self.padded = (self.h_ref, self.d_ref) != (h, d)
         K = n * d
         self.K = K
         self.numel = 2 * h * K + h + K
@@ -76,23 +88,31 @@ class Arena:
             torch.cuda.current_stream(self.data.device).wait_event(self.pending)
             self.pending = None
 
-    # reference-shaped views
+    def like(self, dtype=None, device=None):
+        """A zeroed arena of the same dims (grads / Adam moments)."""
+        return Arena(self.h, self.n, self.d, dtype or self.data.dtype, device or self.data.device,
+                     ref=(self.h_ref, self.d_ref))
+
+    # reference-shaped views ([:h_ref] latents, [:d_ref] columns per model of the kernel layout)
     def W_enc(self):  # [n, d, h], strides (d, 1, K)
-        return self.W_enc_hk.view(self.h, self.n, self.d).permute(1, 2, 0)
+        v = self.W_enc_hk.view(self.h, self.n, self.d)
+        if self.padded:
+            v = v[:self.h_ref, :, :self.d_ref]
+        return v.permute(1, 2, 0)
 
     def W_dec(self):  # [h, n, d]
-        return self.W_dec_hk.view(self.h, self.n, self.d)
+        v = self.W_dec_hk.view(self.h, self.n, self.d)
+        return v[:self.h_ref, :, :self.d_ref] if self.padded else v
+
+    def b_enc_ref(self):  # [h]
+        return self.b_enc[:self.h_ref] if self.padded else self.b_enc
 
     def b_dec(self):  # [n, d]
-        return self.b_dec_flat.view(self.n, self.d)
+        v = self.b_dec_flat.view(self.n, self.d)
+        return v[:, :self.d_ref] if self.padded else v
 
     def views(self):
-        return {"W_enc": self.W_enc(), "W_dec": self.W_dec(), "b_enc": self.b_enc, "b_dec": self.b_dec()}
-
-    def param_sizes(self):
-        """numel of W_enc, W_dec, b_enc, b_dec (the reference's parameters() order)."""
-        hk = self.h * self.K
-        return [hk, hk, self.h, self.K]
+        return {"W_enc": self.W_enc(), "W_dec": self.W_dec(), "b_enc": self.b_enc_ref(), "b_dec": self.b_dec()}
 
 
 class StepWorkspace:

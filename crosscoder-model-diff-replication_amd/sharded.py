@@ -132,9 +132,9 @@ class HipShardBackend:
         self.cc = cc
         self.side = torch.cuda.Stream(device=cc.arena().data.device) if overlap_decoder_adam else None
         a = cc.arena()
-        self.G = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
-        self.M = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
-        self.V = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
+        self.G = a.like()
+        self.M = a.like()
+        self.V = a.like()
         self.red = torch.zeros(6, dtype=torch.float32, device=a.data.device)
         self.recon_chunks = recon_chunks
         self.ws = None
@@ -142,7 +142,7 @@ class HipShardBackend:
     def forward_partial(self, raw, factor):
         cc = self.cc
         ws = self.ws = cc._workspace(raw.shape[0])
-        engine.forward(ws, cc.arena(), raw, factor, loss=False)  # G1, norms, G2 -> fp32 partial recon
+        engine.forward(ws, cc.arena(), cc.pad_input(raw), factor, loss=False)  # G1, norms, G2 -> fp32 partial recon
         return ws.recon
 
     def row_chunks(self):

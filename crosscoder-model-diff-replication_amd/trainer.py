@@ -33,9 +33,9 @@ class FusedAdam:
     def __init__(self, cc, lr, betas, eps=1e-8):
         a = cc.arena()
         self.cc = cc
-        self.exp_avg = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
-        self.exp_avg_sq = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
-        self.grads = engine.Arena(a.h, a.n, a.d, a.data.dtype, a.data.device)
+        self.exp_avg = a.like()
+        self.exp_avg_sq = a.like()
+        self.grads = a.like()
         self.param_groups = [{"lr": lr, "initial_lr": lr, "betas": betas, "eps": eps, "weight_decay": 0.0}]
         self.t = 0
 
@@ -105,6 +105,7 @@ class Trainer:
         backward / clip / Adam launches."""
         cc = self.crosscoder
         raw, factor = self.buffer.next_raw()
+        raw = cc.pad_input(raw)  # (zero columns only when d_in % 8 != 0)
         ws = cc._workspace(raw.shape[0], step=True)
         P = cc.arena()
         opt = self.optimizer

@@ -13,7 +13,8 @@
  *    All accumulations are fp32 (bf16 inputs go through bf16 MFMA with fp32 accumulate,
  *    fp32 inputs through the exact-f32 MFMA).
  *  - Shapes: B batch rows, n models, d d_model, h dict_size, K = n*d.
- *    Requirements: d % 8 == 0, h % 8 == 0 (16-byte vector rows); any B >= 1.
+ *    Requirements: d % 8 == 0, h % 8 == 0 (16-byte vector rows); any B >= 1.  (The Python layer
+ *    serves other dict_size / d_in on zero-padded dims: crosscoder_amd.engine.padded_dims.)
  *  - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream); all launches are
  *    asynchronous on it.  No entry point synchronises, allocates, or keeps global state.
  *  - Return value: 0 = CC_OK, else a CC_ERR_* code (>= CC_ERR_HIP_BASE: hipError_t + base).

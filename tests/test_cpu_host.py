@@ -212,3 +212,31 @@ def test_buffer_norm_factors_match_reference():
     f = [buf.estimate_norm_scaling_factor(cfg["model_batch_size"], FakeLM(r[f"{m}_table"], r[f"{m}_pos"]))
          for m in ("A", "B")]
     assert torch.equal(torch.tensor(f, dtype=torch.float32), r["normalisation_factor"])
+
+
+def test_odd_shapes_keep_reference_params():
+    """dict_size / d_in that are not multiples of 8: the kernels run on zero-padded dims
+    (engine.padded_dims), the parameters are the reference-shaped views -- the same values as the
+    reference init, a zero padding around them, and reference_state_dict() in the reference's own
+    strides (the checkpoint format)."""
+    cfg = _cfg("fp32", h=203, d=37)
+    cc = ca.CrossCoder(cfg)
+    ref = O.init_params(cfg)
+    a = cc.arena()
+    assert (a.h, a.d) == (208, 40) and a.padded
+    for k in O.PARAM_ORDER:
+        p = getattr(cc, k)
+        assert p.shape == ref[k].shape and torch.equal(p.detach(), ref[k]), k
+    # everything outside the views is zero
+    mask = torch.ones_like(a.data, dtype=torch.bool)
+    for v in a.views().values():
+        v_full = torch.zeros_like(a.data, dtype=torch.bool)
+        v_full.as_strided(v.shape, v.stride(), v.storage_offset())[...] = True
+        mask &= ~v_full
+    assert float(a.data[mask].abs().sum()) == 0.0
+    sd = cc.reference_state_dict()
+    for k in O.PARAM_ORDER:
+        assert sd[k].stride() == ref[k].stride() and torch.equal(sd[k], ref[k]), k
+    cc2 = ca.CrossCoder(dict(cfg, seed=1))
+    cc2.load_state_dict(sd)
+    assert all(torch.equal(getattr(cc2, k).detach(), ref[k]) for k in O.PARAM_ORDER)

@@ -1102,3 +1102,86 @@ def test_sae_vis_export_matches_notebook_fold(gpu):
         assert torch.equal(sd[k], ref[k]), k
     for k, v in r["init"].items():  # the source crosscoder is unchanged
         assert torch.equal(cc.state_dict()[k].cpu(), v), k
+
+
+# ----------------------------------------------------------------------------- shapes off the 8-grid
+@pytest.mark.parametrize("enc_dtype,B,n,d,h", [("fp32", 64, 2, 37, 203), ("fp32", 48, 3, 20, 100),
+                                               ("bf16", 96, 2, 37, 203)])
+def test_odd_shapes_match_oracle(gpu, enc_dtype, B, n, d, h):
+    """dict_size / d_in that are not multiples of 8 (the reference takes any shape; the kernels move
+    16-byte rows): the crosscoder runs on zero-padded kernel dims and its reference-shaped parameters,
+    encode / decode, get_losses + autograd and three Trainer steps match the oracle (fp32: the
+    fixtures' tolerances; bf16: the reference's own bf16 envelope), and the padding stays zero."""
+    cfg = {"seed": 13, "batch_size": B, "buffer_mult": 128, "lr": 5e-5, "num_tokens": B * 4, "l1_coeff": 2,
+           "beta1": 0.9, "beta2": 0.999, "dict_size": h, "seq_len": 1024, "enc_dtype": enc_dtype,
+           "device": str(gpu), "dec_init_norm": 0.08, "d_in": d, "log_every": 100, "save_every": 30000}
+    dt = O.DTYPES[enc_dtype]
+    cc = ca.CrossCoder(cfg, n_models=n)
+    P = O.init_params(cfg, n_models=n)
+    for k in O.PARAM_ORDER:
+        assert torch.equal(getattr(cc, k).detach().cpu(), P[k]), k
+    g = torch.Generator().manual_seed(B + d)
+    x = (torch.randn(B, n, d, generator=g) * 2).to(dt)
+    fp32 = dt == torch.float32
+    # encode / decode / forward
+    acts = cc.encode(x.to(gpu)).cpu()
+    recon = cc.decode(acts.to(gpu)).cpu()
+    assert acts.shape == (B, h) and recon.shape == (B, n, d)
+    with torch.no_grad():
+        acts_ref = O.encode(x.double(), {k: v.double() for k, v in P.items()})
+        recon_ref = O.decode(acts.double(), {k: v.double() for k, v in P.items()})
+    assert rel(acts, acts_ref) < (2e-5 if fp32 else 8e-3)
+    assert rel(recon, recon_ref) < (2e-5 if fp32 else 8e-3)
+    # get_losses + backward vs the oracle (fp64 truth on the same inputs)
+    lo = cc.get_losses(x.to(gpu))
+    (lo.l2_loss + 2.0 * lo.l1_loss).backward()
+    torch.cuda.synchronize()
+    P_ref = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    lo_ref = O.get_losses(x, P_ref, dt)
+    (lo_ref["l2_loss"] + 2.0 * lo_ref["l1_loss"]).backward()
+    lo64, g64, _ = truth_fp64(x, P, 2.0)
+    for f in ("l2_loss", "l1_loss"):
+        ours, truth = getattr(lo, f).double().cpu(), lo64[f].detach()
+        if fp32:
+            assert rel(ours, truth) < 2e-5, f
+        else:
+            ok, e = envelope_ok(ours, lo_ref[f].detach(), truth)
+            assert ok, (f, e)
+    for k in O.PARAM_ORDER:
+        gk = getattr(cc, k).grad
+        assert gk is not None and gk.shape == P[k].shape, k
+        if fp32:
+            assert rel(gk, g64[k]) < 2e-5, k
+        else:
+            ok, e = envelope_ok(gk, P_ref[k].grad, g64[k], floor=2e-2 if k == "W_enc" else 2e-3)
+            assert ok, (k, e)
+    # three Trainer steps vs the oracle trainer on the same normalised batches
+    cc2 = ca.CrossCoder(cfg, n_models=n)
+    bufs = [(torch.randn(B, n, d, generator=g) * 3).to(dt) for _ in range(3)]
+    factors = [torch.tensor([0.7, 1.3, 0.9][:n]).to(dt) for _ in range(3)]
+    tr = ca.Trainer(cfg, buffer=_Replay(bufs, factors, gpu), crosscoder=cc2)
+    ref_tr = O.OracleTrainer(dict(cfg, device="cpu"), P, n_models=n)
+    for s in range(3):
+        dd = tr.step()
+        dr = ref_tr.step(O.buffer_next(bufs[s], factors[s]))
+        assert list(dd) == list(dr)
+        tol = 1e-5 if fp32 else 2e-3
+        for k in ("l2_loss", "l1_loss", "explained_variance"):
+            assert abs(dd[k] - dr[k]) <= tol * max(1.0, abs(dr[k])), (s, k, dd[k], dr[k])
+    tr.synchronize()
+    lr = cfg["lr"]
+    for k in O.PARAM_ORDER:
+        p, pr = getattr(cc2, k).detach().cpu().float(), ref_tr.P[k].detach().float()
+        diff = (p - pr).abs()
+        if fp32:  # (m / sqrt(v) of near-zero gradients amplifies fp32 summation-order differences; a
+            # Trainer whose Adam does not run is ~3 lr off)
+            assert diff.max().item() <= 0.05 * lr, (k, diff.max().item() / lr)
+        else:
+            assert (diff <= 2 * _bf16_ulp(pr) + 3 * lr).all(), (k, (diff / lr).max().item())
+    a = cc2.arena()
+    assert a.padded
+    Wenc = a.W_enc_hk.view(a.h, n, a.d)
+    assert float(Wenc[h:].abs().sum()) == 0.0 and float(Wenc[:, :, d:].abs().sum()) == 0.0
+    Wdec = a.W_dec_hk.view(a.h, n, a.d)
+    assert float(Wdec[h:].abs().sum()) == 0.0 and float(Wdec[:, :, d:].abs().sum()) == 0.0
+    assert float(a.b_enc[h:].abs().sum()) == 0.0 and float(a.b_dec_flat.view(n, a.d)[:, d:].abs().sum()) == 0.0
