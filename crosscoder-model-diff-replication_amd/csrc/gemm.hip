@@ -24,6 +24,8 @@
 //                               bf16 / ds_read_b32 fp32), rot chosen conflict-free per geometry.
 // One s_barrier per K-step: wait own DMA (vmcnt 0) -> barrier -> issue DMA of step t+1 into the
 // other stage -> MFMA on stage t.  All LDS is one __shared__ array.
+#include <mutex>
+
 #include "cc_common.h"
 
 namespace cc {
@@ -678,6 +680,26 @@ static int launch(GemmArgs a, hipStream_t st) {
   return CC_OK;
 }
 
+// grid of a ping-pong launch over `tiles` output tiles: one workgroup per tile, or (persistent tile loop)
+// at most one per CU
+static int pp_grid(int64_t tiles) {
+#if CC_PP_PERSIST
+  static int cus = 0;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                 hipSuccess && n > 0)
+      cus = n;
+    else
+      cus = 256;
+  });
+  return (int)(tiles < cus ? tiles : cus);
+#else
+  return (int)tiles;
+#endif
+}
+
 #ifndef CC_PP_FAST  // the epilogue fast form for whole-tile ReLU launches (0: general form, A/B)
 #define CC_PP_FAST 1
 #endif
@@ -692,12 +714,12 @@ static int launch_pp(GemmArgs a, hipStream_t st) {
   a.nbn = (a.N + 255) / 256;
   if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
     if (g_pp_fast && a.M % BM == 0 && a.N % 256 == 0 && (EPI == EPI_DACTS || a.flag)) {  // whole tiles, ReLU on
-      hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI, true>), dim3(a.nbm * a.nbn), dim3(NTHR), 0, st, a);
+      hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI, true>), dim3(pp_grid(a.nbm * a.nbn)), dim3(NTHR), 0, st, a);
       CC_LAUNCH_CHECK();
       return CC_OK;
     }
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI>), dim3(a.nbm * a.nbn), dim3(NTHR), 0, st, a);
+  hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI>), dim3(pp_grid(a.nbm * a.nbn)), dim3(NTHR), 0, st, a);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }
@@ -1089,8 +1111,9 @@ int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, c
   a.nbn = (a.N + 255) / 256;
   const bool fast = B % BM == 0 && a.N % 256 == 0;
   if (!split) {
-    if (fast) hipLaunchKernelGGL((gemm_pp_kernel<true, true, EPI_DLOSS, true>), dim3(a.nbm * a.nbn), dim3(NTHR), 0, st, a);
-    else hipLaunchKernelGGL((gemm_pp_kernel<true, true, EPI_DLOSS>), dim3(a.nbm * a.nbn), dim3(NTHR), 0, st, a);
+    const dim3 grid(pp_grid(a.nbm * a.nbn));
+    if (fast) hipLaunchKernelGGL((gemm_pp_kernel<true, true, EPI_DLOSS, true>), grid, dim3(NTHR), 0, st, a);
+    else hipLaunchKernelGGL((gemm_pp_kernel<true, true, EPI_DLOSS>), grid, dim3(NTHR), 0, st, a);
     CC_LAUNCH_CHECK();
     return CC_OK;
   }
@@ -1223,7 +1246,7 @@ int cc_wgrad_both_t(const void* actsT, const void* g_reconT, const void* W_dec, 
   a0.dbg = a1.dbg = g_stamp_buf;
   a1.stamp_base = 4 * a0.nbm * a0.nbn;
 #endif
-  hipLaunchKernelGGL((gemm_pp_dual_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(2 * a0.nbm * a0.nbn), dim3(NTHR),
+  hipLaunchKernelGGL((gemm_pp_dual_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(pp_grid(2 * a0.nbm * a0.nbn)), dim3(NTHR),
                      0, st, a0, a1);
   CC_LAUNCH_CHECK();
   return CC_OK;
@@ -1250,7 +1273,8 @@ int cc_wgrad_both(const void* acts, const void* g_recon, const void* W_dec, cons
   a0.dbg = a1.dbg = g_stamp_buf;
   a1.stamp_base = 4 * a0.nbm * a0.nbn;
 #endif
-  hipLaunchKernelGGL((gemm_pp_dual_kernel<false, false, EPI_WGDEC, EPI_WGENC>), dim3(2 * a0.nbm * a0.nbn), dim3(NTHR),
+  hipLaunchKernelGGL((gemm_pp_dual_kernel<false, false, EPI_WGDEC, EPI_WGENC>), dim3(pp_grid(2 * a0.nbm * a0.nbn)),
+                     dim3(NTHR),
                      0, st, a0, a1);
   CC_LAUNCH_CHECK();
   return CC_OK;

@@ -229,14 +229,14 @@ constexpr int PP_LDS_W = PP_LDS;
 // One output tile of one GEMM; bid = the tile's block index within that GEMM's grid.  FAST: every tile
 // of the launch lies inside the matrix and the ReLU is on (EPI_ENC / EPI_DACTS epilogue fast form).
 template <bool AKC, bool BKC, int EPI, bool FAST = false>
-CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid) {
+CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadIdx.x) {
   using WG = WaveGeom<256>;
   static_assert(WG::TM == 8 && WG::TN == 4, "ping-pong geometry");
   constexpr int TILE = 256 * 128;  // one operand's K-step image
   constexpr int BUF = 2 * TILE;
 
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   if (CC_PP_PRIO_BASE) __builtin_amdgcn_s_setprio(CC_PP_PRIO_BASE);
   int tm, tn;
@@ -519,9 +519,38 @@ CC_DEV void pp_stamp_end(const GemmArgs& a, int bid, uint64_t t0) {
 }
 #endif
 
+// Persistent tile loop (CC_PP_PERSIST): grid = min(tiles, CUs) workgroups, workgroup b runs tiles b, b + grid,
+// ... -- the same tile -> XCD map as one tile per workgroup (t % 8 == b % 8), without a workgroup
+// launch per tile, and the next tile's first operand DMAs fly while this tile's epilogue stores drain.
+// Between tiles every wave's LDS reads of the epilogue image must be done before any wave's DMAs
+// overwrite it: lgkmcnt(0) + s_barrier (no vmcnt wait: the stores keep draining).
+#ifndef CC_PP_PERSIST
+#define CC_PP_PERSIST 1
+#endif
+CC_DEV void pp_tile_boundary() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+}
+// threadIdx.x as a value the compiler cannot prove loop-invariant: every per-lane offset of a tile is
+// then computed inside the tile (hoisted out of the tile loop they would stay live through the K loop:
+// ~45 more VGPRs, which also keep the side-stream kernels off the GEMM's SIMDs)
+CC_DEV int pp_opaque_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 template <bool AKC, bool BKC, int EPI, bool FAST = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(16))) char smem[EPI == EPI_WGDEC ? PP_LDS_W : PP_LDS];
+#if CC_PP_PERSIST
+  const int nt = args.nbm * args.nbn;
+  for (int t = blockIdx.x; t < nt; t += gridDim.x) {
+    pp_tile<AKC, BKC, EPI, FAST>(args, smem, t, pp_opaque_tid());
+    pp_tile_boundary();
+  }
+  return;
+#endif
 #ifdef CC_EXP_STAGGER  // timing-only experiment build (never shipped): half the first-round blocks start ~CC_EXP_STAGGER x 4 us
 #ifndef CC_EXP_STAGGER_XCD  // late: every other block of each XCD (0), or the odd XCDs' blocks (1)
 #define CC_EXP_STAGGER_XCD 0
@@ -545,6 +574,15 @@ template <bool AKC, bool BKC, int EPI0, int EPI1>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_kernel(const GemmArgs a0, const GemmArgs a1) {
   __shared__ __attribute__((aligned(16))) char smem[EPI0 == EPI_WGDEC || EPI1 == EPI_WGDEC ? PP_LDS_W : PP_LDS];
   const int nb0 = a0.nbm * a0.nbn;
+#if CC_PP_PERSIST
+  for (int t = blockIdx.x; t < 2 * nb0; t += gridDim.x) {
+    const int tid = pp_opaque_tid();
+    if (t < nb0) pp_tile<AKC, BKC, EPI0>(a0, smem, t, tid);
+    else pp_tile<AKC, BKC, EPI1>(a1, smem, t - nb0, tid);
+    pp_tile_boundary();
+  }
+  return;
+#endif
 #ifdef CC_PP_STAMPS
   const uint64_t t0 = pp_stamp_start();
 #endif
