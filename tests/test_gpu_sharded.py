@@ -21,7 +21,7 @@ def _cfg(device):
             "dec_init_norm": 0.08, "d_in": D, "log_every": 100, "save_every": 30000}
 
 
-def _rank(rank, world, port, q, comm, tmpdir):
+def _rank(rank, world, port, q, comm, tmpdir, received):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -40,6 +40,9 @@ def _rank(rank, world, port, q, comm, tmpdir):
         ccmod.SAVE_DIR = __import__("pathlib").Path(tmpdir) / "checkpoints"
         tr.save()
         q.put((rank, dicts, sd if rank == 0 else None))
+        # CPU tensors travel as shared-memory fds this process serves: stay alive until the
+        # parent has unpickled them
+        received.wait(240)
     finally:
         dist.destroy_process_group()
 
@@ -54,13 +57,16 @@ def test_sharded_world2_on_one_gpu_matches_trainer(gpu, comm, tmp_path):
     port = 29000 + random.randint(0, 900)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, q, comm, str(tmp_path))) for r in range(world)]
+    received = ctx.Event()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q, comm, str(tmp_path), received))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = {}
     for _ in range(world):
         r, dicts, sd = q.get(timeout=240)
         res[r] = (dicts, sd)
+    received.set()
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -150,7 +150,9 @@ def _worker(rank, world, port, q, comm):
             if cb is not None:
                 assert torch.equal(seen[-1], red[4:6])
             outs.append(torch.stack([s[0], red[4], red[5]]).clone())
-        q.put((rank, [o.tolist() for o in outs], {k: v.detach().clone() for k, v in backend.P.items()}))
+        # numpy arrays pickle by value: a torch tensor would travel as a shared-memory fd that the
+        # parent can only open while this process is still alive
+        q.put((rank, [o.tolist() for o in outs], {k: v.detach().numpy().copy() for k, v in backend.P.items()}))
     finally:
         dist.destroy_process_group()
 
@@ -196,7 +198,7 @@ def test_sharded_step_matches_unsharded(world, comm):
             assert abs(l0 - lo["l0_loss"].item()) <= 1e-6
     for r in range(world):
         lo_, hi_ = sharded.shard_range(H, world, r)
-        Pl = res[r][1]
+        Pl = {k: torch.from_numpy(a) for k, a in res[r][1].items()}
         torch.testing.assert_close(Pl["W_dec"], ref["W_dec"].detach()[lo_:hi_], rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(Pl["W_enc"], ref["W_enc"].detach()[:, :, lo_:hi_], rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(Pl["b_enc"], ref["b_enc"].detach()[lo_:hi_], rtol=1e-5, atol=1e-6)
