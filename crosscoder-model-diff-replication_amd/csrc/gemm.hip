@@ -633,6 +633,64 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 }
 
 #include "gemm_pp.h"
+#include "grad_tail.h"
+
+// ---- G4 + G5 with the gradient tail in the same launch (the single-GPU step's backward end).
+// What the stand-alone tail kernel (cc_grad_tail) runs after the weight-gradient GEMMs, here inside
+// their persistent launch, so the step loses a kernel boundary and a launch:
+//   (1) before its first tile, 256-thread group g of workgroup b runs bias reduction blocks
+//       2b + g, 2b + g + 2 * grid, ... (b_enc.grad / b_dec.grad column sums of the G3 / loss partial
+//       slabs + their sq partials: reduce_rows_phase1/2, the bits cc_grad_tail writes);
+//   (2) the dual tile loop of gemm_pp_dual_kernel;
+//   (3) the last workgroup to arrive (device-scope arrival counter, reset by it for the next launch)
+//       runs clip_body over the squared-sum slab the whole grid wrote: clip_grad_norm_'s coefficient.
+struct WgradTail {
+  RedSeg red[2];
+  int red_blocks[2];
+  ClipArgs clip;
+  unsigned* counter;
+};
+
+template <bool AKC, bool BKC, int EPI0, int EPI1>
+__global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmArgs a0, const GemmArgs a1,
+                                                                   const WgradTail tl) {
+  __shared__ __attribute__((aligned(16))) char smem[EPI0 == EPI_WGDEC || EPI1 == EPI_WGDEC ? PP_LDS_W : PP_LDS];
+  {
+    const int grp = threadIdx.x >> 8, t = threadIdx.x & 255;
+    float(*red)[RED_COLS] = (float(*)[RED_COLS])(smem + grp * 4 * RED_COLS * sizeof(float));
+    const int nred = tl.red_blocks[0] + tl.red_blocks[1];
+    for (int base = 2 * (int)blockIdx.x; base < nred; base += 2 * (int)gridDim.x) {  // uniform per workgroup
+      const int b = base + grp;
+      const int role = b < tl.red_blocks[0] ? 0 : 1, rb = role ? b - tl.red_blocks[0] : b;
+      if (b < nred) reduce_rows_phase1(tl.red[role], rb, t, red);
+      __syncthreads();
+      if (b < nred) reduce_rows_phase2<CC_BF16>(tl.red[role], rb, t, red);
+      __syncthreads();
+    }
+  }
+  const int nb0 = a0.nbm * a0.nbn;
+  for (int t = blockIdx.x; t < 2 * nb0; t += gridDim.x) {
+    const int tid = pp_opaque_tid();
+    if (t < nb0) pp_tile<AKC, BKC, EPI0>(a0, smem, t, tid);
+    else pp_tile<AKC, BKC, EPI1>(a1, smem, t - nb0, tid);
+    pp_tile_boundary();
+  }
+  // publish: every wave waits for its own stores (the last tile's sq partials among them), the
+  // barrier joins the waves, ONE agent-scope release writes this XCD's L2 back before the arrival count
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  int* last = (int*)smem;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const bool is_last = atomicAdd(tl.counter, 1u) == gridDim.x - 1;
+    if (is_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // drop stale lines before the reads
+    *last = is_last;
+  }
+  __syncthreads();
+  if (!*last) return;
+  clip_body<NTHR>(tl.clip, (double(*)[NTHR / 64])(smem + 64), (float*)(smem + 64 + 8 * (NTHR / 64) * sizeof(double)));
+  if (threadIdx.x == 0) atomicExch(tl.counter, 0u);
+}
 
 // N = n*d multiple of 288 (and an MN-contiguous bf16 B operand): 256 x 288 tiles.  (The fp32
 // parity mode keeps 256 x 256: its 288-wide variant exceeds 256 VGPRs.)
@@ -1248,6 +1306,52 @@ int cc_wgrad_both_t(const void* actsT, const void* g_reconT, const void* W_dec, 
 #endif
   hipLaunchKernelGGL((gemm_pp_dual_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(pp_grid(2 * a0.nbm * a0.nbn)), dim3(NTHR),
                      0, st, a0, a1);
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
+
+int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
+                         const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_preT,
+                         const void* xT, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
+                         const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
+                         const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
+                         const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
+                         uint32_t* counter, int dtype, void* stream) {
+  const int64_t K = n * d;
+  if (!gpre_colpart || !g_b_enc || !sq_b_enc || !loss_colpart || !g_b_dec || !sq_b_dec || !sq || !off || !clip_out ||
+      !counter)
+    return CC_ERR_NULL;
+  if (R_enc <= 0 || R_dec <= 0) return CC_ERR_SHAPE;
+  if (nparams <= 0 || nparams > 8) return CC_ERR_SHAPE;
+  GemmArgs a0, a1;
+  int rc = wgrad_dec_args(a0, actsT, g_reconT, W_dec, inv_norms, colsum_acts, l1_scale, grad_W_dec, sq_dec, B, h, n,
+                          d, dtype, true);
+  if (rc) return rc;
+  rc = wgrad_enc_args(a1, g_preT, xT, grad_W_enc, sq_enc, B, h, K, dtype, true);
+  if (rc) return rc;
+  if (dtype != CC_BF16 || !use_pp(a0.N, true, true, dtype)) {  // the two GEMMs, then the stand-alone tail
+    rc = cc_wgrad_both_t(actsT, g_reconT, W_dec, inv_norms, colsum_acts, l1_scale, grad_W_dec, sq_dec, g_preT, xT,
+                         grad_W_enc, sq_enc, B, h, n, d, dtype, stream);
+    if (rc) return rc;
+    return cc_grad_tail(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec, sq_b_dec, dtype,
+                        sq, off, nparams, max_norm, emulate_bf16, clip_out, counter, stream);
+  }
+  a0.nbm = a1.nbm = (a0.M + BM - 1) / BM;
+  a0.nbn = a1.nbn = (a0.N + 255) / 256;
+  WgradTail tl = {};
+  tl.red[0] = {gpre_colpart, (int)R_enc, (int)h, h, 1.f, nullptr, g_b_enc, sq_b_enc, nullptr, nullptr};
+  tl.red[1] = {loss_colpart, (int)R_dec, (int)K, K, 1.f, nullptr, g_b_dec, sq_b_dec, nullptr, nullptr};
+  tl.red_blocks[0] = (int)((h + RED_COLS - 1) / RED_COLS);
+  tl.red_blocks[1] = (int)((K + RED_COLS - 1) / RED_COLS);
+  tl.clip.sq = sq;
+  for (int i = 0; i <= nparams; ++i) tl.clip.off[i] = off[i];
+  tl.clip.nparams = nparams;
+  tl.clip.max_norm = max_norm;
+  tl.clip.emulate_bf16 = emulate_bf16;
+  tl.clip.out = clip_out;
+  tl.counter = counter;
+  hipLaunchKernelGGL((gemm_pp_dual_tail_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(pp_grid(2 * a0.nbm * a0.nbn)),
+                     dim3(NTHR), 0, (hipStream_t)stream, a0, a1, tl);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }

@@ -7,6 +7,8 @@
 
 namespace cc {
 
+#include "grad_tail.h"
+
 constexpr int PREP_ROWS = 64;   // rows per prep block (column partial granularity)
 constexpr int LOSS_ROWS = 32;   // rows per loss block
 constexpr int LOSS_COLS = 512;  // columns per loss block (64 lanes x 8)
@@ -125,68 +127,6 @@ __global__ __launch_bounds__(256) void prep_kernel(const void* __restrict__ x_in
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// out[j] = scale * sum_i part[i*ld + j]; optional dtype copy, squared-sum partial per block and
-// dot partial per block (sum_j out[j] * dot_w[j]: the L1 loss from the activation column sums).
-// Block = 64 columns x 4 waves; wave w sums rows w, w+4, ... (independent loads in flight),
-// then a fixed-order combine of the 4 wave partials.  One sq / dot partial per block.
-constexpr int RED_COLS = 64;
-// Phase 1 (all 4 waves of a 256-thread group, t = thread in the group): column sums into red;
-// phase 2 (after a barrier, wave 0 of the group): outputs + the group's sq / dot partial.  The
-// stand-alone kernel and the fused tail kernels (grad_tail / loss_tail) run the same two phases.
-struct RedSeg {
-  const float* part;
-  int R, C;
-  int64_t ld;
-  float scale;
-  float* out_f32;
-  void* out_t;
-  float* sq_part;
-  const float* dot_w;
-  float* dot_part;
-};
-CC_DEV void reduce_rows_phase1(const RedSeg& a, int blk, int t, float (*red)[RED_COLS]) {
-  const int lane = t & 63, wave = t >> 6;
-  const int j = blk * RED_COLS + lane;
-  float s = 0.f;
-  if (j < a.C) {
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    int i = wave;
-    for (; i + 12 < a.R; i += 16) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] += a.part[(int64_t)(i + 4 * u) * a.ld + j];
-    }
-    for (; i < a.R; i += 4) v[0] += a.part[(int64_t)i * a.ld + j];
-    s = (v[0] + v[1]) + (v[2] + v[3]);
-  }
-  red[wave][lane] = s;
-}
-template <int DT>
-CC_DEV void reduce_rows_phase2(const RedSeg& a, int blk, int t, float (*red)[RED_COLS]) {
-  if ((t >> 6) != 0) return;
-  const int lane = t & 63;
-  const int j = blk * RED_COLS + lane;
-  float sq = 0.f, dot = 0.f;
-  if (j < a.C) {
-    float s = (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]) * a.scale;
-    if (a.out_f32) a.out_f32[j] = s;
-    if (a.out_t) {
-      typename Elem<DT>::T q = Elem<DT>::from_f(s);
-      ((typename Elem<DT>::T*)a.out_t)[j] = q;
-      float vq = Elem<DT>::to_f(q);
-      sq = vq * vq;
-    }
-    if (a.dot_part) dot = s * a.dot_w[j];
-  }
-  if (a.sq_part) {
-    sq = wave_sum(sq);
-    if (lane == 0) a.sq_part[blk] = sq;
-  }
-  if (a.dot_part) {
-    dot = wave_sum(dot);
-    if (lane == 0) a.dot_part[blk] = dot;
-  }
-}
 template <int DT>
 __global__ __launch_bounds__(256) void reduce_rows_kernel(const RedSeg a) {
   __shared__ float red[4][RED_COLS];
@@ -478,86 +418,11 @@ CC_DEV void loss_scalars_body(const ScalArgs& sa) {
 __global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const ScalArgs a) { loss_scalars_body(a); }
 
 // ---------------------------------------------------------------------------------------
-CC_DEV float bf16r(float f) { return bf2f(f2bf(f)); }
-
-struct ClipArgs {
-  const float* sq;
-  int64_t off[9];
-  int nparams;
-  float max_norm;
-  int emulate_bf16;
-  float* out;
-  int sums_only;   // cc_segment_sums: out[p] = the raw per-parameter sum (0 where zero_mask has bit p)
-  int zero_mask;
-};
-// 1024 threads (SCAL_THREADS), one block
-CC_DEV void clip_body(const ClipArgs& a) {
-  constexpr int NW = SCAL_THREADS / 64;
-  __shared__ double red[8][NW];
+__global__ __launch_bounds__(SCAL_THREADS) void clip_kernel(const ClipArgs a) {
+  __shared__ double red[8][SCAL_THREADS / 64];
   __shared__ float norms[8];
-  // all parameters in one pass: each thread keeps one running sum per parameter
-  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    if (p < a.nparams) {
-      const int64_t lo = a.off[p], hi = a.off[p + 1];
-      // 4 independent loads in flight per trip (clamped index, no branch around a load)
-      for (int64_t i = lo + threadIdx.x; i < hi; i += 4 * SCAL_THREADS) {
-        float v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int64_t j = i + u * SCAL_THREADS;
-          v[u] = j < hi ? a.sq[j < hi ? j : lo] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) s[p] += (double)v[u];
-      }
-    }
-  }
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    double t = wave_sum_d(s[p]);
-    if ((threadIdx.x & 63) == 0) red[p][threadIdx.x >> 6] = t;
-  }
-  __syncthreads();
-  if (a.sums_only) {
-    if (threadIdx.x < a.nparams) {
-      const int p = threadIdx.x;
-      double t = 0.0;
-      for (int w = 0; w < NW; ++w) t += red[p][w];
-      a.out[p] = (a.zero_mask >> p) & 1 ? 0.f : (float)t;
-    }
-    return;
-  }
-  if (threadIdx.x < a.nparams) {
-    const int p = threadIdx.x;
-    double t = 0.0;
-    for (int w = 0; w < NW; ++w) t += red[p][w];
-    float nr = (float)sqrt(t);
-    if (a.emulate_bf16) nr = bf16r(nr);  // torch._foreach_norm on bf16 returns bf16
-    norms[p] = nr;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int p = 0; p < a.nparams; ++p) s += norms[p] * norms[p];
-    float total = sqrtf(s);
-    float coef;
-    if (a.emulate_bf16) {
-      total = bf16r(total);                       // vector_norm(stack(bf16 norms)) -> bf16
-      float den = bf16r(total + 1e-6f);           // bf16 tensor + python scalar
-      coef = bf16r(a.max_norm / den);
-      coef = fminf(coef, 1.f);
-    } else {
-      coef = fminf(a.max_norm / (total + 1e-6f), 1.f);
-    }
-    a.out[0] = coef;
-    a.out[1] = total;
-    for (int p = 0; p < a.nparams; ++p) a.out[2 + p] = norms[p];
-  }
+  clip_body<SCAL_THREADS>(a, red, norms);
 }
-
-__global__ __launch_bounds__(SCAL_THREADS) void clip_kernel(const ClipArgs a) { clip_body(a); }
 
 // ---------------------------------------------------------------------------------------
 // Fused step tails: one launch of 1024-thread blocks = 4 independent 256-thread groups, each
@@ -616,7 +481,11 @@ __global__ __launch_bounds__(SCAL_THREADS) void tail_kernel(const TailArgs a) {
   __syncthreads();
   if (!last) return;
   if (a.fence_all) __threadfence();
-  if (a.finalize == 0) clip_body(a.clip);
+  if (a.finalize == 0) {
+    __shared__ double cred[8][SCAL_THREADS / 64];
+    __shared__ float cnorms[8];
+    clip_body<SCAL_THREADS>(a.clip, cred, cnorms);
+  }
   else loss_scalars_body(a.scal);
   if (threadIdx.x == 0) atomicExch(a.counter, 0u);
 }

@@ -1033,9 +1033,23 @@ def test_fused_tails_match_separate_launches(gpu, enc_dtype, B, n, d, h):
     torch.cuda.synchronize()
     host.wait(8, 7)
     for x, y in ((colsum, ws.colsum_acts), (l1p, ws.l1_part), (ev, ws.ev), (ev_a, ws.ev_a), (ev_b, ws.ev_b),
-                 (sc[:6], ws.scalars[:6]), (sq, ws.sq), (gbe, G.b_enc), (gbd, G.b_dec_flat),
-                 (clip[:6], ws.clip_out[:6])):
+                 (sc[:6], ws.scalars[:6]), (sq, ws.sq), (gbe, G.b_enc), (gbd, G.b_dec_flat)):
         assert torch.equal(x, y)
+    # where the step ran G4 + G5 + the grad tail as one launch (cc_wgrad_both_clip_t), its finaliser
+    # accumulates the same fp64 squared sums with 512 instead of 1024 threads
+    if ws.tr:
+        assert torch.allclose(clip[:6], ws.clip_out[:6], rtol=2 ** -8, atol=0)
+        # ... and its weight gradients / sq partials are the stand-alone dual GEMM's
+        G2 = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+        sq2 = torch.zeros_like(ws.sq)
+        o = ws.sq_off
+        ops.wgrad_both_t(ws.acts_t, ws.g_recon_t, a.W_dec_hk, ws.inv_norms, ws.colsum_acts, 2.0 / B, G2.W_dec_hk,
+                         sq2[o[1]:o[2]], ws.g_pre_t, ws.x_t, G2.W_enc_hk, sq2[o[0]:o[1]], n, d)
+        torch.cuda.synchronize()
+        assert torch.equal(G2.W_dec_hk, G.W_dec_hk) and torch.equal(G2.W_enc_hk, G.W_enc_hk)
+        assert torch.equal(sq2[o[0]:o[2]], ws.sq[o[0]:o[2]])
+    else:
+        assert torch.equal(clip[:6], ws.clip_out[:6])
     assert torch.equal(torch.from_numpy(host.f32[:6].copy()), sc2[:6].cpu())
     assert torch.equal(sc2[:6], sc[:6])
 
