@@ -79,7 +79,7 @@ SPAN_EVERY = 4  # timed steps per roofline-kernel sample (events around the laun
 
 # span name -> kernel-name prefix in the rocprofv3 traces
 SPAN_KERNEL = {"G1_encode": "gemm_pp_kernel<true, true, 1", "G2_decode": "gemm_pp_main_splitk_kernel<true, true, 7",
-               "G3_dacts": "gemm_pp_kernel<true, true, 3", "G4G5_wgrad": "gemm_pp_dual_kernel<true, true, 4, 5>",
+               "G3_dacts": "gemm_pp_kernel<true, true, 3", "G4G5_wgrad": "gemm_pp_dual_tail_kernel<true, true, 4, 5>",
                "adam": "adam_bulk_kernel"}
 
 
@@ -285,6 +285,8 @@ def main():
     step_flop = 5 * 2.0 * B * K * h_total  # whole job
     if not engine.transposed_wgrad(B, K, h_local, torch.bfloat16):  # batch-major MN/MN form (cc_wgrad_both)
         SPAN_KERNEL["G4G5_wgrad"] = "gemm_pp_dual_kernel<false, false, 4, 5>"
+    elif sharded_path:  # the latent-sharded step all-reduces the squared sums: its grad tail is a launch of its own
+        SPAN_KERNEL["G4G5_wgrad"] = "gemm_pp_dual_kernel<true, true, 4, 5>"
     traffic, traffic_src = pmc_traffic(dom) if (config, world, custom) == (2, 1, False) else (None, None)
     # algorithmic operand/output bytes of the dominant launch (each input read once, output written once)
     es = 2  # bf16
@@ -317,7 +319,7 @@ def main():
         "latent_acts_per_s": round(value * h_total, 1),
         "step_mfma_frac": round(step_flop / step_s / 1e12 / (PEAK_BF16_TFLOPS * world), 4),
         "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items())},
-        "roofline": {"bound": "mfma", "kernel": dom, "kernel_ms": round(dom_ms, 4),
+        "roofline": {"bound": "mfma", "kernel": dom, "kernel_name": SPAN_KERNEL.get(dom), "kernel_ms": round(dom_ms, 4),
                      "kernel_samples": len(timer.rec.get(dom, [])), "achieved": round(achieved, 1),
                      "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                      "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
