@@ -89,7 +89,6 @@ class Buffer(_BufferProtocol):
             spare = torch.empty_like(self.buffer)
         ops.gather_rows(self.buffer, perm, out=spare)
         self._spare, self.buffer = self.buffer, spare
-        self.refreshes = getattr(self, "refreshes", 0) + 1  # (the gather writes outside torch's version counter)
 
     def next_raw(self):
         B = self.cfg["batch_size"]
@@ -103,14 +102,6 @@ class Buffer(_BufferProtocol):
                 out = out.clone()
             self.refresh()
         return out, self.normalisation_factor
-
-    def peek_raw(self):
-        """The slice the next next_raw() call hands out (no state change), so the Trainer can prepare
-        it ahead; a refresh inside that call is caught by the Trainer's input check."""
-        B = self.cfg["batch_size"]
-        if self.buffer_pointer + B > self.buffer.shape[0]:
-            return None, None
-        return self.buffer[self.buffer_pointer: self.buffer_pointer + B], self.normalisation_factor
 
 
 class SyntheticBuffer(_BufferProtocol):
@@ -146,9 +137,3 @@ class SyntheticBuffer(_BufferProtocol):
         out = self.buffer[self.buffer_pointer: self.buffer_pointer + B]
         self.buffer_pointer += B
         return out, self.normalisation_factor
-
-    def peek_raw(self):
-        """The slice the next next_raw() call hands out (no state change)."""
-        B = self.cfg["batch_size"]
-        p = 0 if self.buffer_pointer + B > self.buffer.shape[0] else self.buffer_pointer
-        return self.buffer[p: p + B], self.normalisation_factor

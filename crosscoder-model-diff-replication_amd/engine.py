@@ -184,26 +184,9 @@ class StepWorkspace:
         self.tail_ctr = torch.zeros(2, dtype=torch.int32, device=device)
         self.norms_token = None
         self.busy = None  # weakref to the token of an autograd graph whose backward still needs this workspace
-        # the next batch's prologue outputs (x, x^T, column-sum slab, mean), prepared during this step
-        # (forward(ahead=...)), and the identity of the input they were made from (Trainer checks it)
-        self._ahead = None
-        self.ahead_token = None
 
     def sq_slice(self, i):
         return self.sq[self.sq_off[i]:self.sq_off[i + 1]]
-
-    def ahead_buffers(self):
-        """The second set of input buffers the next batch is prepared into (allocated on first use)."""
-        if self._ahead is None:
-            self._ahead = (torch.empty_like(self.x), None if self.x_t is None else torch.empty_like(self.x_t),
-                           torch.empty_like(self.x_colpart), torch.empty_like(self.x_mean))
-        return self._ahead
-
-    def swap_ahead(self):
-        """Make the batch prepared ahead this step's input (the buffers it replaces become the next spare)."""
-        nxt = self.ahead_buffers()
-        self._ahead = (self.x, self.x_t, self.x_colpart, self.x_mean)
-        self.x, self.x_t, self.x_colpart, self.x_mean = nxt
 
 
 def transposed_wgrad(B, K, h, dtype):
@@ -247,20 +230,15 @@ def decoder_norms(ws, P):
     _decoder_derived(ws, P)
 
 
-def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True, finalize=True, prepped=False,
-            ahead=None):
+def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True, finalize=True):
     """Forward + reconstruction-loss gradient.  P: params Arena.  x_in [B, n, d] any of
     fp32/bf16, factor [n] or None.  Leaves losses in ws.scalars / ws.ev*, g_recon ready
     (loss=False: stops at the fp32 reconstruction, for loss_rows / loss_finalize by slices;
     finalize=False: stops after the loss rows, for loss_finalize_beside).  Where the fused entry
-    serves the shape, G2 and the loss rows are one pass (decode_loss_t; no fp32 reconstruction).
-    prepped: ws.x / x^T / x_mean already hold x_in's prologue (swapped in from an earlier ahead=).
-    ahead (x_next, factor_next): prepare the NEXT batch's prologue into ws.ahead_buffers() while
-    this stream would otherwise idle waiting for the side stream's decoder-half Adam (before G2)."""
+    serves the shape, G2 and the loss rows are one pass (decode_loss_t; no fp32 reconstruction)."""
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
-    if not prepped:
-        with _span("prep"):
-            ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart, out_t=ws.x_t)
+    with _span("prep"):
+        ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart, out_t=ws.x_t)
     # G1 reads only the encoder half: it may overlap the previous step's decoder-half Adam
     with _span("G1_encode"):
         if ws.tr:
@@ -271,17 +249,10 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
                            l0_part=ws.l0_part)
     # x.mean(0) is first read by the loss kernel: reduced here it runs while the stream would
     # otherwise idle waiting for the side stream's decoder-half Adam (G1 starts 8 us earlier)
-    if not prepped:
-        ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
+    ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
     # sum_b acts (G4's L1 term, crosscoder.py:126) likewise, in the same wait; the l1 dots against the
     # decoder norms (not known before the side stream's pass) stay in the loss tail
     ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts)
-    if ahead is not None:
-        # the next batch's prologue in the same wait: the next step's G1 then follows its Adam directly
-        ax, axt, acp, am = ws.ahead_buffers()
-        with _span("prep_ahead"):
-            ops.prep_input(ahead[0], ahead[1], ws.dtype, out=ax, colsum_part=acp, out_t=axt)
-        ops.reduce_rows(acp, acp.shape[0], K, scale=1.0 / B, out_f32=am)
     P.wait_pending()
     decoder_norms(ws, P)  # (+ W_dec^T), unless launched already after the last Adam
     if loss and ws.fused_ncb:

@@ -85,7 +85,6 @@ class Trainer:
         self.optimizer = FusedAdam(self.crosscoder, cfg["lr"], (cfg["beta1"], cfg["beta2"]))
         self.scheduler = LambdaLRHost(self.optimizer, self.lr_lambda)
         self.step_counter = 0
-        self.prepped_ahead = 0  # steps whose input prologue was prepared during the step before
         self.logger = logger
         self._host = None  # pinned loss-scalar landing buffer (allocated on the first step)
         self._side = None  # stream of the decoder half's Adam (created on the first step)
@@ -106,24 +105,13 @@ class Trainer:
         backward / clip / Adam launches."""
         cc = self.crosscoder
         raw, factor = self.buffer.next_raw()
-        factor = factor if getattr(self.buffer, "normalize", True) else None
-        ws = cc._workspace(raw.shape[0], step=True)
-        # the prologue of this batch may have been prepared during the last step (forward(ahead=...)):
-        # used only if this is the very input it was made from, unchanged since
-        prepped = ws.ahead_token is not None and ws.ahead_token == self._input_token(raw, factor)
-        if prepped:
-            ws.swap_ahead()
-            self.prepped_ahead += 1
-        ws.ahead_token = None
-        ahead = self._peek_next(raw.shape[0])
         raw = cc.pad_input(raw)  # (zero columns only when d_in % 8 != 0)
+        ws = cc._workspace(raw.shape[0], step=True)
         P = cc.arena()
         opt = self.optimizer
         side = self._side_stream()
         # prep, G1, G2 + the loss rows (one pass where decode_loss_t serves the shape)
-        engine.forward(ws, P, raw, factor, finalize=False, prepped=prepped, ahead=ahead)
-        if ahead is not None:
-            ws.ahead_token = self._input_token(*ahead)
+        engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None, finalize=False)
         # the loss scalars (+ their host copy) on the side stream, beside G3 (read by nothing on this stream)
         engine.loss_finalize_beside(ws, side, on_losses)
         l1c = self.get_l1_coeff()
@@ -137,24 +125,6 @@ class Trainer:
         self.scheduler.step()
         self._last_l1c = l1c
         return ws.scalars
-
-    def _input_token(self, raw, factor):
-        # the identity of a step input: storage, view, torch's version counter (bumped by every in-place
-        # write through torch) and the buffer's refresh count (a refresh may rewrite rows outside torch)
-        f = None if factor is None else (factor.data_ptr(), factor._version, factor.dtype)
-        return (raw.data_ptr(), tuple(raw.shape), raw.stride(), raw.dtype, raw._version, f,
-                getattr(self.buffer, "refreshes", 0))
-
-    def _peek_next(self, B):
-        """(x, factor) of the batch the buffer's next next_raw() will hand out, when the buffer can say
-        so without changing its state (peek_raw) and the rows need no padding; else None."""
-        peek = getattr(self.buffer, "peek_raw", None)
-        if peek is None or self.crosscoder._dp != self.cfg["d_in"]:
-            return None
-        raw, factor = peek()
-        if raw is None or raw.shape[0] != B or not raw.is_contiguous():
-            return None
-        return raw, (factor if getattr(self.buffer, "normalize", True) else None)
 
     def _copy_losses(self, scalars):
         # the step's single device->host copy, enqueued (on the side stream) as soon as the forward has

@@ -240,16 +240,3 @@ def test_odd_shapes_keep_reference_params():
     cc2 = ca.CrossCoder(dict(cfg, seed=1))
     cc2.load_state_dict(sd)
     assert all(torch.equal(getattr(cc2, k).detach(), ref[k]) for k in O.PARAM_ORDER)
-
-
-def test_synthetic_buffer_peek_is_the_next_batch():
-    """peek_raw() names the slice the next next_raw() hands out (incl. the wrap-around) and changes no
-    state: the Trainer prepares that batch's prologue ahead from it."""
-    cfg = {"batch_size": 64, "d_in": 16, "enc_dtype": "fp32", "device": "cpu"}
-    buf = ca.SyntheticBuffer(cfg, rows=64 * 3 + 10, seed=0, device="cpu")
-    for _ in range(8):
-        p, pf = buf.peek_raw()
-        ptr = buf.buffer_pointer
-        assert buf.peek_raw()[0].data_ptr() == p.data_ptr() and buf.buffer_pointer == ptr
-        x, f = buf.next_raw()
-        assert x.data_ptr() == p.data_ptr() and x.shape == p.shape and f is pf

@@ -1096,37 +1096,6 @@ def test_param_access_orders_after_side_stream_adam(gpu):
     assert torch.equal(w, cc.W_dec.detach())
 
 
-@pytest.mark.parametrize("enc_dtype", ["bf16", "fp32"])
-def test_prologue_prepared_ahead_matches_in_step(gpu, enc_dtype):
-    """Trainer prepares the next batch's prologue (x, x^T, x.mean(0)) during the current step from the
-    buffer's peek_raw(); the step that consumes it must see exactly the training a buffer without
-    peek_raw gives: same loss dicts and params bit for bit, across the buffer's wrap-around and after
-    an in-place write to the buffer between steps (which must invalidate the prepared batch)."""
-    B, n, d, h = 512, 2, 128, 1024
-    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype=enc_dtype,
-               num_tokens=B * 20, device=str(gpu))
-
-    class NoPeek(ca.SyntheticBuffer):
-        peek_raw = None
-
-    runs = []
-    for cls in (ca.SyntheticBuffer, NoPeek):
-        buf = cls(cfg, rows=B * 3, seed=2)
-        tr = ca.Trainer(cfg, buffer=buf, crosscoder=ca.CrossCoder(cfg))
-        dicts = []
-        for t in range(7):
-            if t == 4:
-                buf.buffer.mul_(1.5)  # the batch prepared during step 3 is stale now
-            dicts.append(tr.step())
-        tr.synchronize()
-        runs.append((dicts, {k: v.detach().clone() for k, v in tr.crosscoder.state_dict().items()}, tr.prepped_ahead))
-    (da, pa, ua), (db, pb, ub) = runs
-    assert ua == 5 and ub == 0  # steps 1-3 and 5-6 consumed a prepared batch; step 4's was discarded
-    assert da == db
-    for k in pa:
-        assert torch.equal(pa[k], pb[k]), k
-
-
 def test_sae_vis_export_matches_notebook_fold(gpu):
     """Crosscoder_model_diff.ipynb:35752-35801: the encoder-only fold of the scaling factors into a copy,
     exported as the state_dict the sae_vis fork loads: same keys / shapes / strides as the reference,
