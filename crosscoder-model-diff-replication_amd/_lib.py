@@ -118,6 +118,8 @@ def load(path=None):
     lib.cc_debug_set_dec_one_launch.argtypes = [ctypes.c_int]
     lib.cc_debug_set_pp_fast.restype = None
     lib.cc_debug_set_pp_fast.argtypes = [ctypes.c_int]
+    lib.cc_debug_set_enc_grid.restype = None
+    lib.cc_debug_set_enc_grid.argtypes = [ctypes.c_int]
     _lib = lib
     return lib
 

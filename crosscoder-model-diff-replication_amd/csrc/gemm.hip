@@ -763,6 +763,17 @@ static int pp_grid(int64_t tiles) {
 #endif
 static int g_pp_fast = CC_PP_FAST;  // cc_debug_set_pp_fast: in-process check that both forms give the same bits
 extern "C" void cc_debug_set_pp_fast(int on) { g_pp_fast = on; }
+// workgroups of the persistent encoder GEMM (G1): the CUs it leaves free run the side stream's decoder-half
+// Adam beside it (0: one per CU).  Multiple of 8 (the tile -> XCD map).
+#ifndef CC_ENC_GRID
+#define CC_ENC_GRID 0
+#endif
+static int g_enc_grid = CC_ENC_GRID;
+extern "C" void cc_debug_set_enc_grid(int n) { g_enc_grid = n > 0 ? n & ~7 : 0; }
+static int enc_grid(int tiles) {
+  int g = pp_grid(tiles);
+  return g_enc_grid > 0 && g_enc_grid < g ? g_enc_grid : g;
+}
 template <bool AKC, bool BKC, int EPI>
 static int launch_pp(GemmArgs a, hipStream_t st) {
 #ifdef CC_PP_STAMPS
@@ -772,7 +783,8 @@ static int launch_pp(GemmArgs a, hipStream_t st) {
   a.nbn = (a.N + 255) / 256;
   if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
     if (g_pp_fast && a.M % BM == 0 && a.N % 256 == 0 && (EPI == EPI_DACTS || a.flag)) {  // whole tiles, ReLU on
-      hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI, true>), dim3(pp_grid(a.nbm * a.nbn)), dim3(NTHR), 0, st, a);
+      const int grid = EPI == EPI_ENC ? enc_grid(a.nbm * a.nbn) : pp_grid(a.nbm * a.nbn);
+      hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI, true>), dim3(grid), dim3(NTHR), 0, st, a);
       CC_LAUNCH_CHECK();
       return CC_OK;
     }

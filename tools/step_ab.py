@@ -143,6 +143,22 @@ class G2FromWdec:
         self.tr.crosscoder._ws.norms_token = None
 
 
+class EncGrid:
+    """Variant: G1 (persistent) on `grid` workgroups, leaving CUs to the side-stream decoder Adam
+    (cc_debug_set_enc_grid)."""
+
+    def __init__(self, grid):
+        self.grid = grid
+
+    def on(self):
+        from crosscoder_amd import _lib
+        _lib.load().cc_debug_set_enc_grid(self.grid)
+
+    def off(self):
+        from crosscoder_amd import _lib
+        _lib.load().cc_debug_set_enc_grid(0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib")
@@ -176,6 +192,9 @@ def main():
     variants["serial Adam + norms beside G1"] = (serial_adam(True), None, None)
     variants["serial Adam + norms before G2"] = (serial_adam(False), None, None)
     variants["G2 from W_dec (no W_dec^T pass)"] = (shipped, g2mn.on, g2mn.off)
+    for g in (240, 224, 208, 192, 160):
+        v = EncGrid(g)
+        variants[f"G1 grid {g}"] = (shipped, v.on, v.off)
     if args.only:
         keep = args.only.split(",")
         variants = {k: v for k, v in variants.items() if k in keep}
