@@ -100,6 +100,27 @@ def pmc_traffic(span):
     return None, None
 
 
+def n1_same_workload(B, n, d, h):
+    """The committed one-GPU bench line of the same workload (profiles/*_bench_configs.jsonl, measured by this
+    bench with --config on one MI355X), the 1-GPU point of an N > 1 strong-scaling curve -- or None."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_bench_configs.jsonl")))
+    if not files:
+        return None
+    for line in open(files[-1]):
+        line = line.strip()
+        if not line.startswith("{"):
+            continue
+        r = json.loads(line)
+        c = r.get("config", {})
+        if r.get("n_gpus") == 1 and (c.get("global_batch"), c.get("n_models"), c.get("d_model"),
+                                       c.get("dict_size")) == (B, n, d, h):
+            return {"value": r["value"], "ms_per_step": r["ms_per_step"], "unit": r["unit"],
+                    "source": os.path.relpath(files[-1], ROOT)}
+    return None
+
+
 def make_cfg(B, n, d, h):
     return {
         "seed": 49, "batch_size": B, "buffer_mult": 128, "lr": 5e-5, "num_tokens": 400_000_000, "l1_coeff": 2,
@@ -317,6 +338,9 @@ def main():
                    "global_batch": B, "n_models": n, "d_model": d, "dict_size": h_total,
                    "parallelism": f"latent{world}"},
         "latent_acts_per_s": round(value * h_total, 1),
+        # N > 1: the same workload on one GPU (committed measurement), so the strong-scaling curve has its
+        # own 1-GPU point (the driver's N = 1 run is the metric's config 2, a different dictionary)
+        "n1_same_workload": n1_same_workload(B, n, d, h_total) if world > 1 else None,
         "step_mfma_frac": round(step_flop / step_s / 1e12 / (PEAK_BF16_TFLOPS * world), 4),
         "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items())},
         "roofline": {"bound": "mfma", "kernel": dom, "kernel_name": SPAN_KERNEL.get(dom), "kernel_ms": round(dom_ms, 4),
