@@ -642,19 +642,23 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 //       2b + g, 2b + g + 2 * grid, ... (b_enc.grad / b_dec.grad column sums of the G3 / loss partial
 //       slabs + their sq partials: reduce_rows_phase1/2, the bits cc_grad_tail writes);
 //   (2) the dual tile loop of gemm_pp_dual_kernel;
-//   (3) the last workgroup to arrive (device-scope arrival counter, reset by it for the next launch)
-//       runs clip_body over the squared-sum slab the whole grid wrote: clip_grad_norm_'s coefficient.
+//   (3) every workgroup sums, per parameter, the squared-sum partials of its own tiles and bias blocks
+//       (fixed order) into wg_part[workgroup][4]; the last workgroup to arrive (device-scope arrival
+//       counter, reset by it for the next launch) combines those (one load per thread instead of a
+//       pass over the whole per-tile slab after its L2 invalidate) into clip_grad_norm_'s coefficient.
 struct WgradTail {
   RedSeg red[2];
   int red_blocks[2];
   ClipArgs clip;
   unsigned* counter;
+  float* wg_part;  // [grid][4]: W_enc, W_dec, b_enc, b_dec (the order of sq's segments)
 };
 
 template <bool AKC, bool BKC, int EPI0, int EPI1>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmArgs a0, const GemmArgs a1,
                                                                    const WgradTail tl) {
   __shared__ __attribute__((aligned(16))) char smem[EPI0 == EPI_WGDEC || EPI1 == EPI_WGDEC ? PP_LDS_W : PP_LDS];
+#ifndef CC_EXP_TAIL_NOBIAS  // timing-only experiment builds (never shipped): parts of the tail left out
   {
     const int grp = threadIdx.x >> 8, t = threadIdx.x & 255;
     float(*red)[RED_COLS] = (float(*)[RED_COLS])(smem + grp * 4 * RED_COLS * sizeof(float));
@@ -668,6 +672,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmAr
       __syncthreads();
     }
   }
+#endif
   const int nb0 = a0.nbm * a0.nbn;
   for (int t = blockIdx.x; t < 2 * nb0; t += gridDim.x) {
     const int tid = pp_opaque_tid();
@@ -675,8 +680,37 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmAr
     else pp_tile<AKC, BKC, EPI1>(a1, smem, t - nb0, tid);
     pp_tile_boundary();
   }
-  // publish: every wave waits for its own stores (the last tile's sq partials among them), the
-  // barrier joins the waves, ONE agent-scope release writes this XCD's L2 back before the arrival count
+#ifdef CC_EXP_TAIL_NOARRIVE
+  return;
+#endif
+  // this workgroup's squared sums per parameter: its tiles' per-wave partials (G5 -> W_enc, G4 -> W_dec)
+  // and its bias blocks' partials, written by its own waves (visible after their stores drained + the barrier)
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int k = lane >> 3;; k += 8) {  // lane: partial (lane & 7) of own tiles k = lane/8, +8, ...
+      const int t = (int)blockIdx.x + k * (int)gridDim.x;
+      if (t >= 2 * nb0) break;
+      if (t < nb0) s[1] += (double)a0.wave_part0[t * 8 + (lane & 7)];
+      else s[0] += (double)a1.wave_part0[(t - nb0) * 8 + (lane & 7)];
+    }
+    const int nred = tl.red_blocks[0] + tl.red_blocks[1];
+    for (int k = lane;; k += 64) {  // own bias blocks 2b + g + 2 * grid * i
+      const int blk = 2 * (int)blockIdx.x + (k & 1) + 2 * (int)gridDim.x * (k >> 1);
+      if (blk >= nred) break;
+      if (blk < tl.red_blocks[0]) s[2] += (double)tl.red[0].sq_part[blk];
+      else s[3] += (double)tl.red[1].sq_part[blk - tl.red_blocks[0]];
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const double v = wave_sum_d(s[p]);
+      if (lane == 0) tl.wg_part[blockIdx.x * 4 + p] = (float)v;
+    }
+  }
+  // publish: wave 0's stores drained, the barrier joins the waves, ONE agent-scope release writes this
+  // XCD's L2 back before the arrival count
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   int* last = (int*)smem;
@@ -688,7 +722,16 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmAr
   }
   __syncthreads();
   if (!*last) return;
-  clip_body<NTHR>(tl.clip, (double(*)[NTHR / 64])(smem + 64), (float*)(smem + 64 + 8 * (NTHR / 64) * sizeof(double)));
+#ifndef CC_EXP_TAIL_NOCLIP
+  {
+    double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int w = threadIdx.x; w < (int)gridDim.x; w += NTHR)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) s[p] += (double)tl.wg_part[w * 4 + p];
+    clip_finish<NTHR>(tl.clip, s, (double(*)[NTHR / 64])(smem + 64),
+                      (float*)(smem + 64 + 8 * (NTHR / 64) * sizeof(double)));
+  }
+#endif
   if (threadIdx.x == 0) atomicExch(tl.counter, 0u);
 }
 
@@ -1328,13 +1371,13 @@ int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_
                          const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
                          const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
                          const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
-                         uint32_t* counter, int dtype, void* stream) {
+                         uint32_t* counter, float* wg_part, int dtype, void* stream) {
   const int64_t K = n * d;
   if (!gpre_colpart || !g_b_enc || !sq_b_enc || !loss_colpart || !g_b_dec || !sq_b_dec || !sq || !off || !clip_out ||
-      !counter)
+      !counter || !wg_part)
     return CC_ERR_NULL;
   if (R_enc <= 0 || R_dec <= 0) return CC_ERR_SHAPE;
-  if (nparams <= 0 || nparams > 8) return CC_ERR_SHAPE;
+  if (nparams != 4) return CC_ERR_SHAPE;  // W_enc, W_dec, b_enc, b_dec: the segments of sq
   GemmArgs a0, a1;
   int rc = wgrad_dec_args(a0, actsT, g_reconT, W_dec, inv_norms, colsum_acts, l1_scale, grad_W_dec, sq_dec, B, h, n,
                           d, dtype, true);
@@ -1362,8 +1405,11 @@ int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_
   tl.clip.emulate_bf16 = emulate_bf16;
   tl.clip.out = clip_out;
   tl.counter = counter;
-  hipLaunchKernelGGL((gemm_pp_dual_tail_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(pp_grid(2 * a0.nbm * a0.nbn)),
-                     dim3(NTHR), 0, (hipStream_t)stream, a0, a1, tl);
+  tl.wg_part = wg_part;
+  const int grid = pp_grid(2 * a0.nbm * a0.nbn);
+  if (grid > CC_WG_PART_MAX) return CC_ERR_SHAPE;
+  hipLaunchKernelGGL((gemm_pp_dual_tail_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(grid), dim3(NTHR), 0,
+                     (hipStream_t)stream, a0, a1, tl);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }

@@ -80,6 +80,8 @@ struct ClipArgs {
 // One block of NT threads; red / norms: LDS scratch of the caller (the GEMM kernel that runs it as
 // its last workgroup's tail has no LDS to spare for static arrays of its own)
 template <int NT>
+CC_DEV void clip_finish(const ClipArgs& a, const double* s, double (*red)[NT / 64], float* norms);
+template <int NT>
 CC_DEV void clip_body(const ClipArgs& a, double (*red)[NT / 64], float* norms) {
   // all parameters in one pass: each thread keeps one running sum per parameter
   double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -100,6 +102,13 @@ CC_DEV void clip_body(const ClipArgs& a, double (*red)[NT / 64], float* norms) {
       }
     }
   }
+  clip_finish<NT>(a, s, red, norms);
+}
+
+// The finaliser from per-thread partial sums s[p] (every thread of the block): fixed-order combine of
+// the waves, per-parameter norms (bf16-rounded as torch's _foreach_norm on bf16), total, coefficient.
+template <int NT>
+CC_DEV void clip_finish(const ClipArgs& a, const double* s, double (*red)[NT / 64], float* norms) {
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
     double t = wave_sum_d(s[p]);

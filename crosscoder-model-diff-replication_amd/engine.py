@@ -178,6 +178,7 @@ class StepWorkspace:
             self.sq_off.append(self.sq_off[-1] + s)
         self.sq = E(self.sq_off[-1])
         self.clip_out = E(8)
+        self.wg_part = E(ops.WG_PART_FLOATS)  # per-workgroup squared sums of the fused G4G5 + grad tail
         self.clip_ready = False  # backward(clip=...) already wrote clip_out (fused grad tail)
         self.acts_pending = False  # forward deferred the activation column sums to loss_finalize
         # arrival counters of the fused tail launches (loss tail, grad tail); each launch leaves 0
@@ -388,7 +389,7 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
                                   G.W_dec_hk, ws.sq_slice(1), ws.g_pre_t, ws.x_t, G.W_enc_hk, ws.sq_slice(0), n, d,
                                   ws.gpre_colpart, G.b_enc, ws.sq_slice(2), loss_colpart(ws), G.b_dec_flat,
                                   ws.sq_slice(3), ws.sq, ws.sq_off, clip, ws.dtype == torch.bfloat16, ws.clip_out,
-                                  ws.tail_ctr[1:2])
+                                  ws.tail_ctr[1:2], ws.wg_part)
         ws.clip_ready = True
         return
     with _span("G4G5_wgrad"):

@@ -357,9 +357,12 @@ def wgrad_both_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, grad_d
                                 h, n, d, dtype_code(actsT.dtype), _stream(actsT)))
 
 
+WG_PART_FLOATS = 4 * 1024  # CC_WG_PART_MAX x 4 (include/crosscoder_hip.h)
+
+
 def wgrad_both_clip_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, grad_dec, sq_dec, g_preT, xT, grad_enc,
                       sq_enc, n, d, gpre_colpart, g_b_enc, sq_b_enc, loss_colpart, g_b_dec, sq_b_dec, sq, offsets,
-                      max_norm, emulate_bf16, out, counter):
+                      max_norm, emulate_bf16, out, counter, wg_part):
     """wgrad_both_t + grad_tail in one launch (the bias sums before the GEMM tiles, the clip coefficient
     in the last workgroup); same outputs."""
     h, B = actsT.shape
@@ -369,7 +372,7 @@ def wgrad_both_clip_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, g
         _ptr(sq_dec), _ptr(g_preT), _ptr(xT), _ptr(grad_enc), _ptr(sq_enc), B, h, n, d, _ptr(gpre_colpart),
         gpre_colpart.shape[0], _ptr(g_b_enc), _ptr(sq_b_enc), _ptr(loss_colpart), loss_colpart.shape[0], _ptr(g_b_dec),
         _ptr(sq_b_dec), _ptr(sq), arr, len(offsets) - 1, max_norm, int(emulate_bf16), _ptr(out), _ptr(counter),
-        dtype_code(actsT.dtype), _stream(actsT)))
+        _ptr(wg_part), dtype_code(actsT.dtype), _stream(actsT)))
 
 
 def clip_finalize(sq, offsets, max_norm, emulate_bf16, out):

@@ -267,15 +267,17 @@ int cc_grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_
  * + their sq partials) and cc_grad_tail (bias gradients + sq partials, clip_grad_norm_'s coefficient
  * into clip_out) -- the bias sums run before the GEMM tiles, the clip finaliser in the last workgroup
  * to finish.  Same outputs as cc_wgrad_both_t followed by cc_grad_tail (the clip coefficient up to
- * the order of its fp64 squared-sum accumulation).  Where the ping-pong GEMM does not serve the
- * shape (or dtype != bf16) it runs exactly those two entries. */
+ * the order of its fp64 squared-sum accumulation).  nparams must be 4 (sq's segments W_enc, W_dec, b_enc,
+ * b_dec); wg_part: fp32 scratch of CC_WG_PART_MAX x 4 (per-workgroup squared sums).  Where the ping-pong
+ * GEMM does not serve the shape (or dtype != bf16) it runs exactly those two entries. */
+#define CC_WG_PART_MAX 1024
 int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
                          const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_preT,
                          const void* xT, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
                          const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
                          const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
                          const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
-                         uint32_t* counter, int dtype, void* stream);
+                         uint32_t* counter, float* wg_part, int dtype, void* stream);
 /* cc_grad_tail whose finaliser is cc_segment_sums instead of the clip (the latent-sharded step:
  * out[p] = the per-parameter squared sums, 0 where bit p of zero_mask is set, to be all-reduced). */
 int cc_grad_tail_sums(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,
