@@ -83,6 +83,43 @@ def dec_adam_side_norms_main():
     return adam
 
 
+def dec_adam_with_enc():
+    """Decoder-half Adam on the side stream from the moment the clip coefficient exists (event recorded
+    BEFORE the encoder-half Adam), so the two halves share the HBM instead of running back to back."""
+    from crosscoder_amd import engine, ops
+
+    def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None):
+        coef = ws.clip_out[0:1]
+        dev = P.data.device
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side_stream):
+            side_stream.wait_event(ready)
+            ops.adam_step(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), coef, lr, beta1, beta2, eps, step,
+                          max_blocks=engine.DEC_ADAM_BLOCKS)
+            engine.norms_for_next(ws, P)
+            done = torch.cuda.Event()
+            done.record(side_stream)
+        with engine._span("adam"):
+            ops.adam_step(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), coef, lr, beta1, beta2, eps, step)
+        P.pending = done
+    return adam
+
+
+class SidePriority:
+    """Variant: the side stream (decoder-half Adam, W_dec^T + norms, loss tail) created with high priority."""
+
+    def __init__(self, tr):
+        self.tr = tr
+
+    def on(self):
+        self.saved = self.tr._side
+        self.tr._side = torch.cuda.Stream(device=self.tr.crosscoder.arena().data.device, priority=-1)
+
+    def off(self):
+        self.tr._side = self.saved
+
+
 class TwoPassLoss:
     """Variant: G2 to the fp32 reconstruction, then the separate loss kernel (cc_decode_fwd_ws_t +
     cc_loss_fwd_bwd_rows_t: the round-2 form) instead of the loss in G2's epilogue (cc_decode_loss_t)."""
@@ -192,6 +229,10 @@ def main():
     variants["serial Adam + norms beside G1"] = (serial_adam(True), None, None)
     variants["serial Adam + norms before G2"] = (serial_adam(False), None, None)
     variants["G2 from W_dec (no W_dec^T pass)"] = (shipped, g2mn.on, g2mn.off)
+    variants["dec Adam with enc Adam"] = (dec_adam_with_enc(), None, None)
+    sp = SidePriority(tr)
+    variants["side stream high priority"] = (shipped, sp.on, sp.off)
+    variants["dec Adam with enc Adam + side high priority"] = (dec_adam_with_enc(), sp.on, sp.off)
     for g in (240, 224, 208, 192, 160):
         v = EncGrid(g)
         variants[f"G1 grid {g}"] = (shipped, v.on, v.off)
