@@ -326,7 +326,6 @@ CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
                           const float (&cw)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN]) {
   using E = Elem<DT>;
   using WG = WaveGeom<BNT>;
-  const int N = args.N;
   if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
     // FAST (a kernel variant the host picks when every tile lies inside the matrix and the ReLU is on,
     // as in the step's G1 / G3): no range selects, one bf16 conversion per output, an integer l0
