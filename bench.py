@@ -306,8 +306,6 @@ def main():
     step_flop = 5 * 2.0 * B * K * h_total  # whole job
     if not engine.transposed_wgrad(B, K, h_local, torch.bfloat16):  # batch-major MN/MN form (cc_wgrad_both)
         SPAN_KERNEL["G4G5_wgrad"] = "gemm_pp_dual_kernel<false, false, 4, 5>"
-    elif sharded_path:  # the latent-sharded step all-reduces the squared sums: its grad tail is a launch of its own
-        SPAN_KERNEL["G4G5_wgrad"] = "gemm_pp_dual_kernel<true, true, 4, 5>"
     traffic, traffic_src = pmc_traffic(dom) if (config, world, custom) == (2, 1, False) else (None, None)
     # algorithmic operand/output bytes of the dominant launch (each input read once, output written once)
     es = 2  # bf16

@@ -1365,15 +1365,15 @@ int cc_wgrad_both_t(const void* actsT, const void* g_reconT, const void* W_dec, 
   return CC_OK;
 }
 
-int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
-                         const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_preT,
-                         const void* xT, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
-                         const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
-                         const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
-                         const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
-                         uint32_t* counter, float* wg_part, int dtype, void* stream) {
+static int wgrad_both_tail(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
+                           const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_preT,
+                           const void* xT, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
+                           const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
+                           const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
+                           const int64_t* off, int nparams, float max_norm, int emulate_bf16, int sums_only,
+                           int zero_mask, float* out, uint32_t* counter, float* wg_part, int dtype, void* stream) {
   const int64_t K = n * d;
-  if (!gpre_colpart || !g_b_enc || !sq_b_enc || !loss_colpart || !g_b_dec || !sq_b_dec || !sq || !off || !clip_out ||
+  if (!gpre_colpart || !g_b_enc || !sq_b_enc || !loss_colpart || !g_b_dec || !sq_b_dec || !sq || !off || !out ||
       !counter || !wg_part)
     return CC_ERR_NULL;
   if (R_enc <= 0 || R_dec <= 0) return CC_ERR_SHAPE;
@@ -1388,8 +1388,11 @@ int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_
     rc = cc_wgrad_both_t(actsT, g_reconT, W_dec, inv_norms, colsum_acts, l1_scale, grad_W_dec, sq_dec, g_preT, xT,
                          grad_W_enc, sq_enc, B, h, n, d, dtype, stream);
     if (rc) return rc;
+    if (sums_only)
+      return cc_grad_tail_sums(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec, sq_b_dec,
+                               dtype, sq, off, nparams, zero_mask, out, counter, stream);
     return cc_grad_tail(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec, sq_b_dec, dtype,
-                        sq, off, nparams, max_norm, emulate_bf16, clip_out, counter, stream);
+                        sq, off, nparams, max_norm, emulate_bf16, out, counter, stream);
   }
   a0.nbm = a1.nbm = (a0.M + BM - 1) / BM;
   a0.nbn = a1.nbn = (a0.N + 255) / 256;
@@ -1403,7 +1406,9 @@ int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_
   tl.clip.nparams = nparams;
   tl.clip.max_norm = max_norm;
   tl.clip.emulate_bf16 = emulate_bf16;
-  tl.clip.out = clip_out;
+  tl.clip.out = out;
+  tl.clip.sums_only = sums_only;
+  tl.clip.zero_mask = zero_mask;
   tl.counter = counter;
   tl.wg_part = wg_part;
   const int grid = pp_grid(2 * a0.nbm * a0.nbn);
@@ -1412,6 +1417,32 @@ int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_
                      (hipStream_t)stream, a0, a1, tl);
   CC_LAUNCH_CHECK();
   return CC_OK;
+}
+
+int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
+                         const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_preT,
+                         const void* xT, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
+                         const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
+                         const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
+                         const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
+                         uint32_t* counter, float* wg_part, int dtype, void* stream) {
+  return wgrad_both_tail(actsT, g_reconT, W_dec, inv_norms, colsum_acts, l1_scale, grad_W_dec, sq_dec, g_preT, xT,
+                         grad_W_enc, sq_enc, B, h, n, d, gpre_colpart, R_enc, g_b_enc, sq_b_enc, loss_colpart, R_dec,
+                         g_b_dec, sq_b_dec, sq, off, nparams, max_norm, emulate_bf16, 0, 0, clip_out, counter, wg_part,
+                         dtype, stream);
+}
+
+int cc_wgrad_both_sums_t(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
+                         const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_preT,
+                         const void* xT, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
+                         const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
+                         const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
+                         const int64_t* off, int nparams, int zero_mask, float* out, uint32_t* counter, float* wg_part,
+                         int dtype, void* stream) {
+  return wgrad_both_tail(actsT, g_reconT, W_dec, inv_norms, colsum_acts, l1_scale, grad_W_dec, sq_dec, g_preT, xT,
+                         grad_W_enc, sq_enc, B, h, n, d, gpre_colpart, R_enc, g_b_enc, sq_b_enc, loss_colpart, R_dec,
+                         g_b_dec, sq_b_dec, sq, off, nparams, 0.f, 0, 1, zero_mask, out, counter, wg_part, dtype,
+                         stream);
 }
 
 int cc_wgrad_both(const void* acts, const void* g_recon, const void* W_dec, const float* inv_norms,

@@ -382,6 +382,15 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
         dacts_rows(ws, P, l1_coeff, 0, B, l1_grad_weight)
     if tail_done is not None:
         torch.cuda.current_stream(ws.x.device).wait_event(tail_done)
+    if sums_out is not None and ws.tr:
+        # G4 + G5 and the grad tail's per-parameter squared sums (for the all-reduce) in one launch
+        with _span("G4G5_wgrad"):
+            ops.wgrad_both_sums_t(ws.acts_t, ws.g_recon_t, P.W_dec_hk, ws.inv_norms, ws.colsum_acts, l1_scale,
+                                  G.W_dec_hk, ws.sq_slice(1), ws.g_pre_t, ws.x_t, G.W_enc_hk, ws.sq_slice(0), n, d,
+                                  ws.gpre_colpart, G.b_enc, ws.sq_slice(2), loss_colpart(ws), G.b_dec_flat,
+                                  ws.sq_slice(3), ws.sq, ws.sq_off, sums_out, ws.tail_ctr[1:2], ws.wg_part,
+                                  zero_mask=zero_mask)
+        return
     if clip is not None and ws.tr:
         # G4 + G5 and the grad tail (bias sums + clip coefficient) in one launch
         with _span("G4G5_wgrad"):

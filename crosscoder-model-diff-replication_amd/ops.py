@@ -375,6 +375,20 @@ def wgrad_both_clip_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, g
         _ptr(wg_part), dtype_code(actsT.dtype), _stream(actsT)))
 
 
+def wgrad_both_sums_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, grad_dec, sq_dec, g_preT, xT, grad_enc,
+                      sq_enc, n, d, gpre_colpart, g_b_enc, sq_b_enc, loss_colpart, g_b_dec, sq_b_dec, sq, offsets, out,
+                      counter, wg_part, zero_mask=0):
+    """wgrad_both_t + grad_tail_sums in one launch (the latent-sharded step); same outputs."""
+    h, B = actsT.shape
+    arr = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
+    check(lib().cc_wgrad_both_sums_t(
+        _ptr(actsT), _ptr(g_reconT), _ptr(W_dec_hk), _ptr(norms), _ptr(colsum_acts), l1_scale, _ptr(grad_dec),
+        _ptr(sq_dec), _ptr(g_preT), _ptr(xT), _ptr(grad_enc), _ptr(sq_enc), B, h, n, d, _ptr(gpre_colpart),
+        gpre_colpart.shape[0], _ptr(g_b_enc), _ptr(sq_b_enc), _ptr(loss_colpart), loss_colpart.shape[0], _ptr(g_b_dec),
+        _ptr(sq_b_dec), _ptr(sq), arr, len(offsets) - 1, int(zero_mask), _ptr(out), _ptr(counter), _ptr(wg_part),
+        dtype_code(actsT.dtype), _stream(actsT)))
+
+
 def clip_finalize(sq, offsets, max_norm, emulate_bf16, out):
     arr = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
     check(lib().cc_clip_finalize(_ptr(sq), arr, len(offsets) - 1, max_norm, int(emulate_bf16), _ptr(out),

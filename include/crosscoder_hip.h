@@ -278,6 +278,17 @@ int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_
                          const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
                          const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
                          uint32_t* counter, float* wg_part, int dtype, void* stream);
+/* cc_wgrad_both_clip_t whose finaliser is cc_segment_sums instead of the clip (the latent-sharded step,
+ * trainer.py:45-46 split across ranks): out[p] = the per-parameter squared sums, 0 where bit p of
+ * zero_mask is set, to be all-reduced.  Equal to cc_wgrad_both_t + cc_grad_tail_sums (the sums up to the
+ * order of their fp64 accumulation), which it runs itself where the ping-pong GEMM does not serve. */
+int cc_wgrad_both_sums_t(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
+                         const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_preT,
+                         const void* xT, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
+                         const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
+                         const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
+                         const int64_t* off, int nparams, int zero_mask, float* out, uint32_t* counter, float* wg_part,
+                         int dtype, void* stream);
 /* cc_grad_tail whose finaliser is cc_segment_sums instead of the clip (the latent-sharded step:
  * out[p] = the per-parameter squared sums, 0 where bit p of zero_mask is set, to be all-reduced). */
 int cc_grad_tail_sums(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,

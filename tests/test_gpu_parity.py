@@ -1048,6 +1048,21 @@ def test_fused_tails_match_separate_launches(gpu, enc_dtype, B, n, d, h):
         torch.cuda.synchronize()
         assert torch.equal(G2.W_dec_hk, G.W_dec_hk) and torch.equal(G2.W_enc_hk, G.W_enc_hk)
         assert torch.equal(sq2[o[0]:o[2]], ws.sq[o[0]:o[2]])
+        # the latent-sharded form (cc_wgrad_both_sums_t): the per-parameter squared sums of the segment
+        # finaliser, b_dec masked out as on ranks != 0
+        sums, ref_sums = torch.empty(8, device=gpu), torch.empty(8, device=gpu)
+        G3 = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+        sq3 = torch.zeros_like(ws.sq)
+        ops.wgrad_both_sums_t(ws.acts_t, ws.g_recon_t, a.W_dec_hk, ws.inv_norms, ws.colsum_acts, 2.0 / B, G3.W_dec_hk,
+                              sq3[o[1]:o[2]], ws.g_pre_t, ws.x_t, G3.W_enc_hk, sq3[o[0]:o[1]], n, d, ws.gpre_colpart,
+                              G3.b_enc, sq3[o[2]:o[3]], engine.loss_colpart(ws), G3.b_dec_flat, sq3[o[3]:o[4]], sq3, o,
+                              sums, ws.tail_ctr[1:2], ws.wg_part, zero_mask=0b1000)
+        ops.segment_sums(ws.sq, o, ref_sums, zero_mask=0b1000)
+        torch.cuda.synchronize()
+        assert torch.equal(sq3, ws.sq) and torch.equal(G3.b_enc, G.b_enc) and torch.equal(G3.b_dec_flat, G.b_dec_flat)
+        assert sums[3].item() == 0.0
+        assert torch.allclose(sums[:4], ref_sums[:4], rtol=1e-6, atol=0)
+        assert not bool(ws.tail_ctr.any())
     else:
         assert torch.equal(clip[:6], ws.clip_out[:6])
     assert torch.equal(torch.from_numpy(host.f32[:6].copy()), sc2[:6].cpu())
