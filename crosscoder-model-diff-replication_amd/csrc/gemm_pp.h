@@ -29,6 +29,11 @@
 // KC operands keep [256 rows][128 B] with chunk ^ (row & 7).
 
 #include <type_traits>
+#ifdef CC_EXP_G3REG
+#define CC_G3REG_ON(E) ((E) == EPI_DACTS)
+#else
+#define CC_G3REG_ON(E) false
+#endif
 
 #ifndef CC_PP_ORDER
 #define CC_PP_ORDER 1
@@ -452,14 +457,17 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadI
         for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
           for (int j = 0; j < WG::TN; ++j)
-            acc[2 * p + ii][j] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii][kk], acc[2 * p + ii][j], 0, 0, 0);
+            acc[2 * p + ii][j] = CC_G3REG_ON(EPI)
+                ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[ii][kk], bfr[j][kk], acc[2 * p + ii][j], 0, 0, 0)
+                : __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii][kk], acc[2 * p + ii][j], 0, 0, 0);
 #else
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
         for (int j = 0; j < WG::TN; ++j)
-          acc[ib + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii], acc[ib + ii][j], 0, 0, 0);
+          acc[ib + ii][j] = CC_G3REG_ON(EPI)
+              ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[ii], bfr[j][kk], acc[ib + ii][j], 0, 0, 0)
+              : __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii], acc[ib + ii][j], 0, 0, 0);
 #endif
 #if CC_PP_PRIO
       __builtin_amdgcn_s_setprio(CC_PP_PRIO_BASE);
@@ -490,6 +498,20 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadI
     ((uint64_t*)args.dbg)[(int64_t)args.stamp_base + bid * 4 + (CC_PP_STAMPS_EPI ? 0 : 1)] = __builtin_amdgcn_s_memrealtime();
 #endif
 
+#ifdef CC_EXP_G3REG  // timing-only probe (never shipped): G3 with unswapped accumulators (4 consecutive batch rows
+  // of one latent per lane) stored straight to g_pre^T, 8 B per lane, no LDS image (no mask / l1 term / sums)
+  if (EPI == EPI_DACTS && args.out_t) {  // (the batch-major form, out_t == NULL, keeps its epilogue)
+#pragma unroll
+    for (int i = 0; i < WG::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < WG::TN; ++j) {
+        const int m = m0 + wr * WG::WTM + 16 * i + 4 * (lane >> 4), n = n0 + wc * WG::WTN + 16 * j + (lane & 15);
+        const float v4[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (m < M && n < N) *(bf16x4*)((bf16_t*)args.out_t + (int64_t)n * args.ldt + m) = pack4<CC_BF16>(v4);
+      }
+    return;
+  }
+#endif
   if constexpr (EPI == EPI_SPLIT) {  // split-K partial: accumulator fragments stored as they are (1 KB each)
     // slab tile index tm * nbn + tn (row-major over the tiles, whatever the block order)
     float* o = (float*)args.out + ((int64_t)(tm * args.nbn + tn) * 8 + wave) * 32 * 256;
