@@ -1251,9 +1251,10 @@ int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, c
   l.d = (int)d; l.split_stride = split_stride;
   l.b_dec = (const bf16_t*)b_dec; l.x = (const bf16_t*)x; l.x_mean = x_mean; l.gs = grad_scale;
   l.g_recon = (bf16_t*)g_recon; l.g_t = (bf16_t*)g_recon_t; l.row_part = row_part; l.col_part = col_part;
-  hipLaunchKernelGGL(loss_split_kernel, dim3((unsigned)(p.tail_cols / 64), (unsigned)((B + 127) / 128)),
-                     dim3(LSPLIT_THREADS), 0,
-                     st, l);
+  // one block per 128-row half of every 256-row tile (cc_col_part_rows(B) groups, like the main tiles' column-sum
+  // rows): a half past B writes zero column sums, so every partial row the backward reduces is written
+  hipLaunchKernelGGL(loss_split_kernel, dim3((unsigned)(p.tail_cols / 64), (unsigned)cc_col_part_rows(B)),
+                     dim3(LSPLIT_THREADS), 0, st, l);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }

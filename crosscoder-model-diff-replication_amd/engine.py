@@ -140,12 +140,17 @@ class StepWorkspace:
         npart = ops.dec_norms_part_floats(h, n, d) if self.tr else 0
         self.norm_part = E(npart) if npart else None  # fused W_dec^T + norms pass (d % 64 == 0)
         self.acts_t = E(h, B, dt=dtype) if self.tr else None
-        self.acts_colpart = E(ops.col_part_rows(B), h)
+        # G1's activation column-sum / l0 partial slabs, double-buffered: the loss tail that reads a
+        # step's slabs runs on the side stream, which nothing orders before the NEXT step's G1 on torch's
+        # stream; alternating slots orders every rewrite after that tail (the step after next waits for
+        # this step's decoder-half Adam before G2, and the side stream runs the tail before that Adam)
+        self._slots = [(E(ops.col_part_rows(B), h), E(ops.wave_parts(B, h))) for _ in range(2)]
+        self._slot = 1
+        self.acts_colpart, self.l0_part = self._slots[1]
         self.colsum_acts = E(h)
         self.n_wave = ops.wave_parts(B, h)
         self.n_l1 = ops.reduce_parts(h)
         self.l1_part = E(self.n_l1)  # per 64-latent block: sum_h colsum_acts[h] * tn[h] (= B * l1)
-        self.l0_part = E(self.n_wave)
         self.recon = E(B, K)
         nws = ops.decode_ws_floats(B, h, K, dtype)
         self.dec_ws = E(nws) if nws else None  # G2 split-K partials
@@ -159,7 +164,9 @@ class StepWorkspace:
         self.row_part = rp[:2 * n * self.ncb * B].view(2, n * self.ncb, B)  # loss_fwd_bwd's layout
         self.row_part_fused = rp[:2 * n * self.fused_ncb * B].view(2, n * self.fused_ncb, B) if self.fused_ncb \
             else None
-        self.loss_colpart = E(ops.loss_part_rows(B), K)
+        # b_dec-gradient partial rows: the two-pass loss kernel writes one per 32 batch rows, the fused
+        # G2 + loss epilogue one per 128-row wave half of every 256-row tile (more rows when B <= 32)
+        self.loss_colpart = E(max(ops.loss_part_rows(B), ops.col_part_rows(B)), K)
         self.row_ncb = None         # layout of the row terms last written (None: loss_fwd_bwd's)
         self.loss_col_rows = ops.loss_part_rows(B)  # rows of loss_colpart last written
         self.ev = E(B)
@@ -185,6 +192,11 @@ class StepWorkspace:
         self.tail_ctr = torch.zeros(2, dtype=torch.int32, device=device)
         self.norms_token = None
         self.busy = None  # weakref to the token of an autograd graph whose backward still needs this workspace
+
+    def next_slot(self):
+        """Switch G1's partial slabs (acts_colpart, l0_part) to the other slot (once per forward)."""
+        self._slot ^= 1
+        self.acts_colpart, self.l0_part = self._slots[self._slot]
 
     def sq_slice(self, i):
         return self.sq[self.sq_off[i]:self.sq_off[i + 1]]
@@ -238,6 +250,7 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     finalize=False: stops after the loss rows, for loss_finalize_beside).  Where the fused entry
     serves the shape, G2 and the loss rows are one pass (decode_loss_t; no fp32 reconstruction)."""
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
+    ws.next_slot()
     with _span("prep"):
         ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart, out_t=ws.x_t)
     # G1 reads only the encoder half: it may overlap the previous step's decoder-half Adam

@@ -299,44 +299,62 @@ class ShardedTrainer:
         print(loss_dict)
 
     def save(self):
-        """Gather every rank's slice and write ONE reference-format checkpoint on rank 0
+        """Gather every rank's slice on rank 0 and write ONE reference-format checkpoint there
         (crosscoder.py:132-146: checkpoints/version_N/{k}.pt + {k}_cfg.json, the full dictionary)."""
-        sd = self.gather_state_dict()
+        sd = self.gather_state_dict(dst=0)
         if self.rank == 0:
-            self.save_dir, self.save_version = write_checkpoint(
-                {k: v.cpu() for k, v in sd.items()}, self.cfg, self.save_dir, self.save_version)
+            self.save_dir, self.save_version = write_checkpoint(sd, self.cfg, self.save_dir, self.save_version)
         dist.barrier(group=self.group)
 
     def train(self):
-        """trainer.py:69-82 over the shards (logging and checkpoints on rank 0)."""
+        """trainer.py:69-82 over the shards (logging and checkpoints on rank 0).  The reference saves in a
+        `finally:`; here the final save runs only when the loop completed, because the save is a collective:
+        on an exception raised by one rank alone it would wait forever for the others."""
         self.step_counter = 0
-        try:
-            for i in range(self.total_steps):
-                loss_dict = self.step()
-                if i % self.cfg["log_every"] == 0:
-                    self.log(loss_dict)
-                if (i + 1) % self.cfg["save_every"] == 0:
-                    self.save()
-        finally:
-            self.save()
+        for i in range(self.total_steps):
+            loss_dict = self.step()
+            if i % self.cfg["log_every"] == 0:
+                self.log(loss_dict)
+            if (i + 1) % self.cfg["save_every"] == 0:
+                self.save()
+        self.save()
 
-    def gather_state_dict(self):
-        return gather_state_dict(self.crosscoder, self.cfg["dict_size"], self.group)
+    def gather_state_dict(self, dst=None):
+        return gather_state_dict(self.crosscoder, self.cfg["dict_size"], self.group, dst=dst)
 
 
-def gather_state_dict(cc, h_total, group=None):
-    """Full reference-layout state_dict of a latent-sharded crosscoder on every rank (all_gather of the
-    ranks' latent slices; W_enc with the reference's strides (d, 1, n*d), b_dec from this rank -- it
-    is replicated and identical on all ranks)."""
+def gather_state_dict(cc, h_total, group=None, dst=None):
+    """Full reference-layout state_dict of a latent-sharded crosscoder (the ranks' latent slices
+    concatenated; W_enc with the reference's strides (d, 1, n*d), b_dec from this rank -- it is replicated
+    and identical on all ranks; padded kernel columns (d_in % 8 != 0) sliced off like Arena.views()).
+    dst=None: all_gather, every rank gets the dict on its device.  dst=r: gathered one tensor at a time on
+    rank r and moved to its host (no transient full-dictionary copy on the other ranks' GPUs); the other
+    ranks return None."""
     a = cc.arena()
     a.wait_pending()
     world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n, d, d_ref = a.n, a.d, a.d_ref
     out = {}
     for name, t in (("W_dec", a.W_dec_hk), ("W_enc", a.W_enc_hk), ("b_enc", a.b_enc)):
-        parts = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(parts, t.contiguous(), group=group)
+        t = t.contiguous()
+        if dst is None:
+            parts = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(parts, t, group=group)
+        else:
+            parts = [torch.empty_like(t) for _ in range(world)] if rank == dst else None
+            dist.gather(t, parts, dst=dist.get_global_rank(group, dst) if group is not None else dst, group=group)
+            if rank != dst:
+                continue
+            parts = [p.cpu() for p in parts]
         out[name] = torch.cat(parts, 0)
-    n, d = a.n, a.d
-    W_enc = out["W_enc"].view(h_total, n, d).permute(1, 2, 0)
-    return {"W_enc": W_enc, "W_dec": out["W_dec"].view(h_total, n, d), "b_enc": out["b_enc"],
-            "b_dec": a.b_dec().clone()}
+        del parts
+    if dst is not None and rank != dst:
+        return None
+    # compact reference strides (no copy when d_in % 8 == 0)
+    W_dec = out["W_dec"].view(h_total, n, d)[:, :, :d_ref].contiguous()
+    W_enc = out["W_enc"].view(h_total, n, d)[:, :, :d_ref].contiguous().permute(1, 2, 0)
+    b_dec = a.b_dec().clone()
+    if dst is not None:
+        b_dec = b_dec.cpu()
+    return {"W_enc": W_enc, "W_dec": W_dec, "b_enc": out["b_enc"], "b_dec": b_dec}

@@ -100,9 +100,17 @@ class Trainer:
         return self.cfg["l1_coeff"]
 
     def step_async(self, on_losses=None):
-        """Launch one full step (no host sync); returns the device scalars tensor.
-        on_losses(scalars): called right after the forward's loss scalars are enqueued, before the
-        backward / clip / Adam launches."""
+        """Launch one full step (no host sync); returns the device scalars tensor, which torch's current
+        stream may read right away (it is ordered after the side-stream loss tail that writes it).
+        on_losses(scalars): called (on the side stream) right after the loss scalars are enqueued, before
+        the backward / clip / Adam launches."""
+        scalars, done = self._launch_step(on_losses)
+        torch.cuda.current_stream(scalars.device).wait_event(done)
+        return scalars
+
+    def _launch_step(self, on_losses):
+        """The step's launches; returns (ws.scalars, the event that marks the loss tail's end).  step()
+        does not order torch's stream after the tail (the host waits for the loss copy instead)."""
         cc = self.crosscoder
         raw, factor = self.buffer.next_raw()
         raw = cc.pad_input(raw)  # (zero columns only when d_in % 8 != 0)
@@ -113,7 +121,7 @@ class Trainer:
         # prep, G1, G2 + the loss rows (one pass where decode_loss_t serves the shape)
         engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None, finalize=False)
         # the loss scalars (+ their host copy) on the side stream, beside G3 (read by nothing on this stream)
-        engine.loss_finalize_beside(ws, side, on_losses)
+        done = engine.loss_finalize_beside(ws, side, on_losses)
         l1c = self.get_l1_coeff()
         # clip_grad_norm_(max_norm=1.0), trainer.py:46
         engine.backward(ws, P, opt.grads, l1c, clip=1.0)
@@ -124,7 +132,7 @@ class Trainer:
                              side_stream=side)
         self.scheduler.step()
         self._last_l1c = l1c
-        return ws.scalars
+        return ws.scalars, done
 
     def _copy_losses(self, scalars):
         # the step's single device->host copy, enqueued (on the side stream) as soon as the forward has
@@ -150,7 +158,7 @@ class Trainer:
         self.crosscoder.arena().wait_pending()
 
     def step(self):
-        self.step_async(on_losses=self._copy_losses)
+        self._launch_step(self._copy_losses)
         self._copied.synchronize()
         s = self._host[:6].tolist()
         l1c = self._last_l1c

@@ -445,7 +445,10 @@ def test_full_size_step_deterministic(gpu, full_size_case):
 @pytest.mark.parametrize("B,n,d,h", [(4096, 2, 2304, 1024),   # config-2 columns: 256 main tiles + 8-way split
                                      (4000, 2, 2304, 512),    # split, ragged last row block
                                      (1000, 2, 256, 1024),    # whole-tile grid only, ragged rows
-                                     (512, 4, 64, 384)])      # n = 4, d = 64
+                                     (512, 4, 64, 384),       # n = 4, d = 64
+                                     (3968, 2, 2304, 512),    # split, last 256-row tile half empty
+                                     (8, 2, 64, 256),         # B <= 32: more fused partial rows than loss rows
+                                     (32, 2, 128, 256)])
 def test_fused_decode_loss_matches_two_pass(gpu, B, n, d, h):
     """G2 + loss in one pass (cc_decode_loss_t: the loss as the GEMM epilogue, the split-K leftover summed
     in reduce_splits' order) vs the two-pass form (cc_decode_fwd_ws_t + cc_loss_fwd_bwd_rows_t):
@@ -465,6 +468,7 @@ def test_fused_decode_loss_matches_two_pass(gpu, B, n, d, h):
         G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
         ws.g_recon.fill_(float("nan"))
         ws.g_recon_t.fill_(float("nan"))
+        ws.loss_colpart.fill_(float("nan"))  # every partial row the backward reduces must be written
         if fused:
             engine.forward(ws, a, raw, factor)
             assert ws.row_ncb == d // 64

@@ -214,7 +214,7 @@ def test_shard_range_and_clip_combine():
     assert sharded.clip_sums_for_allreduce(s, 1).tolist() == [1, 2, 3, 0]
 
 
-def _init_worker(rank, world, port, q, enc_dtype, tmpdir):
+def _init_worker(rank, world, port, q, enc_dtype, tmpdir, d_in):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -222,7 +222,7 @@ def _init_worker(rank, world, port, q, enc_dtype, tmpdir):
         import crosscoder_amd as ca
         from crosscoder_amd import crosscoder as ccmod
 
-        cfg = {"seed": 49, "dict_size": 96, "d_in": 24, "enc_dtype": enc_dtype, "dec_init_norm": 0.08,
+        cfg = {"seed": 49, "dict_size": 96, "d_in": d_in, "enc_dtype": enc_dtype, "dec_init_norm": 0.08,
                "device": "cpu"}
         lo, hi = sharded.shard_range(cfg["dict_size"], world, rank)
         cc = sharded.shard_crosscoder(cfg, lo, hi)
@@ -231,20 +231,28 @@ def _init_worker(rank, world, port, q, enc_dtype, tmpdir):
         assert torch.equal(cc.W_dec.detach(), full.W_dec.detach()[lo:hi])
         assert torch.equal(cc.W_enc.detach(), full.W_enc.detach()[:, :, lo:hi])
         sd = sharded.gather_state_dict(cc, cfg["dict_size"])
-        ref = full.state_dict()
+        ref = full.reference_state_dict()
         assert list(sd) == list(ref)
         for k in ref:
             assert torch.equal(sd[k], ref[k]) and sd[k].stride() == ref[k].stride(), k
+        # the checkpoint path: gathered on rank 0 only (host tensors), the same dict
+        sd0 = sharded.gather_state_dict(cc, cfg["dict_size"], dst=0)
         if rank == 0:
-            ccmod.write_checkpoint(sd, cfg, save_dir=pathlib.Path(tmpdir), version=0)
+            assert list(sd0) == list(ref)
+            for k in ref:
+                assert sd0[k].device.type == "cpu"
+                assert torch.equal(sd0[k], ref[k]) and sd0[k].stride() == ref[k].stride(), k
+            ccmod.write_checkpoint(sd0, cfg, save_dir=pathlib.Path(tmpdir), version=0)
+        else:
+            assert sd0 is None
         dist.barrier()
         q.put((rank, True))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("enc_dtype", ["fp32", "bf16"])
-def test_sharded_init_is_reference_slice_and_gathers_back(enc_dtype, tmp_path):
+@pytest.mark.parametrize("enc_dtype,d_in", [("fp32", 24), ("bf16", 24), ("bf16", 20)])
+def test_sharded_init_is_reference_slice_and_gathers_back(enc_dtype, d_in, tmp_path):
     """ShardedTrainer's default init (shard_crosscoder) gives rank r latents [lo, hi) of exactly the
     crosscoder the reference builds for the whole dictionary (crosscoder.py:31-62), and
     gather_state_dict reassembles the reference state_dict (values, key order, W_enc strides); the
@@ -253,7 +261,7 @@ def test_sharded_init_is_reference_slice_and_gathers_back(enc_dtype, tmp_path):
     port = 29500 + random.randint(2001, 4000)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_init_worker, args=(r, world, port, q, enc_dtype, str(tmp_path))) for r in range(world)]
+    procs = [ctx.Process(target=_init_worker, args=(r, world, port, q, enc_dtype, str(tmp_path), d_in)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=300) for _ in range(world))
@@ -267,6 +275,6 @@ def test_sharded_init_is_reference_slice_and_gathers_back(enc_dtype, tmp_path):
 
     cfg = json.load(open(tmp_path / "0_cfg.json"))
     sd = torch.load(tmp_path / "0.pt", weights_only=True)
-    ref = ca.CrossCoder(cfg).state_dict()
+    ref = ca.CrossCoder(cfg).reference_state_dict()
     for k in ref:
         assert torch.equal(sd[k], ref[k]) and sd[k].stride() == ref[k].stride(), k
