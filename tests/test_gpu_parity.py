@@ -45,6 +45,13 @@ def envelope_ok(ours, ref, truth, floor=2e-3):
     return e_ours <= 2 * e_ref + floor, (e_ours, e_ref)
 
 
+def assert_fused_loss_path(cc, cfg):
+    """bf16 fixtures with d % 64 == 0 must reach the shipped fused G2 + loss kernel (cc_decode_loss_t)."""
+    if cfg["enc_dtype"] == "bf16" and cfg["d_in"] % 64 == 0:
+        ws = cc._ws
+        assert ws is not None and ws.fused_ncb == cfg["d_in"] // 64 and ws.row_ncb == ws.fused_ncb
+
+
 def make_cc(cfg, P, device, n_models):
     cfg = dict(cfg, device=str(device))
     cc = ca.CrossCoder(cfg, n_models=n_models)
@@ -183,6 +190,7 @@ def test_forward_parity(gpu, name):
         recon = cc.decode(acts.to(gpu)).cpu()
         lo = cc.get_losses(xg)
     torch.cuda.synchronize()
+    assert_fused_loss_path(cc, cfg)
     tlo, _, tpre = truth_fp64(x, P, 0.0)
     fw = r["fwd"]
     if dt == torch.float32:
@@ -234,6 +242,7 @@ def test_backward_parity(gpu, name):
     dt = O.DTYPES[cfg["enc_dtype"]]
     cc = make_cc(cfg, P, gpu, r["n_models"])
     lo = cc.get_losses(x.to(gpu))
+    assert_fused_loss_path(cc, cfg)
     (lo.l2_loss + 2.0 * lo.l1_loss).backward()
     torch.cuda.synchronize()
     _, tg, _ = truth_fp64(x, P, 2.0)
@@ -292,6 +301,7 @@ def test_trainer_steps(gpu, name):
     fp32 = dt == torch.float32
     for s in range(steps):
         d = tr.step()
+        assert_fused_loss_path(cc, cfg)
         ref = r["steps"]["loss_dicts"][s]
         assert list(d) == list(ref)
         assert d["l1_coeff"] == ref["l1_coeff"] and d["lr"] == ref["lr"]
@@ -439,6 +449,52 @@ def test_full_size_step_deterministic(gpu, full_size_case):
     assert outs[0][0] == outs[1][0] and outs[0][1] == outs[1][1]
     assert torch.equal(outs[0][2], outs[1][2])
     assert outs[0][1]["l2_loss"] < outs[0][0]["l2_loss"]
+
+
+def test_full_size_config2_trainer_steps_match_oracle(gpu, full_size_case):
+    """BASELINE config 2 through the shipped schedule (Trainer.step: fused G2 + loss, G4G5 + grad tail + clip
+    in one launch, encoder / decoder Adam halves on two streams) vs the oracle's fp32 OracleTrainer.step
+    (trainer.py:41-63) on the same bf16-valued inputs and init, two steps (l1_coeff 0 then 2): the 9-key loss
+    dicts, the clip total norm / coefficient, and params + both Adam moments after each step, within the
+    SURVEY 8c bf16 envelope (bounds ~2x the values measured on MI355X)."""
+    cfg, P, buf, factor, x = full_size_case
+    cfg = dict(cfg, batch_size=4096, num_tokens=4096 * 20, lr=5e-5, beta1=0.9, beta2=0.999, l1_coeff=2)
+    cc = make_cc(cfg, P, gpu, 2)
+    tr = ca.Trainer(dict(cc.cfg), buffer=_Replay([buf, buf], [factor, factor], gpu), crosscoder=cc)
+    torch.set_num_threads(max(1, torch.get_num_threads()))
+    orc = O.OracleTrainer(dict(cfg, enc_dtype="fp32"), {k: v.float() for k, v in P.items()})
+    x32 = x.to(torch.bfloat16).float()
+    lr = cfg["lr"]
+    for s in range(2):
+        d = tr.step()
+        clip = cc._ws.clip_out[:2].cpu()
+        st = tr.optimizer.state  # (orders after the side-stream decoder half)
+        ours = {k: (getattr(cc, k).detach().float().cpu(), st[getattr(cc, k)]["exp_avg"].float().cpu(),
+                    st[getattr(cc, k)]["exp_avg_sq"].float().cpu()) for k in O.PARAM_ORDER}
+        ref = orc.step(x32)
+        assert list(d) == list(ref)
+        assert d["l1_coeff"] == ref["l1_coeff"] and d["lr"] == ref["lr"], s
+        for k, tol in (("l2_loss", 1e-2), ("l1_loss", 1e-2), ("loss", 1e-2)):
+            assert math.isclose(d[k], ref[k], rel_tol=tol, abs_tol=1e-6), (s, k, d[k], ref[k])
+        for k in ("explained_variance", "explained_variance_A", "explained_variance_B"):
+            assert abs(d[k] - ref[k]) <= 1e-2, (s, k, d[k], ref[k])
+        assert abs(d["l0_loss"] - ref["l0_loss"]) <= 2e-3 * cfg["dict_size"], (s, d["l0_loss"], ref["l0_loss"])
+        tn = orc.last_total_norm.item()
+        assert math.isclose(clip[1].item(), tn, rel_tol=2e-2), (s, clip[1].item(), tn)
+        assert math.isclose(clip[0].item(), min(1.0, 1.0 / (tn + 1e-6)), rel_tol=2e-2), (s, clip[0].item())
+        for k in O.PARAM_ORDER:
+            p, m, v = ours[k]
+            pr = orc.P[k].detach()
+            # Adam's update is ~lr * sign(m): params agree to the bf16 rounding of the result except where a
+            # tiny gradient's sign differs between the two precisions (then ~2 lr apart)
+            diff = (p - pr).abs()
+            close = (diff <= _bf16_ulp(pr) + 0.05 * lr).float().mean().item()
+            assert close >= 0.97, (s, k, close)
+            assert diff.max().item() <= 4 * _bf16_ulp(pr).max().item() + 3 * lr, (s, k, diff.max().item() / lr)
+            tol = 0.2 if k == "W_enc" else 3e-2
+            em, ev = rel(m, orc.m[k]), rel(v, orc.v[k])
+            print(f"step {s} {k}: params close {close:.4f}, exp_avg rel {em:.2e}, exp_avg_sq rel {ev:.2e}")
+            assert em <= tol and ev <= 2 * tol, (s, k, em, ev)
 
 
 # ----------------------------------------------------------------------------- batch slices / sharded
@@ -689,16 +745,17 @@ def test_tiled_decoder_adam_matches_flat(gpu, h, max_blocks):
     assert torch.equal(nm1, nm2) and torch.equal(tn1, tn2) and torch.equal(inv1, inv2)
 
 
-def test_sharded_trainer_world1_matches_trainer(gpu):
-    """ShardedTrainer over a 1-rank RCCL group (the sliced async all-reduce path, 4 slices) takes
-    the same steps as the single-GPU Trainer."""
+@pytest.mark.parametrize("comm", ["all_reduce", "reduce_scatter"])
+def test_sharded_trainer_world1_matches_trainer(gpu, comm):
+    """ShardedTrainer over a 1-rank RCCL group (the sliced async all-reduce path, 4 slices, or the
+    reduce-scatter + all-gather exchange) takes the same steps as the single-GPU Trainer."""
     import os
 
     import torch.distributed as dist
     from crosscoder_amd import sharded
 
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", str(29600 + os.getpid() % 1000))
+    os.environ["MASTER_PORT"] = str(29600 + os.getpid() % 1000 + (comm == "reduce_scatter"))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
     try:
         B, n, d, h = 1024, 2, 256, 2048
@@ -710,7 +767,7 @@ def test_sharded_trainer_world1_matches_trainer(gpu):
             if which == "single":
                 tr = ca.Trainer(cfg, buffer=buf, crosscoder=ca.CrossCoder(cfg))
             else:
-                tr = sharded.ShardedTrainer(cfg, buffer=buf, recon_chunks=4)
+                tr = sharded.ShardedTrainer(cfg, buffer=buf, recon_chunks=4, comm=comm)
             dicts.append([tr.step() for _ in range(3)])
             torch.cuda.synchronize()
             if which == "single":

@@ -271,6 +271,9 @@ def main():
         run_case(ref_cc, ref_tr, f"step_b64_n2_d32_h256_{dt}", 64, 2, 32, 256, dt, steps=2)
         run_case(ref_cc, ref_tr, f"step_b96_n2_d40_h200_{dt}", 96, 2, 40, 200, dt, steps=2, seed=1)
         run_case(ref_cc, ref_tr, f"step_b64_n4_d32_h128_{dt}", 64, 4, 32, 128, dt, steps=2, seed=2)
+        # d % 64 == 0: the shapes the fused G2 + loss epilogue (cc_decode_loss_t) serves in bf16
+        run_case(ref_cc, ref_tr, f"step_b256_n2_d64_h512_{dt}", 256, 2, 64, 512, dt, steps=3, seed=4)
+        run_case(ref_cc, ref_tr, f"step_b128_n4_d64_h256_{dt}", 128, 4, 64, 256, dt, steps=3, seed=5)
     run_case(ref_cc, ref_tr, "dyadic_b64_n2_d32_h128_fp32", 64, 2, 32, 128, "fp32", steps=1, seed=3, dyadic=True)
     run_buffer_case(ref_buf)
     run_ckpt_case(ref_cc)
