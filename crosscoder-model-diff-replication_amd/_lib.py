@@ -4,12 +4,16 @@ The library is built in-tree (`make -C crosscoder-model-diff-replication_amd/csr
 `__graft_entry__.build()`) and loaded from this package directory.  There is no fallback:
 if the library is missing every compute entry point raises.
 """
+import contextlib
 import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcrosscoder_hip.so")
-DEFAULT_PP_MASK = 5  # CC_PP_MASK the library is built with (csrc/gemm.hip)
+# test-only build of the same kernels that also exports the launch-form setters (csrc/Makefile)
+DEBUG_LIB_PATH = os.path.join(_HERE, "libcrosscoder_hip_dbg.so")
+DEFAULT_PP_MASK = 5  # the ping-pong layouts both libraries default to (csrc/gemm.hip)
+DEBUG_SETTERS = ("cc_debug_set_pp_mask", "cc_debug_set_pp_fast", "cc_debug_set_dec_one_launch")
 
 CC_BF16 = 1
 CC_F32 = 2
@@ -89,19 +93,14 @@ SIGNATURES = {
 }
 
 _lib = None
+_debug = None
 
 
 class HipLibraryMissing(RuntimeError):
     pass
 
 
-def load(path=None):
-    """Load (once) and type the in-tree library; raises HipLibraryMissing if it is not built.  (A tool
-    may pass the path of an experiment build on the FIRST call; the product never does.)"""
-    global _lib
-    if _lib is not None:
-        return _lib
-    path = path or LIB_PATH
+def _open(path):
     if not os.path.exists(path):
         raise HipLibraryMissing(
             f"{path} not found: build it with `make -C {os.path.dirname(path)}/csrc` "
@@ -111,19 +110,47 @@ def load(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    # tuning hook outside the public ABI: which bf16 layouts run the ping-pong GEMM loop
-    lib.cc_debug_set_pp_mask.restype = None
-    lib.cc_debug_set_pp_mask.argtypes = [ctypes.c_int]
-    lib.cc_debug_set_tail_fence.restype = None
-    lib.cc_debug_set_tail_fence.argtypes = [ctypes.c_int]
-    lib.cc_debug_set_dec_one_launch.restype = None
-    lib.cc_debug_set_dec_one_launch.argtypes = [ctypes.c_int]
-    lib.cc_debug_set_pp_fast.restype = None
-    lib.cc_debug_set_pp_fast.argtypes = [ctypes.c_int]
-    lib.cc_debug_set_enc_grid.restype = None
-    lib.cc_debug_set_enc_grid.argtypes = [ctypes.c_int]
-    _lib = lib
     return lib
+
+
+def load(path=None):
+    """Load (once) and type the in-tree library; raises HipLibraryMissing if it is not built.  (A tool
+    may pass the path of an experiment build on the FIRST call; the product never does.)"""
+    global _lib
+    if _lib is not None:
+        return _lib
+    _lib = _open(path or LIB_PATH)
+    return _lib
+
+
+def load_debug():
+    """The test-only debug build (same kernels + cc_debug_set_* launch-form setters)."""
+    global _debug
+    if _debug is None:
+        lib = _open(DEBUG_LIB_PATH)
+        for name in DEBUG_SETTERS:
+            fn = getattr(lib, name)
+            fn.restype = None
+            fn.argtypes = [ctypes.c_int]
+        _debug = lib
+    return _debug
+
+
+@contextlib.contextmanager
+def debug_library():
+    """Route every ops.* call through the debug build for the duration (tests comparing launch forms);
+    its setters are reset to the product defaults on exit."""
+    global _lib
+    prev = load()
+    dbg = load_debug()
+    _lib = dbg
+    try:
+        yield dbg
+    finally:
+        dbg.cc_debug_set_pp_mask(DEFAULT_PP_MASK)
+        dbg.cc_debug_set_pp_fast(1)
+        dbg.cc_debug_set_dec_one_launch(1)
+        _lib = prev
 
 
 def check(rc):

@@ -215,9 +215,6 @@ int cc_gather_rows(const void* src, int64_t src_rows, const int64_t* perm, void*
   return CC_OK;
 }
 
-static int g_transpose_rows_fast = -1;  // -1: by shape
-void cc_debug_set_transpose_order(int rows_fast) { g_transpose_rows_fast = rows_fast; }
-
 int cc_transpose_b16(const void* src, int64_t rows, int64_t cols, int64_t ld_src, void* dst, int64_t ld_dst,
                      void* stream) {
   if (rows == 0 || cols == 0) return CC_OK;
@@ -228,7 +225,7 @@ int cc_transpose_b16(const void* src, int64_t rows, int64_t cols, int64_t ld_src
   if (!al16(src) || !al16(dst)) return CC_ERR_ALIGN;
   const unsigned nr = (unsigned)((rows + 63) / 64), nc = (unsigned)((cols + 63) / 64);
   // measured (tools/transpose_bench.py): walking the source rows first is faster when rows >= cols
-  const int rf = g_transpose_rows_fast < 0 ? (rows >= cols) : g_transpose_rows_fast;
+  const int rf = rows >= cols;
   hipLaunchKernelGGL(transpose_b16_kernel<false>, rf ? dim3(nr, nc) : dim3(nc, nr), dim3(256), 0,
                      (hipStream_t)stream, (const char*)src, (int)rows, (int)cols, ld_src, (char*)dst, ld_dst, rf,
                      nullptr, 0);
@@ -255,7 +252,7 @@ int cc_transpose_dec_norms(const void* W_dec, int64_t h, int64_t n, int64_t d, v
   if (h <= 0 || n <= 0 || d <= 0 || d % 64 || h % 8 || h / 64 >= 65535 || K / 64 >= 65535) return CC_ERR_SHAPE;
   if (!al16(W_dec) || !al16(W_dec_t)) return CC_ERR_ALIGN;
   const unsigned nr = (unsigned)((h + 63) / 64), nc = (unsigned)(K / 64);
-  const int rf = g_transpose_rows_fast < 0 ? (h >= K) : g_transpose_rows_fast;
+  const int rf = h >= K;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(transpose_b16_kernel<true>, rf ? dim3(nr, nc) : dim3(nc, nr), dim3(256), 0, st,
                      (const char*)W_dec, (int)h, (int)K, K, (char*)W_dec_t, h, rf, part, (int)(K / 64));

@@ -57,8 +57,6 @@ struct GemmArgs {
   float scale0;
   int flag;             // apply_relu
   int d_model, n_models;
-  void* dbg;            // diagnostic stamp buffer (CC_STAMPS / CC_PP_STAMPS builds only)
-  int stamp_base;       // first record of this GEMM in dbg (CC_PP_STAMPS)
   int k_step0, k_steps; // ping-pong split-K: contraction steps [k_step0, k_step0 + k_steps) (0 steps: all)
   void* out_t;          // ping-pong bf16 epilogue: also store the tile transposed, out_t[n][m] (ld ldt)
   int64_t ldt;
@@ -74,9 +72,6 @@ CC_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint64_t bytes) {
 }
 
 CC_DEV void dma16(__amdgpu_buffer_rsrc_t r, char* lds_base, uint32_t voff) {
-#ifdef CC_EXP_NOLOAD  // timing-only experiment build (never shipped): every lane out of range
-  voff = OOB;
-#endif
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_base, 16, (int)voff, 0, 0, 0);
 }
 
@@ -179,9 +174,6 @@ CC_DEV uint32_t dma_mn_base(int q, int cols_left, int64_t ld, int wave, int lane
   return ok ? (uint32_t)(((int64_t)k * ld + col) * G::ES) : OOB;
 }
 CC_DEV void dma16s(__amdgpu_buffer_rsrc_t r, char* lds_base, uint32_t voff, uint32_t soff) {
-#ifdef CC_EXP_NOLOAD
-  voff = OOB;
-#endif
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_base, 16, (int)voff, (int)soff, 0, 0);
 }
 
@@ -284,10 +276,7 @@ CC_DEV void tile_of_block(int bid, int nbm, int nbn, int& tm, int& tn) {
   int nwg = nbm * nbn;
   int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-#ifndef CC_TILE_GM
-#define CC_TILE_GM 4
-#endif
-  constexpr int GM = CC_TILE_GM;
+  constexpr int GM = 4;
   int per_group = GM * nbn;
   int g = wg / per_group;
   int first = g * GM;
@@ -354,19 +343,6 @@ struct EPB {
   static_assert(WaveGeom<BNT>::TN % JB == 0 && WaveGeom<BNT>::TN % JB_W == 0, "batch must divide the column groups");
 };
 
-// PIPE selects the K pipeline: KROW bytes per KC row per K-step and NST LDS stages.
-//   PIPE 0: KROW 128, NST 2 (prefetch 1 step)   PIPE 1: KROW 64, NST 4 (prefetch 3 steps)
-template <int PIPE> struct Pipe;
-template <> struct Pipe<0> { static constexpr int KROW = 128, NST = 2; };
-template <> struct Pipe<1> { static constexpr int KROW = 64, NST = 4; };
-#ifndef CC_GEMM_PIPE
-#define CC_GEMM_PIPE 0
-#endif
-
-#ifndef CC_FRAG_MODE
-#define CC_FRAG_MODE 1
-#endif
-
 template <int N> CC_DEV void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   // gfx9 s_waitcnt encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]
@@ -375,10 +351,12 @@ template <int N> CC_DEV void wait_vmcnt() {
 
 #include "gemm_epilogue.h"
 
-template <int DT, bool AKC, bool BKC, int EPI, int BNT, int PIPE = CC_GEMM_PIPE>
+// The general two-stage kernel (fp32 mode, BN 288, shapes off the ping-pong path): K-step = KROW bytes of
+// contraction per KC row, NST LDS stages (prefetch distance 1).
+template <int DT, bool AKC, bool BKC, int EPI, int BNT>
 __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
   using WG = WaveGeom<BNT>;
-  constexpr int KROW = Pipe<PIPE>::KROW, NST = Pipe<PIPE>::NST;
+  constexpr int KROW = 128, NST = 2;
   constexpr int ES = DT == CC_BF16 ? 2 : 4;
   constexpr int BK = KROW / ES;
   constexpr int KK = KROW / 64;  // 32-element (bf16) / 16-element (fp32) slices per K-step
@@ -480,46 +458,11 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 #pragma unroll
     for (int q = 0; q < D; ++q) dma(q, p, p, p < nk);
 
-#ifdef CC_STAMPS  // diagnostic build only: per-wave cycle sums of {DMA wait, barrier, compute}
-  uint64_t st_wait = 0, st_bar = 0, st_comp = 0, st_t0 = 0, st_pro = 0;
-  auto stamp = [&]() -> uint64_t {
-    uint64_t t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-  };
-  st_t0 = stamp();
-  uint64_t st_prev = st_t0;
-#endif
   for (int kt = 0; kt < nk; ++kt) {
     // step kt landed (this wave's DMAs): every step issues exactly D DMAs per wave, so the
     // NST-2 younger steps may stay in flight
-#ifdef CC_STAMPS
-    {
-      uint64_t t = stamp();
-      if (kt) st_comp += t - st_prev; else st_pro += t - st_prev;
-      st_prev = t;
-    }
-#endif
-#ifndef CC_EXP_NOWAIT  // timing-only experiment builds (never shipped): skip the DMA wait
     wait_vmcnt<(NST - 2) * D>();
-#endif
-#ifdef CC_STAMPS
-    {
-      uint64_t t = stamp();
-      st_wait += t - st_prev;
-      st_prev = t;
-    }
-#endif
     __builtin_amdgcn_s_barrier();  // ... for every wave; stage (kt-1)%NST is free again
-#ifdef CC_STAMPS
-    {
-      uint64_t t = stamp();
-      st_bar += t - st_prev;
-      st_prev = t;
-    }
-#endif
     const int nxt = kt + NST - 1;
     const bool pf = nxt < nk;
     const int snx = nxt % NST;
@@ -531,11 +474,10 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 #pragma unroll
       for (int q = 0; q < D; ++q) dma(q, nxt, snx, pf);
     }
-#if CC_FRAG_MODE > 0
     if constexpr (DT == CC_BF16) {
-      // all fragments of the step (mode 2) or of each 32-k slice (mode 1) are read first, so a
-      // wave waits for LDS once per slice and then issues its MFMAs back to back
-      constexpr int KB = CC_FRAG_MODE == 2 ? KK : 1;
+      // all fragments of each 32-k slice are read first, so a wave waits for LDS once per slice and
+      // then issues its MFMAs back to back
+      constexpr int KB = 1;
 #pragma unroll
       for (int k0 = 0; k0 < KK; k0 += KB) {
         bf16x8 a[KB][WG::TM], b[KB][WG::TN];
@@ -567,31 +509,9 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
         __builtin_amdgcn_sched_group_barrier(0x100, KB * (WG::TM * (AKC ? 1 : 2) + WG::TN * (BKC ? 1 : 2)), 0);
         __builtin_amdgcn_sched_group_barrier(0x008, KB * WG::TM * WG::TN, 0);
       }
-    } else
-#endif
+    } else {
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      if constexpr (DT == CC_BF16) {
-        bf16x8 b[WG::TN];
-#pragma unroll
-        for (int j = 0; j < WG::TN; ++j) {
-          const int c0 = wc * WG::WTN + j * 16;
-          b[j] = BKC ? frag_kc_bf16<KROW>(lb, c0, kk, lane) : frag_mn_bf16_at<BNT, KROW>(lb, offB[j], kk);
-        }
-#pragma unroll
-        for (int i = 0; i < WG::TM; ++i) {
-          if (SPREAD && kk == 0) {
-#pragma unroll
-            for (int q = 0; q < D; ++q)
-              if (q * WG::TM / D == i) dma(q, nxt, snx, pf);
-          }
-          const int r0 = wr * WG::WTM + i * 16;
-          bf16x8 a = AKC ? frag_kc_bf16<KROW>(la, r0, kk, lane) : frag_mn_bf16_at<BM, KROW>(la, offA[i], kk);
-#pragma unroll
-          for (int j = 0; j < WG::TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a, acc[i][j], 0, 0, 0);
-        }
-      } else {
+      for (int kk = 0; kk < KK; ++kk) {
         f32x4 b[WG::TN];
 #pragma unroll
         for (int j = 0; j < WG::TN; ++j) {
@@ -617,17 +537,6 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
     }
   }
   wait_vmcnt<0>();  // drain the junk-slot DMAs of the last NST-1 steps
-#ifdef CC_STAMPS
-  {
-    uint64_t t = stamp();
-    st_comp += t - st_prev;
-    uint64_t* dbg = (uint64_t*)args.dbg;
-    if (dbg && lane == 0) {
-      uint64_t* o = dbg + ((uint64_t)blockIdx.x * 8 + wave) * 6;
-      o[0] = st_pro; o[1] = st_wait; o[2] = st_bar; o[3] = st_comp; o[4] = t - st_t0; o[5] = nk;
-    }
-  }
-#endif
 
   gemm_epilogue<DT, EPI, BNT>(args, acc, tm, m0, n0, wr, wc, lane, blockIdx.x * 8 + wave);
 }
@@ -658,7 +567,6 @@ template <bool AKC, bool BKC, int EPI0, int EPI1>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmArgs a0, const GemmArgs a1,
                                                                    const WgradTail tl) {
   __shared__ __attribute__((aligned(16))) char smem[EPI0 == EPI_WGDEC || EPI1 == EPI_WGDEC ? PP_LDS_W : PP_LDS];
-#ifndef CC_EXP_TAIL_NOBIAS  // timing-only experiment builds (never shipped): parts of the tail left out
   {
     const int grp = threadIdx.x >> 8, t = threadIdx.x & 255;
     float(*red)[RED_COLS] = (float(*)[RED_COLS])(smem + grp * 4 * RED_COLS * sizeof(float));
@@ -672,7 +580,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmAr
       __syncthreads();
     }
   }
-#endif
   const int nb0 = a0.nbm * a0.nbn;
   for (int t = blockIdx.x; t < 2 * nb0; t += gridDim.x) {
     const int tid = pp_opaque_tid();
@@ -680,9 +587,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmAr
     else pp_tile<AKC, BKC, EPI1>(a1, smem, t - nb0, tid);
     pp_tile_boundary();
   }
-#ifdef CC_EXP_TAIL_NOARRIVE
-  return;
-#endif
   // this workgroup's squared sums per parameter: its tiles' per-wave partials (G5 -> W_enc, G4 -> W_dec)
   // and its bias blocks' partials, written by its own waves (visible after their stores drained + the barrier)
   __builtin_amdgcn_s_waitcnt(0);
@@ -722,7 +626,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmAr
   }
   __syncthreads();
   if (!*last) return;
-#ifndef CC_EXP_TAIL_NOCLIP
   {
     double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int w = threadIdx.x; w < (int)gridDim.x; w += NTHR)
@@ -731,25 +634,33 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmAr
     clip_finish<NTHR>(tl.clip, s, (double(*)[NTHR / 64])(smem + 64),
                       (float*)(smem + 64 + 8 * (NTHR / 64) * sizeof(double)));
   }
-#endif
   if (threadIdx.x == 0) atomicExch(tl.counter, 0u);
 }
 
+// Launch-form switches.  The product library fixes them; the test-only debug build (-DCC_DEBUG_HOOKS,
+// libcrosscoder_hip_dbg.so) exports setters so the parity tests can run the alternate forms in one process
+// and compare their bits.
+//   pp_mask     bf16 GEMM layouts that run the ping-pong kernel (gemm_pp.h, 256 x 256 tiles): bit 0 KC/KC
+//               (G1, G3), bit 1 KC/MN (G2), bit 2 MN/MN (G4, G5); the others run gemm_kernel
+//   pp_fast     the whole-tile ReLU epilogue form of G1 / G3 (same bits as the general form)
+//   dec_one     G2's main tiles and split-K units as one launch (0: two launches, same bits)
+#ifdef CC_DEBUG_HOOKS
+static int g_pp_mask = 5, g_pp_fast = 1, g_dec_one_launch = 1;
+#define CC_DEBUG_API extern "C" __attribute__((visibility("default")))
+CC_DEBUG_API void cc_debug_set_pp_mask(int mask) { g_pp_mask = mask; }
+CC_DEBUG_API void cc_debug_set_pp_fast(int on) { g_pp_fast = on; }
+CC_DEBUG_API void cc_debug_set_dec_one_launch(int on) { g_dec_one_launch = on; }
+#else
+constexpr int g_pp_mask = 5, g_pp_fast = 1, g_dec_one_launch = 1;
+#endif
 // N = n*d multiple of 288 (and an MN-contiguous bf16 B operand): 256 x 288 tiles.  (The fp32
 // parity mode keeps 256 x 256: its 288-wide variant exceeds 256 VGPRs.)
-// bf16 GEMMs whose layout bit is set in CC_PP_MASK run the ping-pong kernel (gemm_pp.h, 256 x 256
-// tiles): bit 0 KC/KC (G1, G3), bit 1 KC/MN (G2), bit 2 MN/MN (G4, G5).
-#ifndef CC_PP_MASK
-#define CC_PP_MASK 5
-#endif
-static int g_pp_mask = CC_PP_MASK;  // cc_debug_set_pp_mask: in-process A/B of the two loops
 static bool use_pp(int64_t N, bool akc, bool bkc, int dtype) {
   // (N % 8: the ping-pong epilogue moves whole 16-byte column chunks through LDS)
   if (dtype != CC_BF16 || (!akc && bkc) || N % 8) return false;
   const int bit = akc && bkc ? 0 : (akc ? 1 : 2);
   return (g_pp_mask >> bit) & 1;
 }
-extern "C" void cc_debug_set_pp_mask(int mask) { g_pp_mask = mask; }
 // 1 when the transposed-operand entries (cc_encode_fwd_t, cc_dacts_bwd_t, cc_wgrad_both_t's fused
 // form) serve this step shape.
 extern "C" int cc_transposed_ok(int64_t B, int64_t K, int64_t h, int dtype) {
@@ -762,17 +673,8 @@ static int pick_bn(int64_t N, bool akc, bool bkc, int dtype) {
 }
 static int64_t n_blocks(int64_t M, int64_t N, int bn) { return ((M + BM - 1) / BM) * ((N + bn - 1) / bn); }
 
-#if defined(CC_STAMPS) || defined(CC_PP_STAMPS)
-static bool g_split_stamps_only = true;  // decode_fwd_ws: stamp the split pass, not the main launch
-static void* g_stamp_buf = nullptr;
-extern "C" void cc_debug_set_stamp_buffer(void* p) { g_stamp_buf = p; }
-#endif
-
 template <int DT, bool AKC, bool BKC, int EPI, int BNT>
 static int launch(GemmArgs a, hipStream_t st) {
-#ifdef CC_STAMPS
-  a.dbg = g_stamp_buf;
-#endif
   a.nbm = (a.M + BM - 1) / BM;
   a.nbn = (a.N + BNT - 1) / BNT;
   dim3 grid(a.nbm * a.nbn), block(NTHR);
@@ -784,7 +686,6 @@ static int launch(GemmArgs a, hipStream_t st) {
 // grid of a ping-pong launch over `tiles` output tiles: one workgroup per tile, or (persistent tile loop)
 // at most one per CU
 static int pp_grid(int64_t tiles) {
-#if CC_PP_PERSIST
   static int cus = 0;
   static std::once_flag once;
   std::call_once(once, [] {
@@ -796,38 +697,15 @@ static int pp_grid(int64_t tiles) {
       cus = 256;
   });
   return (int)(tiles < cus ? tiles : cus);
-#else
-  return (int)tiles;
-#endif
 }
 
-#ifndef CC_PP_FAST  // the epilogue fast form for whole-tile ReLU launches (0: general form, A/B)
-#define CC_PP_FAST 1
-#endif
-static int g_pp_fast = CC_PP_FAST;  // cc_debug_set_pp_fast: in-process check that both forms give the same bits
-extern "C" void cc_debug_set_pp_fast(int on) { g_pp_fast = on; }
-// workgroups of the persistent encoder GEMM (G1): the CUs it leaves free run the side stream's decoder-half
-// Adam beside it (0: one per CU).  Multiple of 8 (the tile -> XCD map).
-#ifndef CC_ENC_GRID
-#define CC_ENC_GRID 0
-#endif
-static int g_enc_grid = CC_ENC_GRID;
-extern "C" void cc_debug_set_enc_grid(int n) { g_enc_grid = n > 0 ? n & ~7 : 0; }
-static int enc_grid(int tiles) {
-  int g = pp_grid(tiles);
-  return g_enc_grid > 0 && g_enc_grid < g ? g_enc_grid : g;
-}
 template <bool AKC, bool BKC, int EPI>
 static int launch_pp(GemmArgs a, hipStream_t st) {
-#ifdef CC_PP_STAMPS
-  a.dbg = g_stamp_buf;
-#endif
   a.nbm = (a.M + BM - 1) / BM;
   a.nbn = (a.N + 255) / 256;
   if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
     if (g_pp_fast && a.M % BM == 0 && a.N % 256 == 0 && (EPI == EPI_DACTS || a.flag)) {  // whole tiles, ReLU on
-      const int grid = EPI == EPI_ENC ? enc_grid(a.nbm * a.nbn) : pp_grid(a.nbm * a.nbn);
-      hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI, true>), dim3(grid), dim3(NTHR), 0, st, a);
+      hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI, true>), dim3(pp_grid(a.nbm * a.nbn)), dim3(NTHR), 0, st, a);
       CC_LAUNCH_CHECK();
       return CC_OK;
     }
@@ -1013,13 +891,6 @@ int64_t cc_decode_ws_floats(int64_t B, int64_t h, int64_t K, int dtype) {
 
 }  // extern "C"
 
-// G2's main tiles and split-K units as one launch (1) or two (0): cc_debug_set_dec_one_launch (A/B)
-#ifndef CC_DEC_ONE_LAUNCH
-#define CC_DEC_ONE_LAUNCH 1
-#endif
-static int g_dec_one_launch = CC_DEC_ONE_LAUNCH;
-extern "C" void cc_debug_set_dec_one_launch(int on) { g_dec_one_launch = on; }
-
 // BKC: W_dec given transposed, W_dec_t [K][h] (both operands contract over h contiguously)
 template <bool BKC>
 static int decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, float* ws, int64_t ws_floats,
@@ -1047,18 +918,12 @@ static int decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, 
   a.out_f32 = recon_f32; a.ldo = K;
   int rc = check_gemm(a, dtype, true, BKC);
   if (rc) return rc;
-#ifdef CC_PP_STAMPS
-  if (g_split_stamps_only) a.dbg = nullptr;
-#endif
   GemmArgs t = {};
   t.A = acts; t.lda = h; t.B = (const bf16_t*)W_dec + (int64_t)p.nbn_main * 256 * (BKC ? h : 1); t.ldb = ldb;
   t.M = (int)B; t.N = p.tail_cols; t.K = (int)h;
   t.out = ws; t.ldo = p.tail_cols;
   t.nbm = (t.M + BM - 1) / BM;
   t.nbn = (t.N + 255) / 256;
-#ifdef CC_PP_STAMPS
-  t.dbg = g_stamp_buf;
-#endif
   if (g_dec_one_launch) {
     // main tiles and split units in one grid (gemm_pp_main_splitk_kernel)
     a.nbm = (a.M + BM - 1) / BM;
@@ -1356,10 +1221,6 @@ int cc_wgrad_both_t(const void* actsT, const void* g_reconT, const void* W_dec, 
   }
   a0.nbm = a1.nbm = (a0.M + BM - 1) / BM;
   a0.nbn = a1.nbn = (a0.N + 255) / 256;
-#ifdef CC_PP_STAMPS
-  a0.dbg = a1.dbg = g_stamp_buf;
-  a1.stamp_base = 4 * a0.nbm * a0.nbn;
-#endif
   hipLaunchKernelGGL((gemm_pp_dual_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(pp_grid(2 * a0.nbm * a0.nbn)), dim3(NTHR),
                      0, st, a0, a1);
   CC_LAUNCH_CHECK();
@@ -1463,10 +1324,6 @@ int cc_wgrad_both(const void* acts, const void* g_recon, const void* W_dec, cons
   }
   a0.nbm = a1.nbm = (a0.M + BM - 1) / BM;
   a0.nbn = a1.nbn = (a0.N + 255) / 256;
-#ifdef CC_PP_STAMPS
-  a0.dbg = a1.dbg = g_stamp_buf;
-  a1.stamp_base = 4 * a0.nbm * a0.nbn;
-#endif
   hipLaunchKernelGGL((gemm_pp_dual_kernel<false, false, EPI_WGDEC, EPI_WGENC>), dim3(pp_grid(2 * a0.nbm * a0.nbn)),
                      dim3(NTHR),
                      0, st, a0, a1);

@@ -14,10 +14,6 @@
 //            transfers.
 // N % 4 == 0 (host check): a lane's 4 columns are all in range or all out.
 
-#ifndef CC_EPI_DPP  // column sums of the epilogue by DPP row reductions (0: ds_bpermute shuffles, A/B)
-#define CC_EPI_DPP 1
-#endif
-
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
@@ -216,18 +212,7 @@ CC_DEV void enc_dacts_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT
     }
     if (args.col_part) {  // reduce over the 16 lanes (rows) that share these 4 columns
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-#if CC_EPI_DPP
-        csum[e] = row16_sum(csum[e]);
-#else
-        float s = csum[e];
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s += __shfl_xor(s, 4, 64);
-        s += __shfl_xor(s, 8, 64);
-        csum[e] = s;
-#endif
-      }
+      for (int e = 0; e < 4; ++e) csum[e] = row16_sum(csum[e]);
       if ((lane & 15) == 0 && fg.cv[j])
         st4<CC_F32>(args.col_part, (int64_t)(tm * WG::WARPS_M + wr) * N + n0 + fg.c0 + 16 * j, csum);
     }
@@ -355,11 +340,7 @@ CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e];
         if constexpr (EPI == EPI_WGDEC) {
-#ifndef CC_EXP_EPI_NOMATH  // timing-only experiment build (never shipped): input loaded, term not added
           if (l1term) {
-#else
-          if (l1term && lane > 64) {
-#endif
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] += cw[i][j] * V4<DT>::get(wraw[i][j % JB], e);
           }

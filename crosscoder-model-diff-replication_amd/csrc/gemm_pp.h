@@ -29,21 +29,6 @@
 // KC operands keep [256 rows][128 B] with chunk ^ (row & 7).
 
 #include <type_traits>
-#ifdef CC_EXP_G3REG
-#define CC_G3REG_ON(E) ((E) == EPI_DACTS)
-#else
-#define CC_G3REG_ON(E) false
-#endif
-
-#ifndef CC_PP_ORDER
-#define CC_PP_ORDER 1
-#endif
-#ifndef CC_PP_STAMPS_EPI  // (CC_PP_STAMPS builds) 1: stamp the epilogue's phases instead of the tile's
-#define CC_PP_STAMPS_EPI 0
-#endif
-#ifndef CC_PP_PRIO_BASE  // experiment: wave priority of the whole GEMM (vs concurrent side-stream kernels)
-#define CC_PP_PRIO_BASE 0
-#endif
 
 CC_DEV int pp_h(int k) { return ((k >> 1) & 1) | ((k >> 2) & 2); }
 
@@ -166,15 +151,6 @@ template <int EPI, bool FAST>
 CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char* smem, const int (&qb)[4],
                             bool input_staged, int tm, int m0, int n0, int wr, int wc, int lane, int wave,
                             int wave_slot, const FragGeom<256>& fg, const EpiCols<CC_BF16, 256>& ecols) {
-#if defined(CC_EXP_NOEPI) || defined(CC_EXP_NOEPICORE)  // timing-only experiment builds (never shipped)
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
-#endif
-#ifdef CC_EXP_NOEPI
-  return;
-#endif
   const int rows = args.M - m0, cols = args.N - n0, ldo = (int)args.ldo;
   const void* in = EPI == EPI_DACTS || EPI == EPI_DLOSS
                        ? args.mask_src
@@ -186,9 +162,6 @@ CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int ci = q * 8 + wave;
-#ifdef CC_EXP_EPI_NOLOAD  // timing-only experiment build (never shipped): no epilogue input transfer
-        if (EPI != EPI_WGDEC)
-#endif
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_void*)(smem + qb[q >> 2] + (ci & 31) * 1024), 16,
                                                  (int)piece_off(ci, lane, rows, cols, ldo), 0, 0, 0);
       }
@@ -199,17 +172,8 @@ CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char
     __builtin_amdgcn_s_barrier();
   }
   const LdsIO io(smem, qb, wr, wc, lane);
-#ifndef CC_EXP_NOEPICORE
   epilogue_core<CC_BF16, EPI, 256, FAST>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, ecols, cw);
-#endif
-#if defined(CC_PP_STAMPS) && CC_PP_STAMPS_EPI
-  if (threadIdx.x == 0 && args.dbg)
-    ((uint64_t*)args.dbg)[(int64_t)args.stamp_base + (int64_t)(wave_slot / 8) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
   __syncthreads();
-#ifdef CC_EXP_NOSTORE  // timing-only experiment build (never shipped): no output tile stores
-  return;
-#endif
   if (args.out) {
     const __amdgpu_buffer_rsrc_t rout = tile_rsrc(args.out, args.ldo, m0, n0, args.M, args.N, 2);
 #pragma unroll
@@ -225,11 +189,7 @@ CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char
 
 constexpr int PP_LDS = 4 * 256 * 128;  // 2 buffers x (A | B) K-step images
 // + one 32 KB quarter of the W_dec tile, prefetched at tile start (dW_dec kernels: 160 KB in all)
-#ifndef CC_PP_NO_WPF
 constexpr int PP_LDS_W = PP_LDS + 256 * 128;
-#else
-constexpr int PP_LDS_W = PP_LDS;
-#endif
 
 // One output tile of one GEMM; bid = the tile's block index within that GEMM's grid.  FAST: every tile
 // of the launch lies inside the matrix and the ReLU is on (EPI_ENC / EPI_DACTS epilogue fast form).
@@ -243,7 +203,6 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadI
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
-  if (CC_PP_PRIO_BASE) __builtin_amdgcn_s_setprio(CC_PP_PRIO_BASE);
   int tm, tn;
   tile_of_block(bid, args.nbm, args.nbn, tm, tn);
   const int m0 = tm * BM, n0 = tn * 256;
@@ -253,9 +212,6 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadI
   {
     const char* a = (const char*)args.A;
     const char* b = (const char*)args.B;
-#ifdef CC_EXP_SAMEPANEL  // timing-only experiment build (never shipped): every tile reads tile (0, 0)'s panels
-    const int m0 = 0, n0 = 0;
-#endif
     if constexpr (AKC) {
       a += (int64_t)m0 * args.lda * 2;
       ra = make_rsrc(a, (uint64_t)(M - m0) * args.lda * 2);
@@ -289,11 +245,7 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadI
   // loop: quarter 3 at tile start into the extra 32 KB of LDS, quarters 0-2 by the DMA slots of
   // the steps past the end (T >= nk), which would otherwise zero-fill regions the loop no longer
   // reads (buffer nk&1's B and A images, buffer (nk+1)&1's B image).
-#ifndef CC_PP_NO_WPF
   const bool pf = EPI == EPI_WGDEC && args.scale0 != 0.f;
-#else  // experiment build: W_dec tile loaded after the loop (no prefetch, 128 KB LDS)
-  const bool pf = false;
-#endif
   const int erows = M - m0, ecols = N - n0, eldo = (int)args.ldo;
   __amdgpu_buffer_rsrc_t rw = ra;
   int qb[4] = {0, TILE, 2 * TILE, 3 * TILE};
@@ -341,11 +293,7 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadI
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const uint32_t v = vo[p][q];
-#ifdef CC_EXP_NOLOAD  // timing-only experiment build (never shipped): every lane out of range
-      const uint32_t off = OOB + 0 * (kin && v != OOB ? v + kadd : 0);
-#else
       const uint32_t off = (kin && v != OOB) ? v + kadd : OOB;
-#endif
       __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? ra : rb, (lds_void*)(dst + pp_ci(p, q, wave) * 1024), 16,
                                                (int)off, 0, 0, 0);
     }
@@ -397,26 +345,6 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadI
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       __builtin_amdgcn_sched_barrier(0);
-#if CC_PP_ORDER == 0
-      // phase p: A tiles 2p, 2p+1 x both k-slices; all B fragments read in phase 0
-      if (p == 0) {
-#pragma unroll
-        for (int j = 0; j < WG::TN; ++j) {
-          const int c0 = wc * WG::WTN + 16 * j;
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk)
-            bfr[j][kk] = BKC ? pp_frag_kc(lb, c0, kc_off[kk]) : pp_frag_mn(lb, c0, kk, mn_off[(c0 >> 4) & 3]);
-        }
-      }
-      bf16x8 afr[2][2];
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii) {
-        const int r0 = wr * WG::WTM + 16 * (2 * p + ii);
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          afr[ii][kk] = AKC ? pp_frag_kc(la, r0, kc_off[kk]) : pp_frag_mn(la, r0, kk, mn_off[(r0 >> 4) & 3]);
-      }
-#else
       // phase p: A tiles 4*(p>>1) .. +3 x k-slice p&1; the B fragments of k-slice p&1 are read in
       // phase p&1 (B read load per phase 8/8/0/0 fragments instead of 16/0/0/0).  Every output
       // still accumulates k-slice 0 before k-slice 1 of a step (bitwise the same sums).
@@ -434,54 +362,26 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadI
         const int r0 = wr * WG::WTM + 16 * (ib + ii);
         afr[ii] = AKC ? pp_frag_kc(la, r0, kc_off[kk]) : pp_frag_mn(la, r0, kk, mn_off[(r0 >> 4) & 3]);
       }
-#endif
       issue_t(tail, p, p < 2 ? t + 1 : t + 2);
-#ifndef CC_PP_EXP_NOWAIT  // timing-only experiment builds (never shipped): skip the DMA wait
       wait_vmcnt<6>();
-#endif
-#if CC_PP_ORDER != 0
       // the B region of this buffer is re-staged in phase 2 (one phase after these reads): retire
       // them before this phase's first barrier (WAR across the staggered wave groups)
       if (p == 1) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-#endif
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-#if CC_PP_PRIO
-      __builtin_amdgcn_s_setprio(1 + CC_PP_PRIO_BASE);
-#endif
-#if CC_PP_ORDER == 0
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-          for (int j = 0; j < WG::TN; ++j)
-            acc[2 * p + ii][j] = CC_G3REG_ON(EPI)
-                ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[ii][kk], bfr[j][kk], acc[2 * p + ii][j], 0, 0, 0)
-                : __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii][kk], acc[2 * p + ii][j], 0, 0, 0);
-#else
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
         for (int j = 0; j < WG::TN; ++j)
-          acc[ib + ii][j] = CC_G3REG_ON(EPI)
-              ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[ii], bfr[j][kk], acc[ib + ii][j], 0, 0, 0)
-              : __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii], acc[ib + ii][j], 0, 0, 0);
-#endif
-#if CC_PP_PRIO
-      __builtin_amdgcn_s_setprio(CC_PP_PRIO_BASE);
-#endif
+          acc[ib + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii], acc[ib + ii][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
     }
   };
   int t = 0;
-#ifndef CC_PP_SOFF
-#define CC_PP_SOFF 1
-#endif
   // steady state: every DMA is an operand DMA
-  if (CC_PP_SOFF && K % 64 == 0)
+  if (K % 64 == 0)
     for (; t < nk - 2; ++t) kstep(std::integral_constant<int, 2>{}, t);
   else
     for (; t < nk - 2; ++t) kstep(std::integral_constant<int, 0>{}, t);
@@ -492,26 +392,7 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadI
   EpiCols<CC_BF16, 256> evec;
   if constexpr (EPI != EPI_F32 && EPI != EPI_DEC) load_epi_cols<CC_BF16, EPI, 256>(evec, args, fg, n0);
   wait_vmcnt<0>();
-#ifdef CC_PP_STAMPS  // diagnostic build only: per-block wall-clock timeline (100 MHz counter)
-  // (CC_PP_STAMPS_EPI: [main-loop end, epilogue core end, end, hw id] instead)
-  if (threadIdx.x == 0 && args.dbg)
-    ((uint64_t*)args.dbg)[(int64_t)args.stamp_base + bid * 4 + (CC_PP_STAMPS_EPI ? 0 : 1)] = __builtin_amdgcn_s_memrealtime();
-#endif
 
-#ifdef CC_EXP_G3REG  // timing-only probe (never shipped): G3 with unswapped accumulators (4 consecutive batch rows
-  // of one latent per lane) stored straight to g_pre^T, 8 B per lane, no LDS image (no mask / l1 term / sums)
-  if (EPI == EPI_DACTS && args.out_t) {  // (the batch-major form, out_t == NULL, keeps its epilogue)
-#pragma unroll
-    for (int i = 0; i < WG::TM; ++i)
-#pragma unroll
-      for (int j = 0; j < WG::TN; ++j) {
-        const int m = m0 + wr * WG::WTM + 16 * i + 4 * (lane >> 4), n = n0 + wc * WG::WTN + 16 * j + (lane & 15);
-        const float v4[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if (m < M && n < N) *(bf16x4*)((bf16_t*)args.out_t + (int64_t)n * args.ldt + m) = pack4<CC_BF16>(v4);
-      }
-    return;
-  }
-#endif
   if constexpr (EPI == EPI_SPLIT) {  // split-K partial: accumulator fragments stored as they are (1 KB each)
     // slab tile index tm * nbn + tn (row-major over the tiles, whatever the block order)
     float* o = (float*)args.out + ((int64_t)(tm * args.nbn + tn) * 8 + wave) * 32 * 256;
@@ -527,28 +408,11 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadI
   }
 }
 
-#ifdef CC_PP_STAMPS
-// block record [start, main-loop end, end, hw id | xcc id << 32] at stamp_base + 4 * bid
-CC_DEV uint64_t pp_stamp_start() { return __builtin_amdgcn_s_memrealtime(); }
-CC_DEV void pp_stamp_end(const GemmArgs& a, int bid, uint64_t t0) {
-  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-  if (threadIdx.x == 0 && a.dbg) {
-    uint64_t* o = (uint64_t*)a.dbg + a.stamp_base + (int64_t)bid * 4;
-    if (!CC_PP_STAMPS_EPI) o[0] = t0;
-    o[2] = t1;
-    o[3] = (uint64_t)__builtin_amdgcn_s_getreg(0xF804) | ((uint64_t)__builtin_amdgcn_s_getreg(0xF814) << 32);
-  }
-}
-#endif
-
-// Persistent tile loop (CC_PP_PERSIST): grid = min(tiles, CUs) workgroups, workgroup b runs tiles b, b + grid,
+// Persistent tile loop: grid = min(tiles, CUs) workgroups, workgroup b runs tiles b, b + grid,
 // ... -- the same tile -> XCD map as one tile per workgroup (t % 8 == b % 8), without a workgroup
 // launch per tile, and the next tile's first operand DMAs fly while this tile's epilogue stores drain.
 // Between tiles every wave's LDS reads of the epilogue image must be done before any wave's DMAs
 // overwrite it: lgkmcnt(0) + s_barrier (no vmcnt wait: the stores keep draining).
-#ifndef CC_PP_PERSIST
-#define CC_PP_PERSIST 1
-#endif
 CC_DEV void pp_tile_boundary() {
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
   __builtin_amdgcn_s_barrier();
@@ -565,28 +429,11 @@ CC_DEV int pp_opaque_tid() {
 template <bool AKC, bool BKC, int EPI, bool FAST = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(16))) char smem[EPI == EPI_WGDEC ? PP_LDS_W : PP_LDS];
-#if CC_PP_PERSIST
   const int nt = args.nbm * args.nbn;
   for (int t = blockIdx.x; t < nt; t += gridDim.x) {
     pp_tile<AKC, BKC, EPI, FAST>(args, smem, t, pp_opaque_tid());
     pp_tile_boundary();
   }
-  return;
-#endif
-#ifdef CC_EXP_STAGGER  // timing-only experiment build (never shipped): half the first-round blocks start ~CC_EXP_STAGGER x 4 us
-#ifndef CC_EXP_STAGGER_XCD  // late: every other block of each XCD (0), or the odd XCDs' blocks (1)
-#define CC_EXP_STAGGER_XCD 0
-#endif
-  if ((CC_EXP_STAGGER_XCD ? (blockIdx.x & 1) : ((blockIdx.x >> 3) & 1)) && blockIdx.x < 256)
-    for (int i = 0; i < CC_EXP_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
-#ifdef CC_PP_STAMPS
-  const uint64_t t0 = pp_stamp_start();
-#endif
-  pp_tile<AKC, BKC, EPI, FAST>(args, smem, blockIdx.x);
-#ifdef CC_PP_STAMPS
-  pp_stamp_end(args, blockIdx.x, t0);
-#endif
 }
 
 // Two independent GEMMs of one layout in one launch: blocks [0, nb0) are a0's tiles, the rest
@@ -596,24 +443,12 @@ template <bool AKC, bool BKC, int EPI0, int EPI1>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_kernel(const GemmArgs a0, const GemmArgs a1) {
   __shared__ __attribute__((aligned(16))) char smem[EPI0 == EPI_WGDEC || EPI1 == EPI_WGDEC ? PP_LDS_W : PP_LDS];
   const int nb0 = a0.nbm * a0.nbn;
-#if CC_PP_PERSIST
   for (int t = blockIdx.x; t < 2 * nb0; t += gridDim.x) {
     const int tid = pp_opaque_tid();
     if (t < nb0) pp_tile<AKC, BKC, EPI0>(a0, smem, t, tid);
     else pp_tile<AKC, BKC, EPI1>(a1, smem, t - nb0, tid);
     pp_tile_boundary();
   }
-  return;
-#endif
-#ifdef CC_PP_STAMPS
-  const uint64_t t0 = pp_stamp_start();
-#endif
-  if ((int)blockIdx.x < nb0) pp_tile<AKC, BKC, EPI0>(a0, smem, blockIdx.x);
-  else pp_tile<AKC, BKC, EPI1>(a1, smem, blockIdx.x - nb0);
-#ifdef CC_PP_STAMPS
-  if ((int)blockIdx.x < nb0) pp_stamp_end(a0, blockIdx.x, t0);
-  else pp_stamp_end(a1, blockIdx.x - nb0, t0);
-#endif
 }
 
 // G2 as ONE launch: blocks [0, nb0) are the whole-wave main tiles (a0, epilogue EPI), the rest the
@@ -637,7 +472,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_main_splitk_kernel(const Gemm
   a.k_step0 = s * steps_per;
   a.k_steps = nk_total - a.k_step0 < steps_per ? nk_total - a.k_step0 : steps_per;
   a.out = (float*)t.out + s * split_stride;
-  a.stamp_base = 4 * s * t.nbm * t.nbn;
   pp_tile<AKC, BKC, EPI_SPLIT>(a, smem, tb);
 }
 
@@ -653,16 +487,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_splitk_kernel(const GemmArgs 
   // config 2, vs 80-134 us with each split pinned to one XCD: s = b % 8)
   const int s = blockIdx.x / (args.nbm * args.nbn);
   const int tb = blockIdx.x - s * args.nbm * args.nbn;
-#ifdef CC_PP_STAMPS
-  const uint64_t t0 = pp_stamp_start();
-#endif
   GemmArgs a = args;
   a.k_step0 = s * steps_per;
   a.k_steps = nk_total - a.k_step0 < steps_per ? nk_total - a.k_step0 : steps_per;
   a.out = (float*)args.out + s * split_stride;
-  a.stamp_base = 4 * s * args.nbm * args.nbn;
   pp_tile<AKC, BKC, EPI_SPLIT>(a, smem, tb);
-#ifdef CC_PP_STAMPS
-  pp_stamp_end(a, tb, t0);
-#endif
 }

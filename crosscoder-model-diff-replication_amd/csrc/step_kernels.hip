@@ -45,13 +45,6 @@ CC_DEV void tile_store_transposed(const char* lds, void* out_t, int64_t ldt, int
   }
 }
 
-#ifndef CC_PREP_RAW_NT  // the raw batch is read once per step
-#define CC_PREP_RAW_NT 0
-#endif
-#ifndef CC_LOSS_RECON_NT  // the fp32 reconstruction is read once
-#define CC_LOSS_RECON_NT 0
-#endif
-
 // ---------------------------------------------------------------------------------------
 // x_out = dtype(x_in * factor[model]);  colsum_part[rb][k] = sum over the block's rows.
 // grid: (ceil(K/512), ceil(B/64)); block 256 = 4 waves; lane -> 8 columns, wave -> 16 rows.
@@ -80,7 +73,7 @@ __global__ __launch_bounds__(256) void prep_kernel(const void* __restrict__ x_in
         float v[8][8];
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-          if (base + wave + 4 * k < B) ld8<DIN, CC_PREP_RAW_NT>(x_in, (int64_t)(base + wave + 4 * k) * K + col, v[k]);
+          if (base + wave + 4 * k < B) load8<DIN>(x_in, (int64_t)(base + wave + 4 * k) * K + col, v[k]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const int r = base + wave + 4 * k;
@@ -216,8 +209,7 @@ __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ rec
 #pragma unroll
       for (int u = 0; u < 2; ++u)
         if (ra + 4 * u < row_end) {
-          if constexpr (CC_LOSS_RECON_NT) load8f_nt(recon, (int64_t)(ra + 4 * u) * K + col, rv[u]);
-          else load8f(recon, (int64_t)(ra + 4 * u) * K + col, rv[u]);
+          load8f(recon, (int64_t)(ra + 4 * u) * K + col, rv[u]);
           load8<DT>(x, (int64_t)(ra + 4 * u) * K + col, xv[u]);
         }
     }
@@ -442,9 +434,7 @@ struct TailArgs {
   ClipArgs clip;
   ScalArgs scal;
   unsigned* counter;
-  int fence_all;
 };
-static int g_tail_fence_all = 0;  // cc_debug_set_tail_fence (A/B tooling, not part of the ABI)
 template <int DT>
 __global__ __launch_bounds__(SCAL_THREADS) void tail_kernel(const TailArgs a) {
   __shared__ float red[4][4][RED_COLS];
@@ -468,9 +458,7 @@ __global__ __launch_bounds__(SCAL_THREADS) void tail_kernel(const TailArgs a) {
   else if (role == 2) ev_phase2(a.ev, b, t, evred[grp]);
   // publish this block's partials, then count arrivals.  The barrier's workgroup-scope release
   // waits for every wave's stores to reach this XCD's L2; ONE agent-scope release (an L2
-  // write-back) then publishes them all before the arrival count.  (fence_all: every thread fences,
-  // seq_cst -- an L2 write-back + invalidate per wave; measured slower, A/B switch.)
-  if (a.fence_all) __threadfence();
+  // write-back) then publishes them all before the arrival count.
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -480,7 +468,6 @@ __global__ __launch_bounds__(SCAL_THREADS) void tail_kernel(const TailArgs a) {
   }
   __syncthreads();
   if (!last) return;
-  if (a.fence_all) __threadfence();
   if (a.finalize == 0) {
     __shared__ double cred[8][SCAL_THREADS / 64];
     __shared__ float cnorms[8];
@@ -526,15 +513,10 @@ CC_DEV void adam_elem(const AdamArgs& a, float coef, float& p, float g, float& m
   v = vj;
 }
 
-#ifndef CC_ADAM_U
-#define CC_ADAM_U 1
-#endif
-// cache policy of the bulk (encoder-half / whole-arena) Adam: 0 every access temporal, 1 g / m / v
-// non-temporal and p temporal (the updated weights stay in the Infinity Cache for the next GEMM that
-// reads them), 2 every access non-temporal
-#ifndef CC_ADAM_BULK_NT
-#define CC_ADAM_BULK_NT 1
-#endif
+// cache policy of the bulk (encoder-half / whole-arena) Adam: g / m / v non-temporal, p temporal (the
+// updated weights stay in the Infinity Cache for the next GEMM that reads them; measured faster than all
+// temporal or all non-temporal)
+constexpr int ADAM_U = 1;
 
 // Bulk of the arena: U 8-element chunks per thread, all 4*U loads issued before any math, one
 // pass over the grid (no grid-stride loop).  U = 1 measured fastest (390 us for the 151 M-element
@@ -548,7 +530,7 @@ __global__ __launch_bounds__(256) void adam_bulk_kernel(const AdamArgs a, int64_
   for (int u = 0; u < U; ++u) {
     const int64_t c = c0 + u * 256;
     if (c < nchunks) {
-      constexpr bool PN = CC_ADAM_BULK_NT == 2, SN = CC_ADAM_BULK_NT >= 1;
+      constexpr bool PN = false, SN = true;
       ld8<DT, PN>(a.p, c * 8, p[u]); ld8<DT, SN>(a.g, c * 8, g[u]); ld8<DT, SN>(a.m, c * 8, m[u]);
       ld8<DT, SN>(a.v, c * 8, v[u]);
     }
@@ -559,7 +541,7 @@ __global__ __launch_bounds__(256) void adam_bulk_kernel(const AdamArgs a, int64_
     if (c < nchunks) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) adam_elem<DT>(a, coef, p[u][j], g[u][j], m[u][j], v[u][j]);
-      constexpr bool PN = CC_ADAM_BULK_NT == 2, SN = CC_ADAM_BULK_NT >= 1;
+      constexpr bool PN = false, SN = true;
       st8<DT, PN>(a.p, c * 8, p[u]); st8<DT, SN>(a.m, c * 8, m[u]); st8<DT, SN>(a.v, c * 8, v[u]);
     }
   }
@@ -603,11 +585,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
       p[j] = pj; m[j] = mj; v[j] = vj;
     }
     if (full) {
-#if CC_ADAM_SIDE_PT  // experiment: the updated weights stored temporal (kept in the Infinity Cache)
-      store8<DT>(a.p, i, p);
-#else
       store8_nt<DT>(a.p, i, p);
-#endif
       store8_nt<DT>(a.m, i, m); store8_nt<DT>(a.v, i, v);
     } else {
       for (int j = 0; j < 8 && i + j < a.numel; ++j) {
@@ -955,11 +933,10 @@ int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const 
     CC_LAUNCH_CHECK();
     return CC_OK;
   }
-#if CC_ADAM_U > 0
   const int64_t nchunks = numel / 8;
   if (nchunks > 0) {
-    const int64_t blocks = (nchunks + 256 * CC_ADAM_U - 1) / (256 * CC_ADAM_U);
-    DISPATCH_DT(dtype, hipLaunchKernelGGL((adam_bulk_kernel<DT_, CC_ADAM_U>), dim3((unsigned)blocks), dim3(256), 0,
+    const int64_t blocks = (nchunks + 256 * ADAM_U - 1) / (256 * ADAM_U);
+    DISPATCH_DT(dtype, hipLaunchKernelGGL((adam_bulk_kernel<DT_, ADAM_U>), dim3((unsigned)blocks), dim3(256), 0,
                                           st, a, nchunks));
     CC_LAUNCH_CHECK();
   }
@@ -972,18 +949,9 @@ int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const 
     DISPATCH_DT(dtype, hipLaunchKernelGGL((adam_kernel<DT_>), dim3(1), dim3(256), 0, st, t));
     CC_LAUNCH_CHECK();
   }
-#else
-  int64_t work = (numel + 7) / 8;
-  int64_t blocks = (work + 255) / 256;
-  if (blocks > 256 * 16) blocks = 256 * 16;
-  DISPATCH_DT(dtype, hipLaunchKernelGGL((adam_kernel<DT_>), dim3((unsigned)blocks), dim3(256), 0, st, a));
-  CC_LAUNCH_CHECK();
-#endif
   return CC_OK;
 }
 
-
-void cc_debug_set_tail_fence(int all) { g_tail_fence_all = all; }
 
 static int grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,
                      const float* loss_colpart, int64_t R_dec, int64_t K, void* g_b_dec, float* sq_b_dec, int dtype,
@@ -1009,7 +977,6 @@ static int grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* 
   a.clip.sums_only = sums_only;
   a.clip.zero_mask = zero_mask;
   a.counter = counter;
-  a.fence_all = g_tail_fence_all;
   dim3 grid((unsigned)((a.red_blocks[0] + a.red_blocks[1] + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_DT(dtype, hipLaunchKernelGGL((tail_kernel<DT_>), grid, dim3(SCAL_THREADS), 0, st, a));
@@ -1058,7 +1025,6 @@ int cc_loss_tail_nb(const float* acts_colpart, int64_t R, int64_t h, float* cols
   a.finalize = 1;
   a.scal = {ev_part, nblk, l1_part, nred, l0_part, n_l0, (int)B, scalars, l1l0_out, host_out, (unsigned)seq};
   a.counter = counter;
-  a.fence_all = g_tail_fence_all;
   dim3 grid((unsigned)((nred + nblk + 3) / 4));
   hipLaunchKernelGGL((tail_kernel<CC_F32>), grid, dim3(SCAL_THREADS), 0, (hipStream_t)stream, a);
   CC_LAUNCH_CHECK();

@@ -31,6 +31,8 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* the library is built with -fvisibility=hidden: exactly the entry points declared here are exported */
+#pragma GCC visibility push(default)
 
 #define CC_BF16 1
 #define CC_F32 2
@@ -354,6 +356,8 @@ int cc_fold_scaling(void* W_enc, void* W_dec, void* b_dec, const float* scale, i
  * cosine[h] = <W_dec[h,0], W_dec[h,1]> / (norms[h,0] norms[h,1]) (optional).  fp32 outputs. */
 int cc_decoder_stats(const void* W_dec, int64_t h, int64_t n, int64_t d, int dtype, float* norms, float* relative,
                      float* cosine, void* stream);
+
+#pragma GCC visibility pop
 
 #ifdef __cplusplus
 }

@@ -37,6 +37,24 @@ def test_library_exports_every_declared_symbol():
     assert lib.cc_version() >= 100
 
 
+def _dynamic_exports(path):
+    import shutil
+    import subprocess
+    nm = shutil.which("nm") or shutil.which("llvm-nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    if not os.path.exists(nm):
+        pytest.skip("no nm")
+    out = subprocess.run([nm, "-D", "--defined-only", path], check=True, capture_output=True, text=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_library_exports_only_the_header():
+    """The product library exports exactly the C ABI of include/crosscoder_hip.h (no global-state setters, no
+    kernel handles); the test-only debug build adds only its launch-form setters."""
+    syms = set(declared_symbols())
+    assert _dynamic_exports(_lib.LIB_PATH) == syms
+    assert _dynamic_exports(_lib.DEBUG_LIB_PATH) == syms | set(_lib.DEBUG_SETTERS)
+
+
 def test_argument_validation_without_gpu():
     lib = _lib.load()
     null = ctypes.c_void_p(0)

@@ -2,7 +2,7 @@ import ctypes, sys, os, torch
 sys.path.insert(0, '/root/repo' if os.path.isdir('/root/repo') else os.getcwd())
 import crosscoder_amd
 from crosscoder_amd import _lib
-L=_lib.load()
+L=_lib.load_debug()  # (the pp_mask setter lives in the test-only debug build)
 dev=torch.device('cuda:0'); g=torch.Generator(device=dev).manual_seed(0)
 B,h=4096,16384
 st=ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)

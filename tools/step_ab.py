@@ -180,22 +180,6 @@ class G2FromWdec:
         self.tr.crosscoder._ws.norms_token = None
 
 
-class EncGrid:
-    """Variant: G1 (persistent) on `grid` workgroups, leaving CUs to the side-stream decoder Adam
-    (cc_debug_set_enc_grid)."""
-
-    def __init__(self, grid):
-        self.grid = grid
-
-    def on(self):
-        from crosscoder_amd import _lib
-        _lib.load().cc_debug_set_enc_grid(self.grid)
-
-    def off(self):
-        from crosscoder_amd import _lib
-        _lib.load().cc_debug_set_enc_grid(0)
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib")
@@ -233,9 +217,6 @@ def main():
     sp = SidePriority(tr)
     variants["side stream high priority"] = (shipped, sp.on, sp.off)
     variants["dec Adam with enc Adam + side high priority"] = (dec_adam_with_enc(), sp.on, sp.off)
-    for g in (240, 224, 208, 192, 160):
-        v = EncGrid(g)
-        variants[f"G1 grid {g}"] = (shipped, v.on, v.off)
     if args.only:
         keep = args.only.split(",")
         variants = {k: v for k, v in variants.items() if k in keep}
