@@ -61,6 +61,8 @@ struct GemmArgs {
   void* out_t;          // ping-pong bf16 epilogue: also store the tile transposed, out_t[n][m] (ld ldt)
   int64_t ldt;
   float* row_part;      // EPI_DLOSS: loss row terms [2][n * d/64][M]
+  uint32_t* mask_bits;  // ping-pong EPI_ENC (out) / EPI_DACTS FAST (in): the activation mask, 1 bit per output
+                        // in accumulator order: [tile tm*nbn + tn][thread][4] u32, bit 4(4i+j)+e of fragment (i,j)
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -704,7 +706,9 @@ static int launch_pp(GemmArgs a, hipStream_t st) {
   a.nbm = (a.M + BM - 1) / BM;
   a.nbn = (a.N + 255) / 256;
   if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
-    if (g_pp_fast && a.M % BM == 0 && a.N % 256 == 0 && (EPI == EPI_DACTS || a.flag)) {  // whole tiles, ReLU on
+    // whole tiles, ReLU on (encode: no l1 partials; d_acts: with G1's mask bits)
+    if (g_pp_fast && a.M % BM == 0 && a.N % 256 == 0 &&
+        (EPI == EPI_DACTS ? a.mask_bits != nullptr : a.flag && !a.wave_part0)) {
       hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI, true>), dim3(pp_grid(a.nbm * a.nbn)), dim3(NTHR), 0, st, a);
       CC_LAUNCH_CHECK();
       return CC_OK;
@@ -796,9 +800,11 @@ int cc_encode_fwd(const void* x, const void* W_enc, const void* b_enc, const flo
 
 // cc_encode_fwd that also stores acts transposed, acts_t [h][B] (the batch-contiguous operand of
 // the KC/KC weight-gradient GEMM, cc_wgrad_both_t).  bf16, B % 8 == 0, ping-pong path only.
+int64_t cc_mask_bits_words(int64_t B, int64_t h) { return n_blocks(B, h, 256) * NTHR * 4; }
+
 int cc_encode_fwd_t(const void* x, const void* W_enc, const void* b_enc, const float* tn, void* acts, void* acts_t,
-                    int apply_relu, float* colsum_part, float* l1_part, float* l0_part, int64_t B, int64_t K, int64_t h,
-                    int dtype, void* stream) {
+                    int apply_relu, float* colsum_part, float* l1_part, float* l0_part, uint32_t* mask_bits, int64_t B,
+                    int64_t K, int64_t h, int dtype, void* stream) {
   if (!acts || !acts_t) return CC_ERR_NULL;
   if (l1_part && !tn) return CC_ERR_NULL;
   GemmArgs a = {};
@@ -806,10 +812,11 @@ int cc_encode_fwd_t(const void* x, const void* W_enc, const void* b_enc, const f
   a.M = (int)B; a.N = (int)h; a.K = (int)K;
   a.out = acts; a.ldo = h; a.bias = b_enc; a.tn = tn; a.flag = apply_relu;
   a.col_part = colsum_part; a.wave_part0 = l1_part; a.wave_part1 = l0_part;
-  a.out_t = acts_t; a.ldt = B;
+  a.out_t = acts_t; a.ldt = B; a.mask_bits = mask_bits;
   int rc = check_gemm(a, dtype, true, true);
   if (rc) return rc;
   if (B % 8 || !al16(acts_t) || !use_pp(a.N, true, true, dtype)) return CC_ERR_SHAPE;
+  if (mask_bits && !al16(mask_bits)) return CC_ERR_ALIGN;
   return launch_pp<true, true, EPI_ENC>(a, (hipStream_t)stream);
 }
 
@@ -1143,16 +1150,17 @@ extern "C" {
 // cc_dacts_bwd storing d pre-activations TRANSPOSED only: g_pre_t[j][b] for b < B (row stride ldt
 // >= B; a batch slice passes g_pre_t + r0).  bf16, B % 8 == 0, ldt % 8 == 0, ping-pong path only.
 int cc_dacts_bwd_t(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
-                   void* g_pre_t, int64_t ldt, float* colsum_part, int64_t B, int64_t K, int64_t h, int dtype,
-                   void* stream) {
+                   const uint32_t* mask_bits, void* g_pre_t, int64_t ldt, float* colsum_part, int64_t B, int64_t K,
+                   int64_t h, int dtype, void* stream) {
   if (!g_pre_t || !acts) return CC_ERR_NULL;
   GemmArgs a = {};
   a.A = g_recon; a.lda = K; a.B = W_dec; a.ldb = K;
   a.M = (int)B; a.N = (int)h; a.K = (int)K;
   a.out = nullptr; a.ldo = h; a.mask_src = acts; a.tn = tn; a.scale0 = l1_scale;
-  a.col_part = colsum_part; a.out_t = g_pre_t; a.ldt = ldt;
+  a.col_part = colsum_part; a.out_t = g_pre_t; a.ldt = ldt; a.mask_bits = const_cast<uint32_t*>(mask_bits);
   int rc = check_gemm(a, dtype, true, true);
   if (rc) return rc;
+  if (mask_bits && !al16(mask_bits)) return CC_ERR_ALIGN;
   if (B % 8 || ldt % 8 || ldt < B || !al16(g_pre_t) || !use_pp(a.N, true, true, dtype)) return CC_ERR_SHAPE;
   return launch_pp<true, true, EPI_DACTS>(a, (hipStream_t)stream);
 }

@@ -126,6 +126,7 @@ template <int DT, int BNT>
 struct EpiCols {
   typename V4<DT>::T bias[WaveGeom<BNT>::TN];
   f32x4 tn[WaveGeom<BNT>::TN];
+  u32x4 bits;  // EPI_DACTS FAST: this thread's activation-mask bits (mask_bits)
   CC_DEV void load(const GemmArgs& args, const FragGeom<BNT>& fg, int n0, bool want_bias) {
     constexpr int ES = DT == CC_BF16 ? 2 : 4;
     const __amdgpu_buffer_rsrc_t rbias = vec_rsrc(want_bias ? args.bias : args.A, n0, args.N, ES);
@@ -138,28 +139,39 @@ struct EpiCols {
     }
   }
 };
-template <int DT, int EPI, int BNT>
-CC_DEV void load_epi_cols(EpiCols<DT, BNT>& c, const GemmArgs& args, const FragGeom<BNT>& fg, int n0) {
+// 16 B of this thread's mask bits in the [tile][thread][4] u32 layout (mask_bits)
+CC_DEV uint32_t* mask_bits_at(const GemmArgs& args, int tm, int tn, int tid) {
+  return args.mask_bits + ((int64_t)(tm * args.nbn + tn) * 512 + tid) * 4;
+}
+template <int DT, int EPI, int BNT, bool FAST = false>
+CC_DEV void load_epi_cols(EpiCols<DT, BNT>& c, const GemmArgs& args, const FragGeom<BNT>& fg, int n0, int tm = 0,
+                          int tn = 0, int tid = 0) {
   if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) c.load(args, fg, n0, EPI == EPI_ENC && args.bias);
+  if constexpr (EPI == EPI_DACTS && FAST) c.bits = *(const u32x4*)mask_bits_at(args, tm, tn, tid);
   if constexpr (EPI == EPI_DLOSS) c.load(args, fg, n0, true);  // b_dec, x_mean
 }
 
 // EPI_ENC / EPI_DACTS element-wise part (see epilogue_core).  FAST (bf16): every fragment in range, ReLU on.
+// Activation mask (EPI_DACTS): FAST reads G1's mask bits (cols.bits, no mask tile), the general form the
+// acts tile through io.in4.  EPI_ENC writes the bits (args.mask_bits, ping-pong path) for the d_acts GEMM
+// of the same tile grid and wave / lane map: bit 4(4i + j) + e <-> acc[i][j][e].
 template <int DT, int EPI, int BNT, bool FAST, class IO>
 CC_DEV void enc_dacts_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN],
                            const FragGeom<BNT>& fg, const IO& io, int tm, int n0, int wr, int lane, int wave_slot,
                            const EpiCols<DT, BNT>& cols) {
 #pragma clang fp contract(off)  // (acc + tn * l1_scale: two roundings in every variant; the l1 sum fuses)
+  static_assert(!(EPI == EPI_DACTS && FAST) || WaveGeom<BNT>::TM * WaveGeom<BNT>::TN == 32, "mask bits: 32 fragments");
+  uint32_t bw[4] = {0u, 0u, 0u, 0u};  // EPI_ENC: the mask bits being formed
   using E = Elem<DT>;
   using WG = WaveGeom<BNT>;
   const int N = args.N;
   constexpr int JB = EPB<DT, BNT>::JB_M;
-  float s_l1 = 0.f, s_l0 = 0.f;
-  int l0i = 0;  // FAST: this lane's count of positive outputs
+  float s_l1 = 0.f;
+  int l0i = 0;  // this lane's count of positive outputs
   typename V4<DT>::T mraw[EPI == EPI_DACTS ? WG::TM : 1][JB];
 #pragma unroll
   for (int j = 0; j < WG::TN; ++j) {
-    if constexpr (EPI == EPI_DACTS) {
+    if constexpr (EPI == EPI_DACTS && !FAST) {
       if (j % JB == 0) {  // the mask vectors of JB column groups, all in flight together
 #pragma unroll
         for (int jj = 0; jj < JB; ++jj)
@@ -187,6 +199,12 @@ CC_DEV void enc_dacts_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT
         float t = acc[i][j][e] + add[e];
         if constexpr (EPI == EPI_ENC) {
           if (FAST || args.flag) t = fmaxf(t, 0.f);
+        } else if constexpr (FAST) {  // bit 4(4i + j) + e = word i / 2, bit 16 (i % 2) + 4j + e
+          // (the bit sign-extended to an all-ones / zero mask, opaque so that it stays two VALU ops instead of
+          // a compare + select per element)
+          int m;
+          asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(cols.bits[i >> 1]), "i"(16 * (i & 1) + 4 * j + e));
+          t = __int_as_float(__float_as_int(t) & m);
         } else {
           t = V4<DT>::get(mraw[i][j % JB], e) > 0.f ? t : 0.f;
         }
@@ -200,15 +218,23 @@ CC_DEV void enc_dacts_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT
       } else {
         io.out4(i, j, v);
       }
+      uint32_t nib = 0u;  // EPI_ENC: this fragment's 4 mask bits
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         csum[e] += v[e];
         if constexpr (EPI == EPI_ENC) {
-          s_l1 = __builtin_fmaf(v[e], tnc[e], s_l1);
-          if constexpr (FAST) l0i += v[e] > 0.f;
-          else s_l0 += v[e] > 0.f ? 1.f : 0.f;
+          if constexpr (!FAST) s_l1 = __builtin_fmaf(v[e], tnc[e], s_l1);  // (FAST: no l1 partials, host)
+          // v > 0 as an integer 0 / 1: med3(bits of v, 0, 1), opaque so that it is not turned back into
+          // compares, whose 128 lane masks would sit in SGPRs until their later uses and spill
+          int pos;
+          if constexpr (FAST) asm("v_med3_i32 %0, %1, 0, 1" : "=v"(pos) : "v"(__float_as_int(v[e])));
+          else pos = v[e] > 0.f;  // (the general form: its range selects need the compares anyway)
+          l0i += pos;
+          nib |= (uint32_t)pos << e;
         }
       }
+      // bit 4(4i + j) + e = word i / 2, bit 16 (i % 2) + 4j + e
+      if constexpr (EPI == EPI_ENC) bw[i >> 1] |= nib << (16 * (i & 1) + 4 * j);
     }
     if (args.col_part) {  // reduce over the 16 lanes (rows) that share these 4 columns
 #pragma unroll
@@ -218,13 +244,17 @@ CC_DEV void enc_dacts_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT
     }
   }
   if constexpr (EPI == EPI_ENC) {
+    if constexpr (WG::TM * WG::TN == 32) {
+      if (args.mask_bits)
+        *(u32x4*)mask_bits_at(args, tm, n0 / BNT, wave_slot % 8 * 64 + lane) = u32x4{bw[0], bw[1], bw[2], bw[3]};
+    }
     if (args.wave_part0) {
       float t = wave_sum(s_l1);
       if (lane == 0) args.wave_part0[wave_slot] = t;
     }
     if (args.wave_part1) {
       // (integer-valued floats below 2^24: the per-lane counts sum exactly either way)
-      float t = wave_sum(FAST ? (float)l0i : s_l0);
+      float t = wave_sum((float)l0i);
       if (lane == 0) args.wave_part1[wave_slot] = t;
     }
   }
@@ -323,6 +353,7 @@ CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
     constexpr int JB = EPB<DT, BNT>::JB_W;
     const bool l1term = EPI == EPI_WGDEC && args.scale0 != 0.f;
     float sq = 0.f;
+    float sqe[4] = {0.f, 0.f, 0.f, 0.f};  // (bf16: one partial per element position, summed at the end)
     typename V4<DT>::T wraw[EPI == EPI_WGDEC ? WG::TM : 1][JB];
 #pragma unroll
     for (int j = 0; j < WG::TN; ++j) {
@@ -345,14 +376,26 @@ CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
             for (int e = 0; e < 4; ++e) v[e] += cw[i][j] * V4<DT>::get(wraw[i][j % JB], e);
           }
         }
+        // out-of-range fragments are exactly 0 (zero-filled operands and inputs): no range selects
+        if constexpr (DT == CC_BF16) {
+          const bf16x4 p = pack4<CC_BF16>(v);  // the bf16 rounding, once (the stored bits)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = E::round(v[e]);
-          sq += v[e] * v[e];  // out-of-range fragments are exactly 0 (zero-filled operands and inputs)
+          for (int e = 0; e < 4; ++e) {
+            const float r = V4<CC_BF16>::get(p, e);
+            sqe[e] = __builtin_fmaf(r, r, sqe[e]);
+          }
+          io.out4p(i, j, p);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = E::round(v[e]);
+            sq += v[e] * v[e];
+          }
+          io.out4(i, j, v);
         }
-        io.out4(i, j, v);
       }
     }
+    if constexpr (DT == CC_BF16) sq = (sqe[0] + sqe[1]) + (sqe[2] + sqe[3]);
     if (args.wave_part0) {
       float t = wave_sum(sq);
       if (lane == 0) args.wave_part0[wave_slot] = t;

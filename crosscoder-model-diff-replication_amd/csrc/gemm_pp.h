@@ -152,7 +152,9 @@ CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char
                             bool input_staged, int tm, int m0, int n0, int wr, int wc, int lane, int wave,
                             int wave_slot, const FragGeom<256>& fg, const EpiCols<CC_BF16, 256>& ecols) {
   const int rows = args.M - m0, cols = args.N - n0, ldo = (int)args.ldo;
-  const void* in = EPI == EPI_DACTS || EPI == EPI_DLOSS
+  // the epilogue's input tile: d_acts' activation mask (the general form; FAST reads G1's mask bits instead),
+  // the fused loss's x tile, dW_dec's W_dec tile (prefetched by the K loop)
+  const void* in = (EPI == EPI_DACTS && !FAST) || EPI == EPI_DLOSS
                        ? args.mask_src
                        : (EPI == EPI_WGDEC && args.scale0 != 0.f ? args.w_src : nullptr);
   float cw[8][4];  // dW_dec L1-term factors (EPI_WGDEC only)
@@ -390,7 +392,7 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadI
   // the epilogue's column vectors fly while the last (zero-fill) DMAs drain
   const FragGeom<256> fg(args, m0, n0, wr, wc, lane);
   EpiCols<CC_BF16, 256> evec;
-  if constexpr (EPI != EPI_F32 && EPI != EPI_DEC) load_epi_cols<CC_BF16, EPI, 256>(evec, args, fg, n0);
+  if constexpr (EPI != EPI_F32 && EPI != EPI_DEC) load_epi_cols<CC_BF16, EPI, 256, FAST>(evec, args, fg, n0, tm, tn, tid);
   wait_vmcnt<0>();
 
   if constexpr (EPI == EPI_SPLIT) {  // split-K partial: accumulator fragments stored as they are (1 KB each)

@@ -140,6 +140,9 @@ class StepWorkspace:
         npart = ops.dec_norms_part_floats(h, n, d) if self.tr else 0
         self.norm_part = E(npart) if npart else None  # fused W_dec^T + norms pass (d % 64 == 0)
         self.acts_t = E(h, B, dt=dtype) if self.tr else None
+        # G1's activation mask as bits in the GEMM accumulator order: G3 reads 16 B per thread and tile instead
+        # of the 128 KB acts tile (1/16 of the bytes, no LDS staging)
+        self.mask_bits = E(ops.mask_bits_words(B, h), dt=torch.int32) if self.tr else None
         # G1's activation column-sum / l0 partial slabs, double-buffered: the loss tail that reads a
         # step's slabs runs on the side stream, which nothing orders before the NEXT step's G1 on torch's
         # stream; alternating slots orders every rewrite after that tail (the step after next waits for
@@ -257,7 +260,7 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     with _span("G1_encode"):
         if ws.tr:
             ops.encode_fwd_t(ws.x, P.W_enc_hk, P.b_enc, ws.acts, ws.acts_t, True, colsum_part=ws.acts_colpart,
-                             l0_part=ws.l0_part)
+                             l0_part=ws.l0_part, mask_bits=ws.mask_bits)
         else:
             ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, colsum_part=ws.acts_colpart,
                            l0_part=ws.l0_part)
@@ -375,7 +378,7 @@ def dacts_rows(ws, P, l1_coeff, r0, r1, l1_grad_weight=1.0):
     with _span("G3_dacts"):
         if ws.tr:
             ops.dacts_bwd_t(ws.g_recon[r0:r1], P.W_dec_hk, ws.acts[r0:r1], ws.tn, l1_scale, ws.g_pre_t[:, r0:r1],
-                            colsum_part=ws.gpre_colpart[c0:c1])
+                            colsum_part=ws.gpre_colpart[c0:c1], mask_bits=ops.mask_bits_rows(ws.mask_bits, ws.h, r0, r1))
         else:
             ops.dacts_bwd(ws.g_recon[r0:r1], P.W_dec_hk, ws.acts[r0:r1], ws.tn, l1_scale, ws.g_pre[r0:r1],
                           colsum_part=ws.gpre_colpart[c0:c1])

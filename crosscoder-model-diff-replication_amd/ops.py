@@ -138,14 +138,21 @@ def encode_fwd(x, W_enc_hk, b_enc, acts, apply_relu=True, tn=None, colsum_part=N
     return acts
 
 
+def mask_bits_words(B, h):
+    return int(lib().cc_mask_bits_words(B, h))
+
+
 def encode_fwd_t(x, W_enc_hk, b_enc, acts, acts_t, apply_relu=True, tn=None, colsum_part=None, l1_part=None,
-                 l0_part=None):
-    """encode_fwd that also stores acts_t [h][B] = acts^T (bf16, B % 8 == 0)."""
+                 l0_part=None, mask_bits=None):
+    """encode_fwd that also stores acts_t [h][B] = acts^T (bf16, B % 8 == 0) and, optionally, the activation
+    mask bits (int32 [mask_bits_words(B, h)]) that dacts_bwd_t reads instead of acts."""
     B, K = x.shape
     h = W_enc_hk.shape[0]
+    if mask_bits is not None and mask_bits.numel() < mask_bits_words(B, h):
+        raise ValueError("mask_bits too small")
     check(lib().cc_encode_fwd_t(_ptr(x), _ptr(W_enc_hk), _ptr(b_enc), _ptr(tn), _ptr(acts), _ptr(acts_t),
-                                int(apply_relu), _ptr(colsum_part), _ptr(l1_part), _ptr(l0_part), B, K, h,
-                                dtype_code(x.dtype), _stream(x)))
+                                int(apply_relu), _ptr(colsum_part), _ptr(l1_part), _ptr(l0_part), _ptr(mask_bits), B,
+                                K, h, dtype_code(x.dtype), _stream(x)))
     return acts
 
 
@@ -276,16 +283,26 @@ def dacts_bwd(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre, colsum_part=None):
                              _ptr(colsum_part), B, K, h, dtype_code(g_recon.dtype), _stream(g_recon)))
 
 
-def dacts_bwd_t(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre_t, colsum_part=None):
+def dacts_bwd_t(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre_t, colsum_part=None, mask_bits=None):
     """dacts_bwd storing g_pre transposed only: g_pre_t [h][>= B] view (column slice allowed, row stride
-    g_pre_t.stride(0))."""
+    g_pre_t.stride(0)).  mask_bits: encode_fwd_t's bits of these rows (see mask_bits_rows)."""
     B, K = g_recon.shape
     h = W_dec_hk.shape[0]
     if g_pre_t.shape[0] != h or g_pre_t.shape[1] != B or g_pre_t.stride(1) != 1:
         raise ValueError("g_pre_t must be an [h, B] view with unit column stride")
-    check(lib().cc_dacts_bwd_t(_ptr(g_recon), _ptr(W_dec_hk), _ptr(acts), _ptr(tn), l1_scale, _ptr(g_pre_t),
-                               g_pre_t.stride(0), _ptr(colsum_part), B, K, h, dtype_code(g_recon.dtype),
-                               _stream(g_recon)))
+    if mask_bits is not None and mask_bits.numel() < mask_bits_words(B, h):
+        raise ValueError("mask_bits too small")
+    check(lib().cc_dacts_bwd_t(_ptr(g_recon), _ptr(W_dec_hk), _ptr(acts), _ptr(tn), l1_scale, _ptr(mask_bits),
+                               _ptr(g_pre_t), g_pre_t.stride(0), _ptr(colsum_part), B, K, h,
+                               dtype_code(g_recon.dtype), _stream(g_recon)))
+
+
+def mask_bits_rows(mask_bits, h, r0, r1):
+    """The mask bits of batch rows [r0, r1) (r0 % 256 == 0) of encode_fwd_t's [B][h] bits."""
+    if r0 % 256:
+        raise ValueError("mask bits slices start on a 256-row tile")
+    w = mask_bits_words(256, h)
+    return mask_bits[(r0 // 256) * w:]
 
 
 def transpose(src, out=None):

@@ -109,10 +109,16 @@ int cc_encode_fwd(const void* x, const void* W_enc, const void* b_enc, const flo
 int cc_transposed_ok(int64_t B, int64_t K, int64_t h, int dtype);
 
 /* cc_encode_fwd that also stores acts transposed, acts_t [h][B] (the batch-contiguous operand of
- * cc_wgrad_both_t).  bf16 with B, K, h % 8 == 0 (else CC_ERR_SHAPE). */
+ * cc_wgrad_both_t).  bf16 with B, K, h % 8 == 0 (else CC_ERR_SHAPE).
+ * mask_bits (optional, cc_mask_bits_words(B, h) u32): the activation mask (acts > 0) as 1 bit per element in
+ * the GEMM's accumulator order, which cc_dacts_bwd_t reads instead of the acts tile (autograd of the ReLU,
+ * crosscoder.py:77). */
 int cc_encode_fwd_t(const void* x, const void* W_enc, const void* b_enc, const float* tn, void* acts, void* acts_t,
-                    int apply_relu, float* colsum_part, float* l1_part, float* l0_part, int64_t B, int64_t K,
-                    int64_t h, int dtype, void* stream);
+                    int apply_relu, float* colsum_part, float* l1_part, float* l0_part, uint32_t* mask_bits,
+                    int64_t B, int64_t K, int64_t h, int dtype, void* stream);
+
+/* u32 words of cc_encode_fwd_t's mask_bits for a [B][h] activation (256 x 256 tiles x 512 threads x 4). */
+int64_t cc_mask_bits_words(int64_t B, int64_t h);
 
 /* CrossCoder.decode (crosscoder.py:82-89): recon = acts[B,h] . W_dec[h][K] (+ b_dec).
  * recon_f32 (optional): fp32 [B][K]; b_dec NULL -> partial sum without bias (latent-sharded use).
@@ -216,10 +222,13 @@ int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const
                  void* g_pre, float* colsum_part, int64_t B, int64_t K, int64_t h, int dtype, void* stream);
 
 /* cc_dacts_bwd writing g_pre TRANSPOSED only: g_pre_t[j][b], row stride ldt >= B (a batch slice
- * [r0, r1) passes g_pre_t + r0 and B = r1 - r0).  bf16 with B, K, h, ldt % 8 == 0. */
+ * [r0, r1) passes g_pre_t + r0 and B = r1 - r0).  bf16 with B, K, h, ldt % 8 == 0.
+ * mask_bits (optional): cc_encode_fwd_t's mask bits of these rows (a slice starting at row r0, r0 % 256 == 0,
+ * passes mask_bits + (r0 / 256) * cc_mask_bits_words(256, h)); used instead of reading the acts tile when
+ * the shape takes the whole-tile form (B, h % 256 == 0), same bits. */
 int cc_dacts_bwd_t(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
-                   void* g_pre_t, int64_t ldt, float* colsum_part, int64_t B, int64_t K, int64_t h, int dtype,
-                   void* stream);
+                   const uint32_t* mask_bits, void* g_pre_t, int64_t ldt, float* colsum_part, int64_t B, int64_t K,
+                   int64_t h, int dtype, void* stream);
 
 /* W_dec.grad [h][K] = acts^T . g_recon + l1_scale * sum_b(acts[:,h]) * W_dec[h,m,:]/||W_dec[h,m,:]||
  * (norm backward is 0 where the norm is 0; inv_norms from cc_dec_norms).

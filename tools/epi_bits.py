@@ -42,11 +42,13 @@ def main():
         colp = torch.zeros(1 << 20, device=dev)
         l1p = torch.zeros(1 << 16, device=dev)
         l0p = torch.zeros(1 << 16, device=dev)
-        assert L.cc_encode_fwd_t(P(x), P(W), P(b_enc), P(tn), P(acts), P(actsT), 1, P(colp), P(l1p), P(l0p), B, K, h, 1,
-                                 st) == 0
+        mbits = torch.zeros(B * h // 32 + 4096, device=dev, dtype=torch.int32)
+        assert L.cc_encode_fwd_t(P(x), P(W), P(b_enc), P(tn), P(acts), P(actsT), 1, P(colp), P(l1p), P(l0p), P(mbits),
+                                 B, K, h, 1, st) == 0
         gpT = torch.empty(h, B, device=dev, dtype=bf)
         colp3 = torch.zeros(1 << 20, device=dev)
-        assert L.cc_dacts_bwd_t(P(g_recon), P(W), P(acts), P(tn), 1e-4, P(gpT), B, P(colp3), B, K, h, 1, st) == 0
+        assert L.cc_dacts_bwd_t(P(g_recon), P(W), P(acts), P(tn), 1e-4, P(mbits), P(gpT), B, P(colp3), B, K, h, 1,
+                                st) == 0
         norms = torch.rand(h, n, device=dev, generator=torch.Generator(device=dev).manual_seed(1)) + 0.5
         colsum = torch.rand(h, device=dev, generator=torch.Generator(device=dev).manual_seed(2))
         gW, gW2 = torch.empty(h, K, device=dev, dtype=bf), torch.empty(h, K, device=dev, dtype=bf)

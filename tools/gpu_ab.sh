@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU-box session for a change under test: GPU tests, a same-box step A/B of exp_head/ (a build of the last
+# commit, tools/snapshot_head.sh) vs this tree, and the GEMM timers.  Each GPU step has its own limit; the
+# script stops at the first fault / abort / timeout (an ordinary test failure, rc 1, does not stop it).
+#   tools/gpu_ab.sh OUT [steps...]   steps: test ab gemm gemmdbg
+OUT=${1:-gpurun_out/ab}
+shift
+STEPS=${*:-test ab}
+mkdir -p "$OUT"
+export TMPDIR=/tmp PYTHONDONTWRITEBYTECODE=1
+run() {
+  local name=$1 lim=$2
+  shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(date +%T))"; tail -3 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping: $name ended with $rc"; exit $rc; fi
+  return 0
+}
+for s in $STEPS; do
+  case $s in
+    test) run pytest_gpu 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ;;
+    ab) run step_ab 600 bash tools/ab_trees.sh exp_head . 4 "$OUT/trees" ;;
+    gemm) run gemm 300 python tools/gemm_bench.py crosscoder-model-diff-replication_amd/libcrosscoder_hip.so ;;
+    gemmdbg) run gemmdbg 300 python tools/gemm_bench.py crosscoder-model-diff-replication_amd/libcrosscoder_hip_dbg.so@5 \
+               crosscoder-model-diff-replication_amd/libcrosscoder_hip_dbg.so@7 ;;
+    bench) run bench 300 python bench.py ;;
+  esac
+done
+echo done
