@@ -258,68 +258,8 @@ __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ rec
   }
 }
 
-// Per-row explained variances (crosscoder.py:110-121) + per-block partial sums of the row terms.
-// grid ceil(B/256), block 256. part_out[blk][4] = {sum l2_row, sum ev, sum ev_a, sum ev_b}.
-struct EvSeg {
-  const float* row_part;
-  int B, n, ncb;
-  float* ev;
-  float* ev_a;
-  float* ev_b;
-  float* part_out;
-};
-CC_DEV void ev_phase1(const EvSeg& a, int blk, int t, float (*red)[4]) {
-  const int r = blk * 256 + t;
-  float v[4] = {0, 0, 0, 0};
-  if (r < a.B) {
-    const int B = a.B, n = a.n, ncb = a.ncb;
-    const int64_t plane = (int64_t)n * ncb * B;
-    const float eps = 1e-8f;
-    float l2 = 0.f, tv = 0.f, l2m[2] = {0, 0}, tvm[2] = {0, 0};
-    for (int m = 0; m < n; ++m) {
-      float s = 0.f, u = 0.f;
-      // 8 column blocks' loads in flight per trip (clamped index, no branch around a load), then the
-      // in-order adds: the sequential sum's bits with one memory latency per 8 blocks
-      for (int cb0 = 0; cb0 < ncb; cb0 += 8) {
-        float vs[8], vu[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int cb = cb0 + q < ncb ? cb0 + q : ncb - 1;
-          vs[q] = a.row_part[(int64_t)(m * ncb + cb) * B + r];
-          vu[q] = a.row_part[plane + (int64_t)(m * ncb + cb) * B + r];
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          if (cb0 + q < ncb) {
-            s += vs[q];
-            u += vu[q];
-          }
-        }
-      }
-      l2 += s;
-      tv += u;
-      if (m < 2) { l2m[m] = s; tvm[m] = u; }
-    }
-    float e = 1.f - l2 / (tv + eps);
-    float ea = 1.f - l2m[0] / (tvm[0] + eps);
-    float eb = n > 1 ? 1.f - l2m[1] / (tvm[1] + eps) : 0.f;
-    if (a.ev) a.ev[r] = e;
-    if (a.ev_a) a.ev_a[r] = ea;
-    if (a.ev_b) a.ev_b[r] = eb;
-    v[0] = l2; v[1] = e; v[2] = ea; v[3] = eb;
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float s = wave_sum(v[q]);
-    if ((t & 63) == 0) red[t >> 6][q] = s;
-  }
-}
-CC_DEV void ev_phase2(const EvSeg& a, int blk, int t, float (*red)[4]) {
-  if (t < 4) {
-    int q = t;
-    a.part_out[blk * 4 + q] = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
-  }
-}
+#include "loss_tail.h"
+
 __global__ __launch_bounds__(256) void ev_kernel(const EvSeg a) {
   __shared__ float red[4][4];
   ev_phase1(a, blockIdx.x, threadIdx.x, red);
@@ -327,87 +267,10 @@ __global__ __launch_bounds__(256) void ev_kernel(const EvSeg a) {
   ev_phase2(a, blockIdx.x, threadIdx.x, red);
 }
 
-// Single block: scalars = {l2, l1, l0, mean ev, mean ev_a, mean ev_b}.
-constexpr int SCAL_THREADS = 1024;
-struct ScalArgs {
-  const float* ev_part;
-  int nblk;
-  const float* l1_part;
-  int64_t n_l1;
-  const float* l0_part;
-  int64_t n_wave;
-  int B;
-  float* scalars;
-  float* l1l0_out;
-  float* host_out;
-  unsigned seq;
-};
-// 1024 threads (SCAL_THREADS), one block
-CC_DEV void loss_scalars_body(const ScalArgs& sa) {
-  const float* __restrict__ ev_part = sa.ev_part;
-  const int nblk = sa.nblk;
-  const float* __restrict__ l1_part = sa.l1_part;
-  const int64_t n_l1 = sa.n_l1;
-  const float* __restrict__ l0_part = sa.l0_part;
-  const int64_t n_wave = sa.n_wave;
-  const int B = sa.B;
-  float* __restrict__ scalars = sa.scalars;
-  float* __restrict__ l1l0_out = sa.l1l0_out;
-  float* __restrict__ host_out = sa.host_out;
-  const unsigned seq = sa.seq;
-  constexpr int NW = SCAL_THREADS / 64;
-  __shared__ double red[NW][6];
-  double acc[6] = {0, 0, 0, 0, 0, 0};
-  for (int i = threadIdx.x; i < nblk; i += SCAL_THREADS) {
-    acc[0] += ev_part[i * 4 + 0];
-    acc[3] += ev_part[i * 4 + 1];
-    acc[4] += ev_part[i * 4 + 2];
-    acc[5] += ev_part[i * 4 + 3];
-  }
-  // 4 independent loads in flight per trip (clamped index, no branch around a load)
-  if (l0_part) {
-    for (int64_t i = threadIdx.x; i < n_wave; i += 4 * SCAL_THREADS) {
-      float b[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t j = i + u * SCAL_THREADS;
-        b[u] = j < n_wave ? l0_part[j < n_wave ? j : 0] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc[2] += b[u];
-    }
-  }
-  if (l1_part)
-    for (int64_t i = threadIdx.x; i < n_l1; i += SCAL_THREADS) acc[1] += l1_part[i];
-#pragma unroll
-  for (int q = 0; q < 6; ++q) {
-    double s = wave_sum_d(acc[q]);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = s;
-  }
-  __syncthreads();
-  if (threadIdx.x < 6) {
-    int q = threadIdx.x;
-    double s = 0.0;
-    for (int w = 0; w < NW; ++w) s += red[w][q];
-    scalars[q] = (float)(s / (double)B);
-    if (l1l0_out && (q == 1 || q == 2)) l1l0_out[q - 1] = (float)(s / (double)B);
-    if (host_out) host_out[q] = (float)(s / (double)B);
-  }
-  if (threadIdx.x == 6 || threadIdx.x == 7) {
-    scalars[threadIdx.x] = 0.f;
-    if (host_out) host_out[threadIdx.x] = 0.f;
-  }
-  if (host_out) {
-    // mapped pinned host memory: the 8 values reach the host before the sequence word the host
-    // polls (no copy kernel, no event on the stream)
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_store((unsigned*)(host_out + 8), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+__global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const ScalArgs a) {
+  __shared__ double red[SCAL_THREADS / 64][6];
+  loss_scalars_body<SCAL_THREADS>(a, red);
 }
-
-__global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const ScalArgs a) { loss_scalars_body(a); }
 
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(SCAL_THREADS) void clip_kernel(const ClipArgs a) {
@@ -473,7 +336,10 @@ __global__ __launch_bounds__(SCAL_THREADS) void tail_kernel(const TailArgs a) {
     __shared__ float cnorms[8];
     clip_body<SCAL_THREADS>(a.clip, cred, cnorms);
   }
-  else loss_scalars_body(a.scal);
+  else {
+    __shared__ double sred[SCAL_THREADS / 64][6];
+    loss_scalars_body<SCAL_THREADS>(a.scal, sred);
+  }
   if (threadIdx.x == 0) atomicExch(a.counter, 0u);
 }
 

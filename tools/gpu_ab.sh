@@ -26,6 +26,13 @@ for s in $STEPS; do
     gemmdbg) run gemmdbg 300 python tools/gemm_bench.py crosscoder-model-diff-replication_amd/libcrosscoder_hip_dbg.so@5 \
                crosscoder-model-diff-replication_amd/libcrosscoder_hip_dbg.so@7 ;;
     bench) run bench 300 python bench.py ;;
+    probe) run probe 400 python tools/gemm_bench.py crosscoder-model-diff-replication_amd/libcrosscoder_hip.so \
+             $(ls crosscoder-model-diff-replication_amd/exp/*.so) ;;
+    prof) run prof_new 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof_new" -o run -- \
+            python bench.py --no-cpu-baseline --steps 20
+          run prof_old 300 bash -c "cd exp_head && rocprofv3 --kernel-trace --output-format csv -d ../$OUT/prof_old -o run -- python bench.py --no-cpu-baseline --steps 20"
+          for t in new old; do f=$(find "$OUT/prof_$t" -name '*kernel_trace.csv' | head -1); \
+            [ -n "$f" ] && python tools/step_timeline.py "$f" 12 > "$OUT/timeline_$t.txt"; done ;;
   esac
 done
 echo done
