@@ -311,7 +311,7 @@ def main():
     es = 2  # bf16
     alg = {"G1_encode": (B * K + h_local * K + 2 * B * h_local) * es,
            "G2_decode": (B * h_local + h_local * K + 3 * B * K) * es,  # + x in, g_recon / g_recon^T out (fused loss)
-           "G3_dacts": (B * K + h_local * K + 2 * B * h_local) * es,
+           "G3_dacts": (B * K + h_local * K + B * h_local) * es + B * h_local // 8,  # (+ G1's mask bits, g_pre^T out)
            "G4G5_wgrad": (2 * B * h_local + 2 * B * K + 3 * h_local * K) * es}
     dom_alg_bytes = alg.get(dom)
     name = f"{n}x{d}->{h_total}"

@@ -81,8 +81,6 @@ SIGNATURES = {
     "cc_encode_fwd_t": (_i, [_p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_mask_bits_words": (_i64, [_i64, _i64]),
     "cc_dacts_bwd_t": (_i, [_p, _p, _p, _p, _f, _p, _p, _i64, _p, _i64, _i64, _i64, _i, _p]),
-    "cc_dacts_bwd_loss_t": (_i, [_p, _p, _p, _p, _f, _p, _p, _i64, _p, _p, _i64, _p, _p, _i64, _p, _i64, _p, _p, _p,
-                                 _p, _p, _p, ctypes.c_uint32, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_transpose_b16": (_i, [_p, _i64, _i64, _i64, _p, _i64, _p]),
     "cc_dec_norms_part_floats": (_i64, [_i64, _i64, _i64]),
     "cc_transpose_dec_norms": (_i, [_p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p]),

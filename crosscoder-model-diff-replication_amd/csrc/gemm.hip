@@ -545,72 +545,6 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 
 #include "gemm_pp.h"
 #include "grad_tail.h"
-#include "loss_tail.h"
-
-// ---- G3 with the loss tail in the same launch (the single-GPU step's forward end).
-// What the stand-alone loss tail (cc_loss_tail_nb) runs after the fused G2 + loss, here in front of G3's
-// persistent tile loop, so the step needs no side stream, no event and no copy for its loss scalars:
-//   (1) 256-thread group g of workgroup b runs tail blocks 2b + g, 2b + g + 2 * grid, ...: the l1 dot partials
-//       of the activation column sums against the decoder norms (reduce_rows with dot_w) and the per-row EVs
-//       + their partial sums (the bits cc_loss_tail writes);
-//   (2) the workgroups count their arrival; the last one (device-scope counter, reset by it) runs the loss
-//       scalar finaliser, which also writes them to mapped host memory with a sequence word the host polls;
-//   (3) the tile loop of gemm_pp_kernel (G3 does not read anything the tail writes).
-struct LossTail {
-  RedSeg red;
-  int red_blocks;
-  EvSeg ev;
-  int ev_blocks;
-  ScalArgs scal;
-  unsigned* counter;
-};
-
-template <bool AKC, bool BKC, int EPI, bool FAST>
-__global__ __launch_bounds__(NTHR, 1) void gemm_pp_losstail_kernel(const GemmArgs args, const LossTail lt) {
-  __shared__ __attribute__((aligned(16))) char smem[PP_LDS];
-  {
-    const int grp = threadIdx.x >> 8, t = threadIdx.x & 255;
-    float(*red)[RED_COLS] = (float(*)[RED_COLS])(smem + grp * 4 * RED_COLS * sizeof(float));
-    float(*evred)[4] = (float(*)[4])(smem + 2 * 4 * RED_COLS * sizeof(float) + grp * 16 * sizeof(float));
-    const int nb = lt.red_blocks + lt.ev_blocks;
-    for (int base = 2 * (int)blockIdx.x; base < nb; base += 2 * (int)gridDim.x) {  // uniform per workgroup
-      const int b = base + grp;
-      const bool isred = b < lt.red_blocks;
-      if (b < nb) {
-        if (isred) reduce_rows_phase1(lt.red, b, t, red);
-        else ev_phase1(lt.ev, b - lt.red_blocks, t, evred);
-      }
-      __syncthreads();
-      if (b < nb) {
-        if (isred) reduce_rows_phase2<CC_F32>(lt.red, b, t, red);
-        else ev_phase2(lt.ev, b - lt.red_blocks, t, evred);
-      }
-      __syncthreads();
-    }
-    // publish: this workgroup's stores drained, the barrier joins the waves, ONE agent-scope release writes this
-    // XCD's L2 back before the arrival count
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    int* last = (int*)(smem + 4096);
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      const bool is_last = atomicAdd(lt.counter, 1u) == gridDim.x - 1;
-      if (is_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // drop stale lines before the reads
-      *last = is_last;
-    }
-    __syncthreads();
-    if (*last) {
-      loss_scalars_body<NTHR>(lt.scal, (double(*)[6])(smem + 8192));
-      if (threadIdx.x == 0) atomicExch(lt.counter, 0u);
-    }
-    __syncthreads();  // (the tiles' DMAs reuse the LDS)
-  }
-  const int nt = args.nbm * args.nbn;
-  for (int t = blockIdx.x; t < nt; t += gridDim.x) {
-    pp_tile<AKC, BKC, EPI, FAST>(args, smem, t, pp_opaque_tid());
-    pp_tile_boundary();
-  }
-}
 
 // ---- G4 + G5 with the gradient tail in the same launch (the single-GPU step's backward end).
 // What the stand-alone tail kernel (cc_grad_tail) runs after the weight-gradient GEMMs, here inside
@@ -1215,11 +1149,11 @@ int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const
 extern "C" {
 // cc_dacts_bwd storing d pre-activations TRANSPOSED only: g_pre_t[j][b] for b < B (row stride ldt
 // >= B; a batch slice passes g_pre_t + r0).  bf16, B % 8 == 0, ldt % 8 == 0, ping-pong path only.
-static int dacts_t_args(GemmArgs& a, const void* g_recon, const void* W_dec, const void* acts, const float* tn,
-                        float l1_scale, const uint32_t* mask_bits, void* g_pre_t, int64_t ldt, float* colsum_part,
-                        int64_t B, int64_t K, int64_t h, int dtype) {
+int cc_dacts_bwd_t(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
+                   const uint32_t* mask_bits, void* g_pre_t, int64_t ldt, float* colsum_part, int64_t B, int64_t K,
+                   int64_t h, int dtype, void* stream) {
   if (!g_pre_t || !acts) return CC_ERR_NULL;
-  a = GemmArgs{};
+  GemmArgs a = {};
   a.A = g_recon; a.lda = K; a.B = W_dec; a.ldb = K;
   a.M = (int)B; a.N = (int)h; a.K = (int)K;
   a.out = nullptr; a.ldo = h; a.mask_src = acts; a.tn = tn; a.scale0 = l1_scale;
@@ -1228,48 +1162,6 @@ static int dacts_t_args(GemmArgs& a, const void* g_recon, const void* W_dec, con
   if (rc) return rc;
   if (mask_bits && !al16(mask_bits)) return CC_ERR_ALIGN;
   if (B % 8 || ldt % 8 || ldt < B || !al16(g_pre_t) || !use_pp(a.N, true, true, dtype)) return CC_ERR_SHAPE;
-  a.nbm = (a.M + BM - 1) / BM;
-  a.nbn = (a.N + 255) / 256;
-  return CC_OK;
-}
-
-int cc_dacts_bwd_loss_t(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
-                        const uint32_t* mask_bits, void* g_pre_t, int64_t ldt, float* colsum_part,
-                        const float* acts_colpart, int64_t R, float* l1_part, const float* row_part, int64_t ncb,
-                        const float* l0_part, int64_t n_l0, float* ev, float* ev_a, float* ev_b, float* scalars,
-                        float* l1l0_out, float* host_out, uint32_t seq, uint32_t* counter, int64_t B, int64_t n,
-                        int64_t d, int64_t h, int dtype, void* stream) {
-  if (!acts_colpart || !tn || !l1_part || !row_part || !scalars || !counter) return CC_ERR_NULL;
-  if (R <= 0 || n <= 0 || d <= 0 || ncb <= 0) return CC_ERR_SHAPE;
-  GemmArgs a;
-  int rc = dacts_t_args(a, g_recon, W_dec, acts, tn, l1_scale, mask_bits, g_pre_t, ldt, colsum_part, B, n * d, h, dtype);
-  if (rc) return rc;
-  LossTail lt = {};
-  const int nred = (int)((h + RED_COLS - 1) / RED_COLS);
-  const int nblk = (int)((B + 255) / 256);
-  float* ev_part = scalars + 8;  // as cc_loss_finalize (cc_loss_scalars_len)
-  lt.red = {acts_colpart, (int)R, (int)h, h, 1.f, nullptr, nullptr, nullptr, tn, l1_part};
-  lt.red_blocks = nred;
-  lt.ev = {row_part, (int)B, (int)n, (int)ncb, ev, ev_a, ev_b, ev_part};
-  lt.ev_blocks = nblk;
-  lt.scal = {ev_part, nblk, l1_part, nred, l0_part, n_l0, (int)B, scalars, l1l0_out, host_out, (unsigned)seq};
-  lt.counter = counter;
-  const dim3 grid(pp_grid(a.nbm * a.nbn));
-  hipStream_t st = (hipStream_t)stream;
-  if (g_pp_fast && a.M % BM == 0 && a.N % 256 == 0 && a.mask_bits)
-    hipLaunchKernelGGL((gemm_pp_losstail_kernel<true, true, EPI_DACTS, true>), grid, dim3(NTHR), 0, st, a, lt);
-  else
-    hipLaunchKernelGGL((gemm_pp_losstail_kernel<true, true, EPI_DACTS, false>), grid, dim3(NTHR), 0, st, a, lt);
-  CC_LAUNCH_CHECK();
-  return CC_OK;
-}
-
-int cc_dacts_bwd_t(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
-                   const uint32_t* mask_bits, void* g_pre_t, int64_t ldt, float* colsum_part, int64_t B, int64_t K,
-                   int64_t h, int dtype, void* stream) {
-  GemmArgs a;
-  int rc = dacts_t_args(a, g_recon, W_dec, acts, tn, l1_scale, mask_bits, g_pre_t, ldt, colsum_part, B, K, h, dtype);
-  if (rc) return rc;
   return launch_pp<true, true, EPI_DACTS>(a, (hipStream_t)stream);
 }
 }  // extern "C"

@@ -384,38 +384,17 @@ def dacts_rows(ws, P, l1_coeff, r0, r1, l1_grad_weight=1.0):
                           colsum_part=ws.gpre_colpart[c0:c1])
 
 
-def loss_tail_in_dacts(ws):
-    """Whether G3 can run the forward's deferred loss tail in its own launch (backward(loss_tail=...))."""
-    return bool(ws.tr)
-
-
-def dacts_loss(ws, P, l1_coeff, l1_grad_weight=1.0, host=None, seq=0):
-    """G3 over the whole batch + the loss tail the forward deferred (forward(finalize=False)) in one launch:
-    ws.scalars / ws.ev* (and the mapped host copy + sequence word) are final when G3 is."""
-    assert ws.acts_pending, "the loss tail already ran"
-    l1_scale = float(l1_coeff) * l1_grad_weight / ws.B
-    ncb = ws.row_ncb if ws.row_ncb is not None else ws.ncb
-    with _span("G3_dacts"):
-        ops.dacts_bwd_loss_t(ws.g_recon, P.W_dec_hk, ws.acts, ws.tn, l1_scale, ws.g_pre_t, ws.gpre_colpart,
-                             ws.mask_bits, ws.acts_colpart, ws.l1_part, _row_part(ws), ncb, ws.l0_part, ws.n_wave,
-                             ws.ev, ws.ev_a, ws.ev_b, ws.scalars, ws.tail_ctr[0:1], ws.n, ws.d, host=host, seq=seq)
-    ws.acts_pending = False
-
-
 def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None, sums_out=None, zero_mask=0,
-             tail_done=None, loss_tail=None):
+             tail_done=None):
     """Gradients of l2 + l1_coeff * l1 into the grads Arena G (+ squared-sum partials).
     dacts_done: G3 already ran per batch slice (dacts_rows).  tail_done: the event of a loss tail
     running beside (loss_finalize_beside), waited for before G4.  clip (max_norm, single-GPU step): the
     bias-gradient sums and clip_grad_norm_'s coefficient in one launch (clip_and_adam then skips
     its clip_finalize).  sums_out (latent-sharded step): instead, the per-parameter squared sums in
-    the same launch (segment_sums semantics, zero_mask), for the all-reduce.  loss_tail (host, seq): the
-    forward deferred its loss tail; G3 runs it (dacts_loss, loss_tail_in_dacts)."""
+    the same launch (segment_sums semantics, zero_mask), for the all-reduce."""
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
     l1_scale = float(l1_coeff) * l1_grad_weight / B
-    if loss_tail is not None:
-        dacts_loss(ws, P, l1_coeff, l1_grad_weight, *loss_tail)
-    elif not dacts_done:
+    if not dacts_done:
         dacts_rows(ws, P, l1_coeff, 0, B, l1_grad_weight)
     if tail_done is not None:
         torch.cuda.current_stream(ws.x.device).wait_event(tail_done)

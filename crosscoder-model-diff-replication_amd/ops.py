@@ -297,25 +297,6 @@ def dacts_bwd_t(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre_t, colsum_part=None
                                dtype_code(g_recon.dtype), _stream(g_recon)))
 
 
-def dacts_bwd_loss_t(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre_t, colsum_part, mask_bits, acts_colpart, l1_part,
-                     row_part, ncb, l0_part, n_l0, ev, ev_a, ev_b, scalars, counter, n, d, host=None, seq=0,
-                     l1l0_out=None):
-    """dacts_bwd_t over the whole batch + the forward's loss tail in the same launch (cc_dacts_bwd_loss_t):
-    the loss scalars (and, with a _hip.MappedHostBuffer `host`, their host copy + sequence word `seq`)."""
-    B, K = g_recon.shape
-    h = W_dec_hk.shape[0]
-    if g_pre_t.shape != (h, B) or g_pre_t.stride(1) != 1:
-        raise ValueError("g_pre_t must be an [h, B] view with unit column stride")
-    if mask_bits is not None and mask_bits.numel() < mask_bits_words(B, h):
-        raise ValueError("mask_bits too small")
-    check(lib().cc_dacts_bwd_loss_t(
-        _ptr(g_recon), _ptr(W_dec_hk), _ptr(acts), _ptr(tn), l1_scale, _ptr(mask_bits), _ptr(g_pre_t),
-        g_pre_t.stride(0), _ptr(colsum_part), _ptr(acts_colpart), acts_colpart.shape[0], _ptr(l1_part),
-        _ptr(row_part), ncb, _ptr(l0_part), n_l0, _ptr(ev), _ptr(ev_a), _ptr(ev_b), _ptr(scalars), _ptr(l1l0_out),
-        host.device_ptr if host is not None else None, seq, _ptr(counter), B, n, d, h, dtype_code(g_recon.dtype),
-        _stream(g_recon)))
-
-
 def mask_bits_rows(mask_bits, h, r0, r1):
     """The mask bits of batch rows [r0, r1) (r0 % 256 == 0) of encode_fwd_t's [B][h] bits."""
     if r0 % 256:

@@ -9,7 +9,7 @@ reference's) lives in arenas mirroring the parameter arena, exposed through
 import torch
 import tqdm
 
-from . import _hip, engine
+from . import engine
 from .buffer import Buffer
 from .crosscoder import CrossCoder
 
@@ -87,8 +87,6 @@ class Trainer:
         self.step_counter = 0
         self.logger = logger
         self._host = None  # pinned loss-scalar landing buffer (allocated on the first step)
-        self._mapped = None  # mapped host words G3's loss tail writes (loss scalars + sequence word)
-        self._seq = 0
         self._side = None  # stream of the decoder half's Adam (created on the first step)
 
     def lr_lambda(self, step):
@@ -107,17 +105,12 @@ class Trainer:
         on_losses(scalars): called (on the side stream) right after the loss scalars are enqueued, before
         the backward / clip / Adam launches."""
         scalars, done = self._launch_step(on_losses)
-        if done is not None:
-            torch.cuda.current_stream(scalars.device).wait_event(done)
-        elif on_losses is not None:
-            on_losses(scalars)
+        torch.cuda.current_stream(scalars.device).wait_event(done)
         return scalars
 
     def _launch_step(self, on_losses):
-        """The step's launches; returns (ws.scalars, the event that marks the loss tail's end, or None when G3 ran
-        the loss tail on torch's stream -- then the scalars also land in the mapped host words with sequence
-        number self._seq, and on_losses is not called).  step() does not order torch's stream after a
-        side-stream tail (the host waits for the loss copy instead)."""
+        """The step's launches; returns (ws.scalars, the event that marks the loss tail's end).  step()
+        does not order torch's stream after the tail (the host waits for the loss copy instead)."""
         cc = self.crosscoder
         raw, factor = self.buffer.next_raw()
         raw = cc.pad_input(raw)  # (zero columns only when d_in % 8 != 0)
@@ -127,19 +120,11 @@ class Trainer:
         side = self._side_stream()
         # prep, G1, G2 + the loss rows (one pass where decode_loss_t serves the shape)
         engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None, finalize=False)
+        # the loss scalars (+ their host copy) on the side stream, beside G3 (read by nothing on this stream)
+        done = engine.loss_finalize_beside(ws, side, on_losses)
         l1c = self.get_l1_coeff()
-        if engine.loss_tail_in_dacts(ws):
-            # the loss scalars in G3's launch, straight to mapped host memory (no side stream, event or copy);
-            # clip_grad_norm_(max_norm=1.0), trainer.py:46
-            if self._mapped is None:
-                self._mapped = _hip.MappedHostBuffer(16)
-            self._seq += 1
-            done = None
-            engine.backward(ws, P, opt.grads, l1c, clip=1.0, loss_tail=(self._mapped, self._seq))
-        else:
-            # the loss scalars (+ their host copy) on the side stream, beside G3 (read by nothing on this stream)
-            done = engine.loss_finalize_beside(ws, side, on_losses)
-            engine.backward(ws, P, opt.grads, l1c, clip=1.0)
+        # clip_grad_norm_(max_norm=1.0), trainer.py:46
+        engine.backward(ws, P, opt.grads, l1c, clip=1.0)
         g = opt.param_groups[0]
         opt.t += 1
         b1, b2 = g["betas"]
@@ -173,13 +158,9 @@ class Trainer:
         self.crosscoder.arena().wait_pending()
 
     def step(self):
-        _, done = self._launch_step(self._copy_losses)
-        if done is None:
-            self._mapped.wait(8, self._seq)
-            s = [float(v) for v in self._mapped.f32[:6]]
-        else:
-            self._copied.synchronize()
-            s = self._host[:6].tolist()
+        self._launch_step(self._copy_losses)
+        self._copied.synchronize()
+        s = self._host[:6].tolist()
         l1c = self._last_l1c
         dt = self.crosscoder.dtype
         l2, l1, l0 = s[0], rounded(s[1], dt), s[2]

@@ -230,20 +230,6 @@ int cc_dacts_bwd_t(const void* g_recon, const void* W_dec, const void* acts, con
                    const uint32_t* mask_bits, void* g_pre_t, int64_t ldt, float* colsum_part, int64_t B, int64_t K,
                    int64_t h, int dtype, void* stream);
 
-/* cc_dacts_bwd_t (whole batch, K = n*d) with the forward's loss tail in the same launch (the single-GPU
- * Trainer.step, trainer.py:43-44 -> crosscoder.py:106-130): before its tiles the launch forms the l1 dot
- * partials of the activation column sums (acts_colpart, R rows) against tn, the per-row EVs from the loss row
- * terms (row_part, ncb column blocks per model) and, in the last workgroup to arrive, the loss scalars --
- * exactly what cc_loss_tail_nb(acts_colpart, R, h, NULL, tn, l1_part, row_part, ncb, ...) computes.  host_out
- * (optional, mapped pinned memory): also receives scalars[0:8] and then `seq` in word 8.  counter: a device
- * word that is 0 between launches. */
-int cc_dacts_bwd_loss_t(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
-                        const uint32_t* mask_bits, void* g_pre_t, int64_t ldt, float* colsum_part,
-                        const float* acts_colpart, int64_t R, float* l1_part, const float* row_part, int64_t ncb,
-                        const float* l0_part, int64_t n_l0, float* ev, float* ev_a, float* ev_b, float* scalars,
-                        float* l1l0_out, float* host_out, uint32_t seq, uint32_t* counter, int64_t B, int64_t n,
-                        int64_t d, int64_t h, int dtype, void* stream);
-
 /* W_dec.grad [h][K] = acts^T . g_recon + l1_scale * sum_b(acts[:,h]) * W_dec[h,m,:]/||W_dec[h,m,:]||
  * (norm backward is 0 where the norm is 0; inv_norms from cc_dec_norms).
  * sq_part [cc_wgrad_parts(h,K,dtype)]: sum of grad^2. */

@@ -22,10 +22,15 @@ for s in $STEPS; do
   case $s in
     test) run pytest_gpu 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ;;
     ab) run step_ab 600 bash tools/ab_trees.sh exp_head . 4 "$OUT/trees" ;;
+    ab3) run step_ab3 900 bash tools/ab_multi.sh 4 "$OUT/trees3" exp_prev exp_head . ;;
     gemm) run gemm 300 python tools/gemm_bench.py crosscoder-model-diff-replication_amd/libcrosscoder_hip.so ;;
     gemmdbg) run gemmdbg 300 python tools/gemm_bench.py crosscoder-model-diff-replication_amd/libcrosscoder_hip_dbg.so@5 \
                crosscoder-model-diff-replication_amd/libcrosscoder_hip_dbg.so@7 ;;
     bench) run bench 300 python bench.py ;;
+    sprof) run sprof 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/sprof" -o run -- \
+             python bench.py --no-cpu-baseline --steps 20 --force-sharded
+           f=$(find "$OUT/sprof" -name '*kernel_trace.csv' | head -1); [ -n "$f" ] && python tools/step_timeline.py "$f" 12 > "$OUT/timeline_sharded.txt" ;;
+    sbench) run sbench 400 bash -c "python bench.py --no-cpu-baseline --force-sharded > $OUT/sh4.json && python bench.py --no-cpu-baseline --force-sharded --recon-chunks 2 > $OUT/sh2.json && python bench.py --no-cpu-baseline --force-sharded --recon-chunks 1 > $OUT/sh1.json && python bench.py --no-cpu-baseline > $OUT/single.json" ;;
     probe) run probe 400 python tools/gemm_bench.py crosscoder-model-diff-replication_amd/libcrosscoder_hip.so \
              $(ls crosscoder-model-diff-replication_amd/exp/*.so) ;;
     prof) run prof_new 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof_new" -o run -- \

@@ -1,9 +1,11 @@
 #!/bin/bash
-# Build tree of a commit (default HEAD) for tools/ab_trees.sh: exp_head/ (sources + its own library, no fixtures)
+# Build tree of a commit (default HEAD) for tools/ab_trees.sh / ab_multi.sh: DIR (default exp_head/; sources +
+# its own library, no fixtures).   tools/snapshot_head.sh [REV] [DIR]
 set -e
 REV=${1:-HEAD}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-rm -rf "$ROOT/exp_head" && mkdir -p "$ROOT/exp_head"
-git -C "$ROOT" archive "$REV" | tar -x -C "$ROOT/exp_head" --exclude=tests/golden
-make -s -C "$ROOT/exp_head/crosscoder-model-diff-replication_amd/csrc" -j8 > /dev/null
-echo "$ROOT/exp_head"
+DIR=$ROOT/${2:-exp_head}
+rm -rf "$DIR" && mkdir -p "$DIR"
+git -C "$ROOT" archive "$REV" | tar -x -C "$DIR" --exclude=tests/golden
+make -s -C "$DIR/crosscoder-model-diff-replication_amd/csrc" -j8 > /dev/null
+echo "$DIR"
