@@ -217,7 +217,7 @@ def main():
     ap.add_argument("--comm", choices=("all_reduce", "reduce_scatter"), default="all_reduce",
                     help="latent-sharded step: the partial-reconstruction exchange")
     ap.add_argument("--recon-chunks", type=int, default=None,
-                    help="latent-sharded step: batch slices the exchange is overlapped by (default 4)")
+                    help="latent-sharded step: batch slices the exchange is overlapped by (default 2)")
     ap.add_argument("--force-sharded", action="store_true",
                     help="diagnostic: run the latent-sharded step even on one rank (1-rank RCCL group)")
     args = ap.parse_args()

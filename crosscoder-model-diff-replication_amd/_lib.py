@@ -91,6 +91,7 @@ SIGNATURES = {
     "cc_fold_scaling": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_decoder_stats": (_i, [_p, _i64, _i64, _i64, _i, _p, _p, _p, _p]),
     "cc_adam_step": (_i, [_p, _p, _p, _p, _i64, _p, _d, _d, _d, _d, _i64, _i64, _i, _p]),
+    "cc_adam_step_clip": (_i, [_p, _p, _p, _p, _i64, _p, _i, _f, _i, _p, _d, _d, _d, _d, _i64, _i64, _i, _p]),
 }
 
 _lib = None

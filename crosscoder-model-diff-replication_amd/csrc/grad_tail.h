@@ -67,6 +67,24 @@ CC_DEV void reduce_rows_phase2(const RedSeg& a, int blk, int t, float (*red)[RED
 }
 CC_DEV float bf16r(float f) { return bf2f(f2bf(f)); }
 
+// clip_grad_norm_'s scalar arithmetic (torch/nn/utils/clip_grad.py): a parameter's norm from its squared sum
+// (bf16-rounded as torch._foreach_norm on bf16 returns bf16), then the total norm and the coefficient
+CC_DEV float clip_param_norm(double sq, int emulate_bf16) {
+  const float nr = (float)sqrt(sq);
+  return emulate_bf16 ? bf16r(nr) : nr;
+}
+CC_DEV float clip_coef(const float* norms, int nparams, float max_norm, int emulate_bf16, float& total) {
+  float s = 0.f;
+  for (int p = 0; p < nparams; ++p) s += norms[p] * norms[p];
+  total = sqrtf(s);
+  if (emulate_bf16) {
+    total = bf16r(total);                       // vector_norm(stack(bf16 norms)) -> bf16
+    const float den = bf16r(total + 1e-6f);     // bf16 tensor + python scalar
+    return fminf(bf16r(max_norm / den), 1.f);
+  }
+  return fminf(max_norm / (total + 1e-6f), 1.f);
+}
+
 struct ClipArgs {
   const float* sq;
   int64_t off[9];
@@ -128,24 +146,12 @@ CC_DEV void clip_finish(const ClipArgs& a, const double* s, double (*red)[NT / 6
     const int p = threadIdx.x;
     double t = 0.0;
     for (int w = 0; w < NT / 64; ++w) t += red[p][w];
-    float nr = (float)sqrt(t);
-    if (a.emulate_bf16) nr = bf16r(nr);  // torch._foreach_norm on bf16 returns bf16
-    norms[p] = nr;
+    norms[p] = clip_param_norm(t, a.emulate_bf16);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int p = 0; p < a.nparams; ++p) s += norms[p] * norms[p];
-    float total = sqrtf(s);
-    float coef;
-    if (a.emulate_bf16) {
-      total = bf16r(total);                       // vector_norm(stack(bf16 norms)) -> bf16
-      float den = bf16r(total + 1e-6f);           // bf16 tensor + python scalar
-      coef = bf16r(a.max_norm / den);
-      coef = fminf(coef, 1.f);
-    } else {
-      coef = fminf(a.max_norm / (total + 1e-6f), 1.f);
-    }
+    float total;
+    const float coef = clip_coef(norms, a.nparams, a.max_norm, a.emulate_bf16, total);
     a.out[0] = coef;
     a.out[1] = total;
     for (int p = 0; p < a.nparams; ++p) a.out[2 + p] = norms[p];

@@ -359,7 +359,29 @@ struct AdamArgs {
   float beta2, omb2, eps;
   float bc2s;       // sqrt(1 - beta2^t)
   float neg_step;   // -lr / (1 - beta1^t)
+  // clip coefficient formed in the kernel (instead of read from coef): clip_grad_norm_ over the clip_np
+  // per-parameter squared sums clip_sums (e.g. all-reduced over the latent shards); block 0 writes clip_out
+  // [coef, total, norms...] like cc_clip_finalize
+  const float* clip_sums;
+  int clip_np, clip_emulate;
+  float clip_max_norm;
+  float* clip_out;
 };
+// The step's clip coefficient: read (coef), formed from squared sums (clip_sums), or 1
+CC_DEV float adam_coef(const AdamArgs& a) {
+  if (a.clip_sums) {
+    float norms[8], total;
+    for (int p = 0; p < a.clip_np; ++p) norms[p] = clip_param_norm((double)a.clip_sums[p], a.clip_emulate);
+    const float c = clip_coef(norms, a.clip_np, a.clip_max_norm, a.clip_emulate, total);
+    if (a.clip_out && blockIdx.x == 0 && threadIdx.x == 0) {
+      a.clip_out[0] = c;
+      a.clip_out[1] = total;
+      for (int p = 0; p < a.clip_np; ++p) a.clip_out[2 + p] = norms[p];
+    }
+    return c;
+  }
+  return a.coef ? *a.coef : 1.f;
+}
 // One Adam element update with torch's rounding points (see adam_kernel).
 template <int DT>
 CC_DEV void adam_elem(const AdamArgs& a, float coef, float& p, float g, float& m, float& v) {
@@ -389,7 +411,7 @@ constexpr int ADAM_U = 1;
 // config-2 arena = 5.4 TB/s; U = 2: 398 us; the grid-stride loop: 431 us).
 template <int DT, int U>
 __global__ __launch_bounds__(256) void adam_bulk_kernel(const AdamArgs a, int64_t nchunks) {
-  const float coef = a.coef ? *a.coef : 1.f;
+  const float coef = adam_coef(a);
   const int64_t c0 = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
   float p[U][8], g[U][8], m[U][8], v[U][8];
 #pragma unroll
@@ -416,7 +438,7 @@ __global__ __launch_bounds__(256) void adam_bulk_kernel(const AdamArgs a, int64_
 template <int DT>
 __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   using E = Elem<DT>;
-  const float coef = a.coef ? *a.coef : 1.f;
+  const float coef = adam_coef(a);
   const int64_t stride = (int64_t)gridDim.x * 256 * 8;
   for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8; i < a.numel; i += stride) {
     float p[8], g[8], m[8], v[8];
@@ -474,7 +496,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
 __global__ __launch_bounds__(256) void adam_dec_tr_kernel(const AdamArgs a, int h, int K, char* __restrict__ wt,
                                                           float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) char tile[64 * 128];
-  const float coef = a.coef ? *a.coef : 1.f;
+  const float coef = adam_coef(a);
   const int nr = (h + 63) / 64, nblk = K / 64, ntiles = nr * nblk;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g4 = lane >> 4, i = lane & 15, q4 = i >> 2, p4 = i & 3;
@@ -765,6 +787,7 @@ static AdamArgs adam_args(void* p, const void* g, void* m, void* v, int64_t nume
   a.neg_step = (float)(-((double)lr / bc1));
   return a;
 }
+static int adam_launch(const AdamArgs& a, int64_t max_blocks, int dtype, hipStream_t st);
 
 extern "C" {
 
@@ -789,8 +812,29 @@ int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const 
   if (!p || !g || !m || !v) return CC_ERR_NULL;
   if (numel <= 0 || step <= 0) return CC_ERR_SHAPE;
   if (!al16(p) || !al16(g) || !al16(m) || !al16(v)) return CC_ERR_ALIGN;
-  const AdamArgs a = adam_args(p, g, m, v, numel, coef, lr, beta1, beta2, eps, step);
-  hipStream_t st = (hipStream_t)stream;
+  return adam_launch(adam_args(p, g, m, v, numel, coef, lr, beta1, beta2, eps, step), max_blocks, dtype,
+                     (hipStream_t)stream);
+}
+
+int cc_adam_step_clip(void* p, const void* g, void* m, void* v, int64_t numel, const float* sums, int nparams,
+                      float max_norm, int emulate_bf16, float* clip_out, double lr, double beta1, double beta2,
+                      double eps, int64_t step, int64_t max_blocks, int dtype, void* stream) {
+  if (!p || !g || !m || !v || !sums) return CC_ERR_NULL;
+  if (numel <= 0 || step <= 0 || nparams <= 0 || nparams > 6) return CC_ERR_SHAPE;
+  if (!al16(p) || !al16(g) || !al16(m) || !al16(v)) return CC_ERR_ALIGN;
+  AdamArgs a = adam_args(p, g, m, v, numel, nullptr, lr, beta1, beta2, eps, step);
+  a.clip_sums = sums;
+  a.clip_np = nparams;
+  a.clip_emulate = emulate_bf16;
+  a.clip_max_norm = max_norm;
+  a.clip_out = clip_out;
+  return adam_launch(a, max_blocks, dtype, (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+static int adam_launch(const AdamArgs& a, int64_t max_blocks, int dtype, hipStream_t st) {
+  const int64_t numel = a.numel;
   if (max_blocks > 0) {  // capped grid-stride form: leaves most CUs to a concurrent GEMM
     int64_t work = (numel + 7) / 8;
     int64_t blocks = (work + 255) / 256;
@@ -810,13 +854,15 @@ int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const 
     const int es = dtype == CC_BF16 ? 2 : 4;
     const int64_t off = nchunks * 8 * es;
     AdamArgs t = a;
-    t.p = (char*)p + off; t.g = (const char*)g + off; t.m = (char*)m + off; t.v = (char*)v + off;
+    t.p = (char*)a.p + off; t.g = (const char*)a.g + off; t.m = (char*)a.m + off; t.v = (char*)a.v + off;
     t.numel = numel % 8;
     DISPATCH_DT(dtype, hipLaunchKernelGGL((adam_kernel<DT_>), dim3(1), dim3(256), 0, st, t));
     CC_LAUNCH_CHECK();
   }
   return CC_OK;
 }
+
+extern "C" {
 
 
 static int grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,

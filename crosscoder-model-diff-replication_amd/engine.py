@@ -451,20 +451,31 @@ def clip_and_adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, max_norm=1.0, sid
     adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream)
 
 
-def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None):
-    """Adam with the clip coefficient in ws.clip_out[0].  side_stream: the encoder half runs on torch's
+def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sums=None):
+    """Adam with the clip coefficient in ws.clip_out[0] -- or, clip_sums (sums [4], max_norm): formed in each
+    launch from the per-parameter squared gradient sums (cc_adam_step_clip; the encoder-half launch also writes
+    ws.clip_out), so no clip launch sits between the sums' all-reduce and Adam.  side_stream: the encoder half runs on torch's
     stream, then the decoder half (+ the next step's decoder norms / W_dec^T) on the side stream, so it
     overlaps the next step's prep / encoder GEMM (G1 reads only the encoder half); P.pending orders every
     later decoder-half use (forward() waits before G2; CrossCoder's accessors, FusedAdam.state and
     Trainer.synchronize() wait).  Without a side stream: one launch over the whole arena."""
     coef = ws.clip_out[0:1]
+    emulate = ws.dtype == torch.bfloat16
+
+    def step_(p, g, m, v, max_blocks=0, clip_out=None):
+        if clip_sums is None:
+            ops.adam_step(p, g, m, v, coef, lr, beta1, beta2, eps, step, max_blocks=max_blocks)
+        else:
+            ops.adam_step_clip(p, g, m, v, clip_sums[0], clip_sums[1], emulate, lr, beta1, beta2, eps, step,
+                               max_blocks=max_blocks, clip_out=clip_out)
+
     if side_stream is None:
         with _span("adam"):
-            ops.adam_step(P.data, G.data, M.data, V.data, coef, lr, beta1, beta2, eps, step)
+            step_(P.data, G.data, M.data, V.data, clip_out=ws.clip_out)
         return
     dev = P.data.device
     with _span("adam"):
-        ops.adam_step(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), coef, lr, beta1, beta2, eps, step)
+        step_(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), clip_out=ws.clip_out)
     # both halves are HBM-bound: the decoder half starts after the encoder half (run together they only
     # share the bandwidth), i.e. beside the next step's prep / G1 on the main stream
     enc_done = torch.cuda.Event()
@@ -472,8 +483,7 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None):
     with torch.cuda.stream(side_stream):
         side_stream.wait_event(enc_done)
         with _span("adam_dec"):
-            ops.adam_step(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), coef, lr, beta1, beta2, eps, step,
-                          max_blocks=DEC_ADAM_BLOCKS)
+            step_(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), max_blocks=DEC_ADAM_BLOCKS)
         norms_for_next(ws, P)
         done = torch.cuda.Event()
         done.record(side_stream)

@@ -417,6 +417,14 @@ def adam_step(p, g, m, v, coef, lr, beta1, beta2, eps, step, max_blocks=0):
                              int(step), int(max_blocks), dtype_code(p.dtype), _stream(p)))
 
 
+def adam_step_clip(p, g, m, v, sums, max_norm, emulate_bf16, lr, beta1, beta2, eps, step, max_blocks=0,
+                   clip_out=None):
+    """adam_step with the clip coefficient formed in the kernel from per-parameter squared sums (fp32 [nparams])."""
+    check(lib().cc_adam_step_clip(_ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(sums), sums.numel(),
+                                  float(max_norm), int(emulate_bf16), _ptr(clip_out), lr, beta1, beta2, eps, int(step),
+                                  int(max_blocks), dtype_code(p.dtype), _stream(p)))
+
+
 # ---------------------------------------------------------------- around the step (SURVEY §8f)
 def gather_rows(src, perm, out=None):
     """out[i] = src[perm[i]] over dim 0 (Buffer.refresh's shuffle); perm int64 on the same device."""

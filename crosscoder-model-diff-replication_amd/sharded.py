@@ -6,7 +6,7 @@ moments; b_dec is replicated.  Per step (reference Trainer.step, trainer.py:41-6
   1. every rank reads the SAME batch (replicated x), encodes its latents and decodes them into
      an fp32 partial reconstruction [B, n*d] (no bias)                     -> G1, G2 local
   2. all_reduce(SUM) of the partial reconstructions (the only bulk exchange: 4*B*n*d bytes),
-     issued per batch slice (`recon_chunks`, default 4) on RCCL's stream.  As soon as slice c
+     issued per batch slice (`recon_chunks`, default 2) on RCCL's stream.  As soon as slice c
      has landed, its loss rows / g_recon and its d_acts rows (G3) run on the compute stream
      while the all-reduce of slice c+1 is still on the wire, so only the first slice's
      all-reduce is exposed.  (Slicing the encode/decode instead would leave the 256-tile G2
@@ -23,6 +23,8 @@ drives a backend that does the local compute: `HipShardBackend` (the product, en
 kernels on one GPU).  The CPU tests drive the same `ShardedStep` with a torch-CPU backend over
 gloo to check the decomposition.
 """
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -114,9 +116,12 @@ class ShardedStep:
         # before the backward runs, so the host can read them (on_losses) and enqueue the next step
         # while this step's backward / clip / Adam still run.  The collective stream is in order, so
         # the compute stream's wait for the clip sums below also orders it after this one.
-        lw = dist.all_reduce(red[4:6], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-        if on_losses is not None:
-            on_losses(scalars, red, lw)
+        # (issued from the backend's auxiliary stream, which waits for the compute stream once: the compute
+        # stream records one event for both the collective and the host copy of on_losses)
+        with getattr(b, "collective_context", contextlib.nullcontext)():
+            lw = dist.all_reduce(red[4:6], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            if on_losses is not None:
+                on_losses(scalars, red, lw)
         b.backward(l1c, red, self.rank)              # red[0:4] = local squared sums (b_dec on rank 0 only)
         dist.all_reduce(red[0:4], op=dist.ReduceOp.SUM, group=self.group)
         if on_losses is None:
@@ -128,7 +133,7 @@ class ShardedStep:
 class HipShardBackend:
     """Local compute of one rank on its GPU (engine.py kernels)."""
 
-    def __init__(self, cc, recon_chunks=4, overlap_decoder_adam=True):
+    def __init__(self, cc, recon_chunks=2, overlap_decoder_adam=True):
         self.cc = cc
         self.side = torch.cuda.Stream(device=cc.arena().data.device) if overlap_decoder_adam else None
         a = cc.arena()
@@ -138,6 +143,17 @@ class HipShardBackend:
         self.red = torch.zeros(6, dtype=torch.float32, device=a.data.device)
         self.recon_chunks = recon_chunks
         self.ws = None
+        self._aux = None
+
+    @contextlib.contextmanager
+    def collective_context(self):
+        """torch's current stream -> an auxiliary stream that has waited for the compute stream (one event)."""
+        dev = self.cc.arena().data.device
+        if self._aux is None:
+            self._aux = torch.cuda.Stream(device=dev)
+        self._aux.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(self._aux):
+            yield
 
     def forward_partial(self, raw, factor):
         cc = self.cc
@@ -201,10 +217,10 @@ class HipShardBackend:
         return self.red
 
     def clip_and_adam_from_sums(self, sums, lr, betas, eps, t, max_norm):
-        ws = self.ws
-        ops.clip_finalize(sums, [0, 1, 2, 3, 4], max_norm, ws.dtype == torch.bfloat16, ws.clip_out)
-        # encoder half on this stream, decoder half + next step's norms on the side stream (engine.adam)
-        engine.adam(ws, self.cc.arena(), self.G, self.M, self.V, lr, betas[0], betas[1], eps, t, self.side)
+        # encoder half on this stream, decoder half + next step's norms on the side stream (engine.adam); each
+        # launch forms clip_grad_norm_'s coefficient from the all-reduced sums itself (no clip launch between)
+        engine.adam(self.ws, self.cc.arena(), self.G, self.M, self.V, lr, betas[0], betas[1], eps, t, self.side,
+                    clip_sums=(sums, max_norm))
 
 
 def shard_crosscoder(cfg, lo, hi, n_models=None):
@@ -232,7 +248,9 @@ class ShardedTrainer:
             crosscoder = shard_crosscoder(cfg, lo, hi)
         self.crosscoder = crosscoder
         self.buffer = buffer
-        chunks = recon_chunks if recon_chunks is not None else cfg.get("recon_chunks", 4)
+        # 2 slices: each costs a loss + d_acts launch pair and two stream hand-offs (~50 us, one GPU:
+        # profiles/r03_sharded_one_gpu.txt) and hides the exchange of the slices after the first
+        chunks = recon_chunks if recon_chunks is not None else cfg.get("recon_chunks", 2)
         self.backend = HipShardBackend(crosscoder, recon_chunks=chunks)
         self.engine = ShardedStep(self.backend, group, comm=comm)
         self.total_steps = cfg["num_tokens"] // cfg["batch_size"]
@@ -256,17 +274,15 @@ class ShardedTrainer:
         # pinned landing buffers, filled on a copy stream that waits for the forward (compute stream)
         # and for the l1 / l0 all-reduce: the host waits for the losses only, and the compute stream
         # never waits for the copy
+        # (called on the backend's auxiliary stream, which already waited for the compute stream)
         if self._host is None:
             self._host = torch.empty(8, dtype=torch.float32, pin_memory=True)
             self._host_red = torch.empty(6, dtype=torch.float32, pin_memory=True)
             self._copied = torch.cuda.Event()
-            self._copy_stream = torch.cuda.Stream(device=scalars.device)
-        self._copy_stream.wait_stream(torch.cuda.current_stream(scalars.device))
-        with torch.cuda.stream(self._copy_stream):
-            l1l0_work.wait()  # (the copy stream waits for the collective stream)
-            self._host.copy_(scalars[:8], non_blocking=True)
-            self._host_red.copy_(red[:6], non_blocking=True)
-            self._copied.record(self._copy_stream)
+        l1l0_work.wait()  # (this stream waits for the collective stream)
+        self._host.copy_(scalars[:8], non_blocking=True)
+        self._host_red.copy_(red[:6], non_blocking=True)
+        self._copied.record()
 
     def synchronize(self):
         """Order torch's current stream after the last step's side-stream (decoder-half) Adam."""

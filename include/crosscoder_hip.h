@@ -321,6 +321,14 @@ int cc_segment_sums(const float* sq, const int64_t* off, int nparams, int zero_m
 int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, double lr,
                  double beta1, double beta2, double eps, int64_t step, int64_t max_blocks, int dtype, void* stream);
 
+/* cc_adam_step with clip_grad_norm_'s coefficient formed in the kernel from the per-parameter squared
+ * gradient sums `sums` [nparams] (trainer.py:46 over parameters whose sums were combined elsewhere, e.g.
+ * all-reduced over the latent shards): the arithmetic of cc_clip_finalize over one element per parameter.
+ * clip_out (optional): [coef, total norm, per-parameter norms] as cc_clip_finalize writes them. */
+int cc_adam_step_clip(void* p, const void* g, void* m, void* v, int64_t numel, const float* sums, int nparams,
+                      float max_norm, int emulate_bf16, float* clip_out, double lr, double beta1, double beta2,
+                      double eps, int64_t step, int64_t max_blocks, int dtype, void* stream);
+
 /* ---- around the step ---- */
 
 /* Buffer.refresh's shuffle (buffer.py:111-113: buffer = buffer[randperm(rows)]): dst[i] = src[perm[i]]

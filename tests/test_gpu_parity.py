@@ -375,6 +375,37 @@ def test_adam_matches_torch(gpu, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("scale", [1e-3, 3.0])  # clip inactive / active
+def test_adam_with_in_kernel_clip_matches_clip_then_adam(gpu, dtype, scale):
+    """cc_adam_step_clip (the clip coefficient formed in the Adam launch from per-parameter squared sums, the
+    latent-sharded step's form) == cc_clip_finalize over the same sums + cc_adam_step, bit for bit (params,
+    moments and the clip outputs), in the one-pass and the capped grid-stride launch forms."""
+    g = torch.Generator().manual_seed(7)
+    n = 50021
+    mk = lambda sc: (torch.randn(n, generator=g) * sc).to(dtype).to(gpu)  # noqa: E731
+    p0, gr, m0 = mk(0.05), mk(1e-3), mk(1e-4)
+    v0 = (torch.rand(n, generator=g) * 1e-6).to(dtype).to(gpu)
+    sums = (torch.rand(4, generator=g) * scale).to(gpu)
+    outs = []
+    for fused in (False, True):
+        for max_blocks in (0, 64):
+            p, m, v = p0.clone(), m0.clone(), v0.clone()
+            clip = torch.zeros(8, device=gpu)
+            if fused:
+                ops.adam_step_clip(p, gr, m, v, sums, 1.0, dtype == torch.bfloat16, 5e-5, 0.9, 0.999, 1e-8, 3,
+                                   max_blocks=max_blocks, clip_out=clip)
+            else:
+                ops.clip_finalize(sums, [0, 1, 2, 3, 4], 1.0, dtype == torch.bfloat16, clip)
+                ops.adam_step(p, gr, m, v, clip[0:1], 5e-5, 0.9, 0.999, 1e-8, 3, max_blocks=max_blocks)
+            outs.append((p, m, v, clip[:6]))
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        for a, b in zip(o, outs[0]):
+            assert torch.equal(a, b)
+    assert (outs[0][3][0].item() < 1.0) == (scale > 1.0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_clip_matches_torch(gpu, dtype):
     g = torch.Generator().manual_seed(5)
     grads = [torch.randn(s, generator=g).to(dtype) for s in (1000, 3000, 16, 40)]
