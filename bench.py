@@ -25,8 +25,15 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
+# one HIP hardware queue per stream (HIP's default is 4 per process): the latent-sharded step uses the
+# compute stream, the side stream and RCCL's streams, and on a shared queue the side stream's decoder-half
+# Adam serialises behind the compute stream instead of running beside G1 (+0.2 ms per step, DESIGN.md
+# section 6; neutral for the single-GPU step).  Must be set before the process touches the GPU.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

@@ -200,21 +200,23 @@ __global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ rec
     if (x_mean) load8f(x_mean, col, mu);
   }
   const int64_t plane = (int64_t)n * ncb * B;  // row_part [2][n*ncb][B]
-  // two rows per trip (r, r + 4): both rows' loads are in flight together
-  for (int i = 0; i < LOSS_ROWS / 4; i += 2) {
+  // LOSS_U rows per trip (r, r + 4, ...): their loads are in flight together (the column sums still
+  // add the wave's rows in order)
+  constexpr int LOSS_U = 2;
+  for (int i = 0; i < LOSS_ROWS / 4; i += LOSS_U) {
     const int ra = r0 + wave + 4 * i;
     if (ra >= row_end) break;  // wave-uniform
-    float rv[2][8], xv[2][8];
+    float rv[LOSS_U][8], xv[LOSS_U][8];
     if (cv) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < LOSS_U; ++u)
         if (ra + 4 * u < row_end) {
           load8f(recon, (int64_t)(ra + 4 * u) * K + col, rv[u]);
           load8<DT>(x, (int64_t)(ra + 4 * u) * K + col, xv[u]);
         }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < LOSS_U; ++u) {
       const int r = ra + 4 * u;
       if (r >= row_end) break;
       float l2 = 0.f, tv = 0.f;
@@ -382,6 +384,21 @@ CC_DEV float adam_coef(const AdamArgs& a) {
   }
   return a.coef ? *a.coef : 1.f;
 }
+// adam_coef for the whole block: from the squared sums it is ~100 dependent VALU ops (fp64 square roots), so
+// one wave forms it and the others read it from LDS -- with one 8-element chunk per thread (the bulk
+// kernel) every wave forming it costs the launch ~20 us.  Call with every thread of the block.  (Not for a
+// kernel meant to share CUs with the GEMMs: any LDS keeps its workgroups off a CU whose LDS a GEMM
+// workgroup holds.)
+CC_DEV float adam_coef_block(const AdamArgs& a) {
+  if (!a.clip_sums) return a.coef ? *a.coef : 1.f;
+  __shared__ float s_coef;
+  if (threadIdx.x < 64) {
+    const float c = adam_coef(a);
+    if (threadIdx.x == 0) s_coef = c;
+  }
+  __syncthreads();
+  return s_coef;
+}
 // One Adam element update with torch's rounding points (see adam_kernel).
 template <int DT>
 CC_DEV void adam_elem(const AdamArgs& a, float coef, float& p, float g, float& m, float& v) {
@@ -411,7 +428,6 @@ constexpr int ADAM_U = 1;
 // config-2 arena = 5.4 TB/s; U = 2: 398 us; the grid-stride loop: 431 us).
 template <int DT, int U>
 __global__ __launch_bounds__(256) void adam_bulk_kernel(const AdamArgs a, int64_t nchunks) {
-  const float coef = adam_coef(a);
   const int64_t c0 = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
   float p[U][8], g[U][8], m[U][8], v[U][8];
 #pragma unroll
@@ -423,6 +439,9 @@ __global__ __launch_bounds__(256) void adam_bulk_kernel(const AdamArgs a, int64_
       ld8<DT, SN>(a.v, c * 8, v[u]);
     }
   }
+  // the coefficient after the element loads are in flight (its inputs' latency hides under theirs; formed
+  // from the squared sums it also stores clip_out, which must not hold the loads back)
+  const float coef = adam_coef_block(a);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t c = c0 + u * 256;
@@ -438,6 +457,8 @@ __global__ __launch_bounds__(256) void adam_bulk_kernel(const AdamArgs a, int64_
 template <int DT>
 __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   using E = Elem<DT>;
+  // (per thread, once before the grid-stride loop: no LDS, so its workgroups still fit beside a GEMM
+  // workgroup that holds a CU's whole LDS -- the decoder half runs beside G1)
   const float coef = adam_coef(a);
   const int64_t stride = (int64_t)gridDim.x * 256 * 8;
   for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8; i < a.numel; i += stride) {

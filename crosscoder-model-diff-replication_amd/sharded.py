@@ -6,11 +6,12 @@ moments; b_dec is replicated.  Per step (reference Trainer.step, trainer.py:41-6
   1. every rank reads the SAME batch (replicated x), encodes its latents and decodes them into
      an fp32 partial reconstruction [B, n*d] (no bias)                     -> G1, G2 local
   2. all_reduce(SUM) of the partial reconstructions (the only bulk exchange: 4*B*n*d bytes),
-     issued per batch slice (`recon_chunks`, default 2) on RCCL's stream.  As soon as slice c
-     has landed, its loss rows / g_recon and its d_acts rows (G3) run on the compute stream
-     while the all-reduce of slice c+1 is still on the wire, so only the first slice's
-     all-reduce is exposed.  (Slicing the encode/decode instead would leave the 256-tile G2
-     launch a fraction of the 256 CUs per slice.)
+     issued per batch slice (`recon_chunks`: 2 over several ranks, 1 on one) on RCCL's stream.
+     As soon as slice c has landed, its loss rows / g_recon and its d_acts rows (G3) run on the
+     compute stream while the all-reduce of slice c+1 is still on the wire, so only the first
+     slice's all-reduce is exposed.  One slice is a synchronous collective on the compute stream.
+     (Slicing the encode/decode instead would leave the 256-tile G2 launch a fraction of the 256
+     CUs per slice: DESIGN.md section 6.)
   3. b_dec + loss + g_recon on the full reconstruction: identical on all ranks
   4. the rest of the backward is local (g_recon is replicated): G4, G5, db_enc local; db_dec
      replicated
@@ -24,6 +25,8 @@ kernels on one GPU).  The CPU tests drive the same `ShardedStep` with a torch-CP
 gloo to check the decomposition.
 """
 import contextlib
+import os
+import warnings
 
 import torch
 import torch.distributed as dist
@@ -82,6 +85,12 @@ class ShardedStep:
     def _combine_all_reduce(self, recon, l1c):
         b = self.b
         chunks = b.row_chunks()
+        if len(chunks) == 1:
+            # one slice: nothing to overlap, so a synchronous collective on the compute stream itself (torch
+            # runs it there: no event hand-off to the collective stream and back, ~55 us on one GPU)
+            dist.all_reduce(recon, op=dist.ReduceOp.SUM, group=self.group)
+            b.rows_ready(0, recon.shape[0], l1c)
+            return
         # every slice's all-reduce is queued at once on the collective stream; the compute stream
         # waits for slice c only when it needs it
         works = [dist.all_reduce(recon[r0:r1], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
@@ -103,7 +112,8 @@ class ShardedStep:
     def step(self, raw, factor, l1c, lr, betas, eps, t, max_norm=1.0, on_losses=None):
         """One step -> (scalars, red): the loss scalars (l1 / l0 of this rank's latents only) and the
         all-reduced [4 squared-gradient sums, l1, l0].  on_losses(scalars, red) is called once both
-        are final on the device (before the clip / Adam launches)."""
+        are final on the device (before the clip / Adam launches; torch's current stream is then an
+        auxiliary stream ordered after them)."""
         b = self.b
         recon = b.forward_partial(raw, factor)
         if self.comm == "all_reduce":
@@ -112,20 +122,16 @@ class ShardedStep:
             self._combine_reduce_scatter(recon, l1c)
         red = b.reduce_buffer()                      # [6]: 4 clip sums + l1, l0 (latent-local)
         scalars = b.loss_finalize(red)               # [l2, l1, l0, ev, ev_a, ev_b, ...]; red[4:6] = local l1, l0
-        # l1 / l0 over all ranks first (8 bytes, async on the collective stream): the losses are final
-        # before the backward runs, so the host can read them (on_losses) and enqueue the next step
-        # while this step's backward / clip / Adam still run.  The collective stream is in order, so
-        # the compute stream's wait for the clip sums below also orders it after this one.
-        # (issued from the backend's auxiliary stream, which waits for the compute stream once: the compute
-        # stream records one event for both the collective and the host copy of on_losses)
-        with getattr(b, "collective_context", contextlib.nullcontext)():
-            lw = dist.all_reduce(red[4:6], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            if on_losses is not None:
-                on_losses(scalars, red, lw)
         b.backward(l1c, red, self.rank)              # red[0:4] = local squared sums (b_dec on rank 0 only)
-        dist.all_reduce(red[0:4], op=dist.ReduceOp.SUM, group=self.group)
-        if on_losses is None:
-            lw.wait()
+        # one 24-byte collective for the squared sums and l1 / l0: a synchronous collective runs on torch's
+        # current stream (no hand-off to the collective stream and back)
+        dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
+        if on_losses is not None:
+            # the host copy from the backend's auxiliary stream (forked here, one event): the compute
+            # stream goes straight on to the clip + Adam launches
+            fork = getattr(b, "fork_aux", None)
+            with (fork() if fork is not None else contextlib.nullcontext()):
+                on_losses(scalars, red)
         b.clip_and_adam_from_sums(red[0:4], lr, betas, eps, t, max_norm)
         return scalars, red
 
@@ -133,7 +139,7 @@ class ShardedStep:
 class HipShardBackend:
     """Local compute of one rank on its GPU (engine.py kernels)."""
 
-    def __init__(self, cc, recon_chunks=2, overlap_decoder_adam=True):
+    def __init__(self, cc, recon_chunks=1, overlap_decoder_adam=True):
         self.cc = cc
         self.side = torch.cuda.Stream(device=cc.arena().data.device) if overlap_decoder_adam else None
         a = cc.arena()
@@ -145,15 +151,21 @@ class HipShardBackend:
         self.ws = None
         self._aux = None
 
-    @contextlib.contextmanager
-    def collective_context(self):
-        """torch's current stream -> an auxiliary stream that has waited for the compute stream (one event)."""
+    def fork_aux(self):
+        """A stream other than the compute stream, ordered after the compute stream's work so far (one
+        event); returns the context that makes it torch's current stream.  It is the side stream: idle
+        between its decoder-half Adam + norms and this step's Adam (which it waits for next), and on a
+        hardware queue of its own -- a stream created later may share the compute stream's queue (4 per
+        process), where the host copies would sit in front of the Adam launch."""
         dev = self.cc.arena().data.device
-        if self._aux is None:
-            self._aux = torch.cuda.Stream(device=dev)
-        self._aux.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(self._aux):
-            yield
+        if self.side is not None:
+            s = self.side
+        else:
+            if self._aux is None:
+                self._aux = torch.cuda.Stream(device=dev)
+            s = self._aux
+        s.wait_stream(torch.cuda.current_stream(dev))
+        return torch.cuda.stream(s)
 
     def forward_partial(self, raw, factor):
         cc = self.cc
@@ -248,9 +260,17 @@ class ShardedTrainer:
             crosscoder = shard_crosscoder(cfg, lo, hi)
         self.crosscoder = crosscoder
         self.buffer = buffer
-        # 2 slices: each costs a loss + d_acts launch pair and two stream hand-offs (~50 us, one GPU:
-        # profiles/r03_sharded_one_gpu.txt) and hides the exchange of the slices after the first
-        chunks = recon_chunks if recon_chunks is not None else cfg.get("recon_chunks", 2)
+        # batch slices of the exchange: one on a single rank (nothing to hide: a synchronous collective on
+        # the compute stream), otherwise 2 -- the second slice's exchange hides under the first slice's
+        # loss + d_acts, for a loss + d_acts launch pair and two stream hand-offs (~55 us,
+        # profiles/r03_sharded_one_gpu.txt)
+        chunks = recon_chunks if recon_chunks is not None else cfg.get("recon_chunks", 1 if self.world == 1 else 2)
+        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+            # RCCL's streams take hardware queues of their own: with HIP's default 4 per process the side
+            # stream can land on the compute stream's queue, and its decoder-half Adam then runs after the
+            # encoder half instead of beside the next G1 (+~0.2 ms per step, profiles/r03_sharded_one_gpu.txt)
+            warnings.warn("latent-sharded step: set GPU_MAX_HW_QUEUES=8 before the process touches the GPU "
+                          "(streams may share hardware queues)", RuntimeWarning, stacklevel=2)
         self.backend = HipShardBackend(crosscoder, recon_chunks=chunks)
         self.engine = ShardedStep(self.backend, group, comm=comm)
         self.total_steps = cfg["num_tokens"] // cfg["batch_size"]
@@ -270,16 +290,14 @@ class ShardedTrainer:
             return self.cfg["l1_coeff"] * self.step_counter / (0.05 * self.total_steps)
         return self.cfg["l1_coeff"]
 
-    def _copy_losses(self, scalars, red, l1l0_work):
-        # pinned landing buffers, filled on a copy stream that waits for the forward (compute stream)
-        # and for the l1 / l0 all-reduce: the host waits for the losses only, and the compute stream
-        # never waits for the copy
-        # (called on the backend's auxiliary stream, which already waited for the compute stream)
+    def _copy_losses(self, scalars, red):
+        # pinned landing buffers, filled on the backend's auxiliary stream (ordered after the all-reduce of
+        # the sums and l1 / l0): the host waits for the losses only, and the compute stream never waits for
+        # the copy
         if self._host is None:
             self._host = torch.empty(8, dtype=torch.float32, pin_memory=True)
             self._host_red = torch.empty(6, dtype=torch.float32, pin_memory=True)
             self._copied = torch.cuda.Event()
-        l1l0_work.wait()  # (this stream waits for the collective stream)
         self._host.copy_(scalars[:8], non_blocking=True)
         self._host_red.copy_(red[:6], non_blocking=True)
         self._copied.record()

@@ -19,8 +19,9 @@ B, N_MODELS, D, H, STEPS = 32, 2, 16, 64, 3
 class CpuShardBackend:
     """Local compute of one latent shard with torch autograd (test-side stand-in for the GPU)."""
 
-    def __init__(self, P):
+    def __init__(self, P, slices=2):
         self.P = {k: torch.nn.Parameter(v.detach().clone()) for k, v in P.items()}
+        self.slices = slices
         self.m = {k: torch.zeros_like(v) for k, v in self.P.items()}
         self.v = {k: torch.zeros_like(v) for k, v in self.P.items()}
         self.rs = False
@@ -34,7 +35,8 @@ class CpuShardBackend:
         return self.recon
 
     def row_chunks(self):
-        return [(0, B // 2), (B // 2, B)]  # two slices: exercises the sliced all-reduce path
+        # two slices: the sliced (asynchronous) all-reduce; one: the synchronous one
+        return [(0, B // 2), (B // 2, B)] if self.slices == 2 else [(0, B)]
 
     def rows_ready(self, r0, r1, l1c):
         pass  # the torch backend does all loss / backward work in loss_finalize / backward
@@ -124,7 +126,7 @@ def _setup():
     return cfg, P, raws, factor
 
 
-def _worker(rank, world, port, q, comm):
+def _worker(rank, world, port, q, comm, slices=2):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -133,22 +135,21 @@ def _worker(rank, world, port, q, comm):
         lo, hi = sharded.shard_range(H, world, rank)
         Ps = {"W_enc": P["W_enc"][:, :, lo:hi], "W_dec": P["W_dec"][lo:hi], "b_enc": P["b_enc"][lo:hi],
               "b_dec": P["b_dec"]}
-        backend = CpuShardBackend(Ps)
+        backend = CpuShardBackend(Ps, slices)
         step = sharded.ShardedStep(backend, comm=comm)
         outs = []
         seen = []
 
-        def on_losses(scalars, red, l1l0_work):
-            # called before the backward: after the l1 / l0 all-reduce the losses are already final
-            l1l0_work.wait()
-            seen.append(red[4:6].clone())
+        def on_losses(scalars, red):
+            # called after the all-reduce of the sums and l1 / l0, before the clip / Adam
+            seen.append(red.clone())
 
         for t in range(STEPS):
             l1c = 2.0 if t else 0.0
             cb = on_losses if t % 2 else None
             s, red = step.step(raws[t], factor, l1c, cfg["lr"], (0.9, 0.999), 1e-8, t + 1, on_losses=cb)
             if cb is not None:
-                assert torch.equal(seen[-1], red[4:6])
+                assert torch.equal(seen[-1], red)
             outs.append(torch.stack([s[0], red[4], red[5]]).clone())
         # numpy arrays pickle by value: a torch tensor would travel as a shared-memory fd that the
         # parent can only open while this process is still alive
@@ -157,15 +158,16 @@ def _worker(rank, world, port, q, comm):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("comm", ["all_reduce", "reduce_scatter"])
+@pytest.mark.parametrize("comm,slices", [("all_reduce", 2), ("all_reduce", 1), ("reduce_scatter", 1)])
 @pytest.mark.parametrize("world", [2])
-def test_sharded_step_matches_unsharded(world, comm):
-    """Both exchanges of the partial reconstructions: the sliced all-reduce, and the
-    reduce-scatter by batch rows -> loss on B/G rows -> all-gather of g_recon and the row terms."""
+def test_sharded_step_matches_unsharded(world, comm, slices):
+    """Both exchanges of the partial reconstructions: the all-reduce (in two batch slices, or
+    one synchronous collective), and the reduce-scatter by batch rows -> loss on B/G rows -> all-gather
+    of g_recon and the row terms."""
     port = 29500 + random.randint(0, 2000)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, comm)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, comm, slices)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}

@@ -1,5 +1,7 @@
 """A/B timing of the five step GEMMs (config-2 shapes) across library builds, interleaved in
-ONE process (cdna guide rule 24).  Usage: python tools/gemm_bench.py lib1.so [lib2.so ...]"""
+ONE process (cdna guide rule 24).  Usage: python tools/gemm_bench.py lib1.so [lib2.so ...]
+Env: CC_GEMM_B (batch rows, default 4096: e.g. 2048 for one of two batch slices), CC_GEMM_ONLY (comma list of
+the names below)."""
 import ctypes
 import os
 import sys
@@ -10,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import crosscoder_amd  # noqa: F401,E402
 from crosscoder_amd._lib import SIGNATURES  # noqa: E402
 
-B, n, d, h = 4096, 2, 2304, 16384
+B, n, d, h = int(os.environ.get("CC_GEMM_B", 4096)), 2, 2304, 16384
 K = n * d
 PEAK = 256 * 2.4e9 * 4096 / 1e12
 
@@ -97,7 +99,10 @@ def main():
         for path, L, mask in libs:
             if mask is not None:
                 L.cc_debug_set_pp_mask(mask)
+            only = os.environ.get("CC_GEMM_ONLY")
             for name, fn in calls(L).items():
+                if only and name not in only.split(","):
+                    continue
                 for _ in range(2):
                     assert fn() == 0
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -110,7 +115,7 @@ def main():
     for (p, name), ts in sorted(res.items(), key=lambda kv: (kv[0][1], kv[0][0])):
         ts.sort()
         med = ts[len(ts) // 2]
-        print(f"{name:14s} {p:34s} median {med*1e3:7.1f} us  min {ts[0]*1e3:7.1f} us  {flop/med/1e9:7.1f} TF/s "
+        print(f"B={B} {name:14s} {p:34s} median {med*1e3:7.1f} us  min {ts[0]*1e3:7.1f} us  {flop/med/1e9:7.1f} TF/s "
               f"({flop/med/1e9/PEAK*100:4.1f}% peak)")
 
 
