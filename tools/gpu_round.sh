@@ -2,13 +2,17 @@
 # One GPU-box session: parity tests, the bench line, a rocprofv3 kernel-trace summary of the same
 # bench command, and the GEMM / Adam A/B timers.  Every GPU step has its own time limit; the script
 # stops at the first fault, abort, segfault or timeout (test FAILURES -- exit 1 -- do not stop it).
-# Usage (repo root on the box): tools/gpu_round.sh [OUT] [steps...]   steps: test bench prof gemm ab stepab small adam pmc
+# Usage (repo root on the box): tools/gpu_round.sh [OUT] [steps...]
+#   steps: test smoke bench prof configs sharded gemm ab stepab small adam pmc
 OUT=${1:-gpurun_out/round}
 shift
 STEPS=${*:-test bench prof gemm adam}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 export PYTHONDONTWRITEBYTECODE=1
+# bench.py raises the HIP hardware-queue count to 8 itself; under rocprofv3 the profiler initialises HIP
+# before bench.py runs, so the profiled runs get it from here
+export GPU_MAX_HW_QUEUES=8
 
 run() {  # run NAME LIMIT CMD...; returns 0 on success or ordinary failure (1), else aborts
   local name=$1 lim=$2
@@ -28,7 +32,11 @@ run() {  # run NAME LIMIT CMD...; returns 0 on success or ordinary failure (1), 
 for s in $STEPS; do
   case $s in
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    smoke) run smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ;;
+    configs) for c in 3 4 5; do run bench_config$c 400 python bench.py --config $c --no-cpu-baseline --steps 10 --warmup 3; done ;;
+    sharded) run bench_sharded 300 python bench.py --no-cpu-baseline --force-sharded
+             run bench_sharded_rs 300 python bench.py --no-cpu-baseline --force-sharded --comm reduce_scatter ;;
     prof) run rocprof_stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
             python bench.py --no-cpu-baseline ;;
     gemm) run gemm_bench 300 python tools/gemm_bench.py crosscoder-model-diff-replication_amd/libcrosscoder_hip.so ;;
