@@ -3,7 +3,7 @@
 # bench command, and the GEMM / Adam A/B timers.  Every GPU step has its own time limit; the script
 # stops at the first fault, abort, segfault or timeout (test FAILURES -- exit 1 -- do not stop it).
 # Usage (repo root on the box): tools/gpu_round.sh [OUT] [steps...]
-#   steps: test smoke bench prof configs sharded gemm ab stepab small adam pmc
+#   steps: test smoke bench prof configs sharded rehearse gemm ab stepab small adam pmc
 OUT=${1:-gpurun_out/round}
 shift
 STEPS=${*:-test bench prof gemm adam}
@@ -35,6 +35,8 @@ for s in $STEPS; do
     smoke) run smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ;;
     configs) for c in 3 4 5; do run bench_config$c 400 python bench.py --config $c --no-cpu-baseline --steps 10 --warmup 3; done ;;
+    rehearse) for n in 2 4; do CC_BENCH_ONE_DEVICE=1 run rehearse_n$n 400 python -m torch.distributed.run --nnodes=1 \
+                --nproc-per-node $n --master-addr 127.0.0.1 --master-port 2951$n bench.py --gpus $n --steps 5 --warmup 2; done ;;
     sharded) run bench_sharded 300 python bench.py --no-cpu-baseline --force-sharded
              run bench_sharded_rs 300 python bench.py --no-cpu-baseline --force-sharded --comm reduce_scatter ;;
     prof) run rocprof_stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
