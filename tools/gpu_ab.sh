@@ -2,7 +2,7 @@
 # One GPU-box session for a change under test: GPU tests, a same-box step A/B of exp_head/ (a build of the last
 # commit, tools/snapshot_head.sh) vs this tree, and the GEMM timers.  Each GPU step has its own limit; the
 # script stops at the first fault / abort / timeout (an ordinary test failure, rc 1, does not stop it).
-#   tools/gpu_ab.sh OUT [steps...]   steps: test testk(TESTK=expr) ab ab3 sab3 shab gslice lossb qmap gemm gemmdbg bench sprof sproft sbench host probe prof
+#   tools/gpu_ab.sh OUT [steps...]   steps: test testk(TESTK=expr) ab ab3 sab3 shab gslice lossb trp qmap gemm gemmdbg bench sprof sproft sbench host probe prof
 OUT=${1:-gpurun_out/ab}
 shift
 STEPS=${*:-test ab}
@@ -27,6 +27,7 @@ for s in $STEPS; do
     sab3) AB_ARGS=--force-sharded run step_sab3 900 bash tools/ab_multi.sh 4 "$OUT/strees3" exp_head exp_b . ;;
     gslice) run gslice 300 bash -c "for b in 4096 2048 1024; do CC_GEMM_B=\$b CC_GEMM_ONLY=G1_encode_T,G2_decode_ws_T,G3_dacts_T python tools/gemm_bench.py crosscoder-model-diff-replication_amd/libcrosscoder_hip.so || exit 1; done" ;;
     shab) run shard_ab 900 bash tools/shard_ab.sh 3 "$OUT/shab" exp_head . ;;
+    trp) run trp 300 python tools/transpose_probe.py crosscoder-model-diff-replication_amd/libcrosscoder_hip.so $(ls crosscoder-model-diff-replication_amd/exp/*.so) ;;
     lossb) run lossb 300 python tools/loss_bench.py $(ls crosscoder-model-diff-replication_amd/exp/*.so) crosscoder-model-diff-replication_amd/libcrosscoder_hip.so ;;
     qmap) for q in 4 8; do for c in 1 2; do
             GPU_MAX_HW_QUEUES=$q run qmap_q${q}_c${c} 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/qmap_q${q}_c${c}" -o run -- \
