@@ -9,9 +9,15 @@ Workloads are BASELINE.json's configs (synthetic normalised activations, referen
   config 4  2x3584->65536, batch 8192                       config 5  4x2304->32768, batch 4096
 (--batch / --n-models / --d-model / --dict-size override single fields).  N > 1 (torchrun, one rank per
 GPU): the FIXED dictionary of the config is split into N latent slices (strong scaling) with an RCCL
-all-reduce of the fp32 partial reconstructions; every rank processes the same batch.  `value` is the
-real number of activations (batch rows) trained per second by the whole job; `latent_acts_per_s`
-(= value x dict_size) is the work-normalised throughput that is comparable across configs and N.
+all-reduce of the fp32 partial reconstructions; every rank processes the same batch.
+
+`value` is in the metric's own unit, activations of the 2x2304->16384 crosscoder trained per second: a batch
+row of a workload with n models of width d and h latents is 10.n.d.h FLOP of step work, i.e.
+(n.d.h) / (2.2304.16384) metric activations.  At N = 1 on config 2 (the driver's N = 1 run) that factor is 1
+and `value` = batch rows / s; a config-3 row (2^17 latents) counts 8.  So the driver's per-N values compare
+like for like (config 2 at N = 1, config 3 split over N > 1), and value_N / (N . value_1) is the scaling
+efficiency.  `rows_per_s` is the raw batch rows trained per second by the whole job, `latent_acts_per_s`
+= rows_per_s x dict_size.
 
 The JSON line also carries `roofline` (dominant kernel's achieved TFLOP/s from HIP events around its
 launches inside the timed region, vs the bf16 dense MFMA peak), `hbm` (achieved GB/s of the
@@ -123,8 +129,10 @@ def n1_same_workload(B, n, d, h):
         c = r.get("config", {})
         if r.get("n_gpus") == 1 and (c.get("global_batch"), c.get("n_models"), c.get("d_model"),
                                        c.get("dict_size")) == (B, n, d, h):
-            return {"value": r["value"], "ms_per_step": r["ms_per_step"], "unit": r["unit"],
-                    "source": os.path.relpath(files[-1], ROOT)}
+            # (value in this bench's unit, from the line's own step time: older lines carried raw rows / s)
+            per_row = (n * d * h) / (2 * 2304 * 16384)
+            return {"value": round(B / (r["ms_per_step"] * 1e-3) * per_row, 1), "ms_per_step": r["ms_per_step"],
+                    "rows_per_s": round(B / (r["ms_per_step"] * 1e-3), 1), "source": os.path.relpath(files[-1], ROOT)}
     return None
 
 
@@ -304,7 +312,11 @@ def main():
 
     step_s = elapsed / args.steps
     ms = step_s * 1e3
-    value = B / step_s  # activations (batch rows) trained per second by the whole job
+    rows_per_s = B / step_s  # batch rows trained per second by the whole job
+    # metric activations (2x2304->16384 crosscoder rows) per row of this workload: step work is 10.n.d.h FLOP
+    # per row, so config 2 counts 1 and config 3 (2^17 latents) 8
+    per_row = (n * d * h_total) / (2 * 2304 * 16384)
+    value = rows_per_s * per_row
     dom_ms = timer.averages_ms()[dom]
     gemm_flop = 2.0 * B * K * h_local  # per GEMM (per rank)
     # G4G5_wgrad is one launch computing both weight gradients (cc_wgrad_both)
@@ -325,7 +337,7 @@ def main():
     result = {
         "metric": "activations/sec per train step (fwd+bwd+Adam), 2x2304->16384; % bf16 MFMA peak",
         "value": round(value, 1),
-        "unit": "activations/s",
+        "unit": "activations/s" if per_row == 1 else "activations/s (2x2304->16384-equivalent)",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -342,7 +354,9 @@ def main():
                    "baseline_config": None if custom else config,
                    "global_batch": B, "n_models": n, "d_model": d, "dict_size": h_total,
                    "parallelism": f"latent{world}"},
-        "latent_acts_per_s": round(value * h_total, 1),
+        "rows_per_s": round(rows_per_s, 1),
+        "metric_activations_per_row": per_row,
+        "latent_acts_per_s": round(rows_per_s * h_total, 1),
         # N > 1: the same workload on one GPU (committed measurement), so the strong-scaling curve has its
         # own 1-GPU point (the driver's N = 1 run is the metric's config 2, a different dictionary)
         "n1_same_workload": n1_same_workload(B, n, d, h_total) if world > 1 else None,
