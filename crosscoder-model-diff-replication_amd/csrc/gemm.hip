@@ -647,13 +647,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmAr
 //   pp_fast     the whole-tile ReLU epilogue form of G1 / G3 (same bits as the general form)
 //   dec_one     G2's main tiles and split-K units as one launch (0: two launches, same bits)
 #ifdef CC_DEBUG_HOOKS
-static int g_pp_mask = 5, g_pp_fast = 1, g_dec_one_launch = 1;
+static int g_pp_mask = 7, g_pp_fast = 1, g_dec_one_launch = 1;
 #define CC_DEBUG_API extern "C" __attribute__((visibility("default")))
 CC_DEBUG_API void cc_debug_set_pp_mask(int mask) { g_pp_mask = mask; }
 CC_DEBUG_API void cc_debug_set_pp_fast(int on) { g_pp_fast = on; }
 CC_DEBUG_API void cc_debug_set_dec_one_launch(int on) { g_dec_one_launch = on; }
 #else
-constexpr int g_pp_mask = 5, g_pp_fast = 1, g_dec_one_launch = 1;
+constexpr int g_pp_mask = 7, g_pp_fast = 1, g_dec_one_launch = 1;
 #endif
 // N = n*d multiple of 288 (and an MN-contiguous bf16 B operand): 256 x 288 tiles.  (The fp32
 // parity mode keeps 256 x 256: its 288-wide variant exceeds 256 VGPRs.)
@@ -1058,7 +1058,7 @@ __global__ __launch_bounds__(LSPLIT_THREADS) void loss_split_kernel(const LossSp
   }
   // g_recon^T: column cblk + cc gets rows [r0, r0 + 128) as 16 chunks of 16 B (one per thread)
   const int cc = threadIdx.x >> 4, ch = threadIdx.x & 15;
-  if (r0 + ch * 8 < a.B)
+  if (a.g_t && r0 + ch * 8 < a.B)
     *(u32x4*)(a.g_t + (int64_t)(cblk + cc) * a.B + r0 + ch * 8) = *(const u32x4*)(tt + cc * TP + ch * 8);
 }
 
@@ -1073,32 +1073,36 @@ int64_t cc_decode_loss_ncb(int64_t B, int64_t h, int64_t n, int64_t d, int dtype
   return d / 64;
 }
 
-int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, const void* x, const float* x_mean,
-                     float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
-                     int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
-  if (!acts || !W_dec_t || !b_dec || !x || !x_mean || !g_recon || !g_recon_t || !row_part || !col_part)
-    return CC_ERR_NULL;
-  if (!cc_decode_loss_ncb(B, h, n, d, dtype)) return CC_ERR_SHAPE;
+}  // extern "C"
+
+// BKC: W_dec given transposed (W_dec_t [K][h], KC/KC); otherwise W_dec [h][K] itself (KC/MN)
+template <bool BKC>
+static int decode_loss(const void* acts, const void* W_dec, const void* b_dec, const void* x, const float* x_mean,
+                       float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
+                       int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, hipStream_t st) {
+  if (!acts || !W_dec || !b_dec || !x || !x_mean || !g_recon || !row_part || !col_part) return CC_ERR_NULL;
+  if (BKC && !g_recon_t) return CC_ERR_NULL;
+  if (!cc_decode_loss_ncb(B, h, n, d, dtype) || !use_pp(n * d, true, BKC, dtype)) return CC_ERR_SHAPE;
   if (!al16(x) || !al16(g_recon) || !al16(g_recon_t) || !al16(x_mean) || !al16(b_dec)) return CC_ERR_ALIGN;
   const int64_t K = n * d;
-  hipStream_t st = (hipStream_t)stream;
+  const int64_t ldb = BKC ? h : K;
   DecPlan p;
   const bool split = dec_plan(B, h, K, dtype, p);
   GemmArgs a = {};
-  a.A = acts; a.lda = h; a.B = W_dec_t; a.ldb = h;
+  a.A = acts; a.lda = h; a.B = W_dec; a.ldb = ldb;
   a.M = (int)B; a.N = split ? p.nbn_main * 256 : (int)K; a.K = (int)h;
   a.out = g_recon; a.ldo = K; a.out_t = g_recon_t; a.ldt = B;
   a.mask_src = x; a.bias = b_dec; a.tn = x_mean; a.scale0 = grad_scale;
   a.col_part = col_part; a.row_part = row_part; a.d_model = (int)d; a.n_models = (int)n;
-  int rc = check_gemm(a, dtype, true, true);
+  int rc = check_gemm(a, dtype, true, BKC);
   if (rc) return rc;
   a.nbm = (a.M + BM - 1) / BM;
   a.nbn = (a.N + 255) / 256;
   const bool fast = B % BM == 0 && a.N % 256 == 0;
   if (!split) {
     const dim3 grid(pp_grid(a.nbm * a.nbn));
-    if (fast) hipLaunchKernelGGL((gemm_pp_kernel<true, true, EPI_DLOSS, true>), grid, dim3(NTHR), 0, st, a);
-    else hipLaunchKernelGGL((gemm_pp_kernel<true, true, EPI_DLOSS>), grid, dim3(NTHR), 0, st, a);
+    if (fast) hipLaunchKernelGGL((gemm_pp_kernel<true, BKC, EPI_DLOSS, true>), grid, dim3(NTHR), 0, st, a);
+    else hipLaunchKernelGGL((gemm_pp_kernel<true, BKC, EPI_DLOSS>), grid, dim3(NTHR), 0, st, a);
     CC_LAUNCH_CHECK();
     return CC_OK;
   }
@@ -1107,15 +1111,15 @@ int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, c
   if (ws_floats < (int64_t)p.nsplit * split_stride) return CC_ERR_SHAPE;
   if (!al16(ws)) return CC_ERR_ALIGN;
   GemmArgs t = {};
-  t.A = acts; t.lda = h; t.B = (const bf16_t*)W_dec_t + (int64_t)p.nbn_main * 256 * h; t.ldb = h;
+  t.A = acts; t.lda = h; t.B = (const bf16_t*)W_dec + (int64_t)p.nbn_main * 256 * (BKC ? h : 1); t.ldb = ldb;
   t.M = (int)B; t.N = p.tail_cols; t.K = (int)h;
   t.out = ws; t.ldo = p.tail_cols;
   t.nbm = (t.M + BM - 1) / BM;
   t.nbn = (t.N + 255) / 256;
   const dim3 grid(a.nbm * a.nbn + p.nsplit * t.nbm * t.nbn);
-  if (fast) hipLaunchKernelGGL((gemm_pp_main_splitk_kernel<true, true, EPI_DLOSS, true>), grid, dim3(NTHR), 0, st, a, t,
+  if (fast) hipLaunchKernelGGL((gemm_pp_main_splitk_kernel<true, BKC, EPI_DLOSS, true>), grid, dim3(NTHR), 0, st, a, t,
                                p.steps_per, p.nk, split_stride);
-  else hipLaunchKernelGGL((gemm_pp_main_splitk_kernel<true, true, EPI_DLOSS>), grid, dim3(NTHR), 0, st, a, t,
+  else hipLaunchKernelGGL((gemm_pp_main_splitk_kernel<true, BKC, EPI_DLOSS>), grid, dim3(NTHR), 0, st, a, t,
                           p.steps_per, p.nk, split_stride);
   CC_LAUNCH_CHECK();
   LossSplitArgs l = {};
@@ -1129,6 +1133,22 @@ int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, c
                      dim3(LSPLIT_THREADS), 0, st, l);
   CC_LAUNCH_CHECK();
   return CC_OK;
+}
+
+extern "C" {
+
+int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, const void* x, const float* x_mean,
+                     float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
+                     int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
+  return decode_loss<true>(acts, W_dec_t, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t, row_part, col_part, ws,
+                           ws_floats, B, h, n, d, dtype, (hipStream_t)stream);
+}
+
+int cc_decode_loss(const void* acts, const void* W_dec, const void* b_dec, const void* x, const float* x_mean,
+                   float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
+                   int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
+  return decode_loss<false>(acts, W_dec, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t, row_part, col_part, ws,
+                            ws_floats, B, h, n, d, dtype, (hipStream_t)stream);
 }
 
 int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,

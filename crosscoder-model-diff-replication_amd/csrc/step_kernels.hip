@@ -368,6 +368,11 @@ struct AdamArgs {
   int clip_np, clip_emulate;
   float clip_max_norm;
   float* clip_out;
+  // decoder norms' per-(row, 64-column block) squared sums of the UPDATED parameters over the first
+  // norm_rows x norm_ld elements (W_dec [h][K]), in cc_dec_norms' order, into norm_part[row][K / 64]
+  // (adam_kernel only; nullptr: none)
+  float* norm_part;
+  int norm_rows, norm_ld;
 };
 // The step's clip coefficient: read (coef), formed from squared sums (clip_sums), or 1
 CC_DEV float adam_coef(const AdamArgs& a) {
@@ -492,6 +497,18 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
       den = E::round(den + a.eps);
       float pj = E::round(p[j] + a.neg_step * (mj / den));
       p[j] = pj; m[j] = mj; v[j] = vj;
+    }
+    if (a.norm_part && i < (int64_t)a.norm_rows * a.norm_ld) {
+      // the 8 lanes of an aligned group hold one 64-column block of a row (i % 64 == 8 * (lane & 7): the
+      // grid stride is a multiple of 64, K % 64 == 0), all of them inside the matrix together
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q = __fmaf_rn(p[j], p[j], q);
+      q = block8_sum(q);
+      if ((threadIdx.x & 7) == 0) {
+        const int row = (int)(i / a.norm_ld);
+        a.norm_part[(int64_t)row * (a.norm_ld >> 6) + ((int)(i - (int64_t)row * a.norm_ld) >> 6)] = q;
+      }
     }
     if (full) {
       store8_nt<DT>(a.p, i, p);
@@ -850,6 +867,29 @@ int cc_adam_step_clip(void* p, const void* g, void* m, void* v, int64_t numel, c
   a.clip_max_norm = max_norm;
   a.clip_out = clip_out;
   return adam_launch(a, max_blocks, dtype, (hipStream_t)stream);
+}
+
+int cc_adam_dec_norms(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, const float* sums,
+                      int nparams, float max_norm, int emulate_bf16, double lr, double beta1, double beta2,
+                      double eps, int64_t step, int64_t max_blocks, float* norm_part, int64_t h, int64_t K, int dtype,
+                      void* stream) {
+  if (!p || !g || !m || !v || !norm_part || (!coef && !sums)) return CC_ERR_NULL;
+  if (numel <= 0 || step <= 0 || h <= 0 || K <= 0 || K % 64 || h * K > numel || h * K >= ((int64_t)1 << 31))
+    return CC_ERR_SHAPE;
+  if (sums && (nparams <= 0 || nparams > 6)) return CC_ERR_SHAPE;
+  if (!al16(p) || !al16(g) || !al16(m) || !al16(v) || !al16(norm_part)) return CC_ERR_ALIGN;
+  AdamArgs a = adam_args(p, g, m, v, numel, sums ? nullptr : coef, lr, beta1, beta2, eps, step);
+  if (sums) {
+    a.clip_sums = sums;
+    a.clip_np = nparams;
+    a.clip_emulate = emulate_bf16;
+    a.clip_max_norm = max_norm;
+  }
+  a.norm_part = norm_part;
+  a.norm_rows = (int)h;
+  a.norm_ld = (int)K;
+  // (the grid-stride form: the bulk kernel does not form the partials)
+  return adam_launch(a, max_blocks > 0 ? max_blocks : 1024, dtype, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -135,10 +135,17 @@ class StepWorkspace:
         self.norms = E(h, n)
         self.tn = E(h)
         self.acts = E(B, h, dt=dtype)
-        # W_dec^T [K][h]: G2 then reads both operands h-contiguous (refreshed with the decoder norms)
-        self.W_dec_t = E(K, h, dt=dtype) if self.tr else None
+        # G2 + loss in one pass (decode_loss) when it serves the shape: its row terms come per 64-column
+        # block and its b_dec-gradient partials per 128-row group; one storage holds either layout
+        self.fused_ncb = ops.decode_loss_ncb(B, h, n, d, dtype) if self.tr else 0
+        # the fused G2 reads W_dec [h][K] itself (transposed LDS reads); elsewhere in the transposed mode G2 reads
+        # W_dec^T [K][h] (both operands h-contiguous), refreshed with the decoder norms after Adam
+        self.W_dec_t = E(K, h, dt=dtype) if self.tr and not self.fused_ncb else None
         npart = ops.dec_norms_part_floats(h, n, d) if self.tr else 0
-        self.norm_part = E(npart) if npart else None  # fused W_dec^T + norms pass (d % 64 == 0)
+        # per-(row, 64-column block) squared sums of W_dec (d % 64 == 0): written by the decoder-half Adam
+        # (cc_adam_dec_norms) or by the fused W_dec^T + norms pass
+        self.norm_part = E(npart) if npart else None
+        self.norms_event = None  # the side stream's decoder-norms launch the next main-stream reader waits for
         self.acts_t = E(h, B, dt=dtype) if self.tr else None
         # G1's activation mask as bits in the GEMM accumulator order: G3 reads 16 B per thread and tile instead
         # of the 128 KB acts tile (1/16 of the bytes, no LDS staging)
@@ -160,9 +167,6 @@ class StepWorkspace:
         self.g_recon = E(B, K, dt=dtype)
         self.g_recon_t = E(K, B, dt=dtype) if self.tr else None
         self.ncb = ops.loss_col_blocks(d)
-        # G2 + loss in one pass (decode_loss_t) when it serves the shape: its row terms come per 64-column
-        # block and its b_dec-gradient partials per 128-row group; one storage holds either layout
-        self.fused_ncb = ops.decode_loss_ncb(B, h, n, d, dtype) if self.tr else 0
         rp = E(2 * n * max(self.ncb, self.fused_ncb) * B)
         self.row_part = rp[:2 * n * self.ncb * B].view(2, n * self.ncb, B)  # loss_fwd_bwd's layout
         self.row_part_fused = rp[:2 * n * self.fused_ncb * B].view(2, n * self.fused_ncb, B) if self.fused_ncb \
@@ -228,13 +232,21 @@ def norms_for_next(ws, P):
 
 
 def _decoder_derived(ws, P):
-    if ws.norm_part is not None:  # W_dec^T and the norms from one pass over W_dec
+    if ws.W_dec_t is not None and ws.norm_part is not None:  # W_dec^T and the norms from one pass over W_dec
         with _span("dec_norms_T"):
             ops.transpose_dec_norms(P.W_dec_hk, ws.n, ws.d, ws.W_dec_t, ws.norm_part, ws.norms, ws.tn, ws.inv_norms)
         return
-    if ws.tr:
+    if ws.W_dec_t is not None:
         ops.transpose(P.W_dec_hk, out=ws.W_dec_t)
     ops.dec_norms(P.W_dec_hk, ws.h, ws.n, ws.d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
+
+
+def wait_norms(ws):
+    """Order torch's stream after the decoder norms the side stream formed beside the decoder-half Adam (a
+    completed event by the time G2 has run: no stall)."""
+    if ws.norms_event is not None:
+        torch.cuda.current_stream(ws.x.device).wait_event(ws.norms_event)
+        ws.norms_event = None
 
 
 def decoder_norms(ws, P):
@@ -274,15 +286,17 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     decoder_norms(ws, P)  # (+ W_dec^T), unless launched already after the last Adam
     if loss and ws.fused_ncb:
         decode_loss(ws, P, grad_scale)
+        wait_norms(ws)
         ws.acts_pending = True
         if finalize:
             loss_finalize(ws)
         return
     with _span("G2_decode"):
-        if ws.tr:
+        if ws.W_dec_t is not None:
             ops.decode_partial_t(ws.acts, ws.W_dec_t, ws.recon, ws.dec_ws)
         else:
             ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
+    wait_norms(ws)
     # B * l1 = sum_h colsum_acts[h] * tn[h] (crosscoder.py:126) rides in the loss finaliser's launch
     # (loss_tail)
     ws.acts_pending = True
@@ -293,11 +307,12 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
 
 
 def decode_loss(ws, P, grad_scale=None):
-    """G2 + loss rows + g_recon (and g_recon^T) in one pass over the whole batch (decode_loss_t)."""
+    """G2 + loss rows + g_recon (and g_recon^T) in one pass over the whole batch (decode_loss: W_dec read
+    directly)."""
     gs = 2.0 / ws.B if grad_scale is None else grad_scale
     with _span("G2_decode"):
-        ops.decode_loss_t(ws.acts, ws.W_dec_t, P.b_dec_flat, ws.x, ws.x_mean, gs, ws.g_recon, ws.g_recon_t,
-                          ws.row_part_fused, ws.loss_colpart, ws.dec_ws, ws.n, ws.d)
+        ops.decode_loss(ws.acts, P.W_dec_hk, P.b_dec_flat, ws.x, ws.x_mean, gs, ws.g_recon, ws.g_recon_t,
+                        ws.row_part_fused, ws.loss_colpart, ws.dec_ws, ws.n, ws.d)
     ws.row_ncb = ws.fused_ncb
     ws.loss_col_rows = ops.col_part_rows(ws.B)
 
@@ -482,9 +497,24 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
     enc_done.record(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side_stream):
         side_stream.wait_event(enc_done)
-        with _span("adam_dec"):
-            step_(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), max_blocks=DEC_ADAM_BLOCKS)
-        norms_for_next(ws, P)
-        done = torch.cuda.Event()
-        done.record(side_stream)
+        if ws.W_dec_t is None and ws.norm_part is not None:
+            # the decoder norms' partials come out of the Adam launch itself (no pass over W_dec of their own);
+            # G2 waits only for the updated W_dec, the finaliser runs beside it
+            with _span("adam_dec"):
+                ops.adam_dec_norms(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), ws.h, ws.K, lr, beta1,
+                                   beta2, eps, step, ws.norm_part, coef=coef if clip_sums is None else None,
+                                   clip_sums=clip_sums, emulate=emulate, max_blocks=DEC_ADAM_BLOCKS)
+            done = torch.cuda.Event()
+            done.record(side_stream)
+            with _span("dec_norms"):
+                ops.dec_norms_finalize(ws.norm_part, ws.h, ws.n, ws.d, ws.norms, ws.tn, ws.inv_norms)
+            ws.norms_token = _norms_token(P)
+            ws.norms_event = torch.cuda.Event()
+            ws.norms_event.record(side_stream)
+        else:
+            with _span("adam_dec"):
+                step_(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), max_blocks=DEC_ADAM_BLOCKS)
+            norms_for_next(ws, P)
+            done = torch.cuda.Event()
+            done.record(side_stream)
     P.pending = done

@@ -197,6 +197,15 @@ def decode_loss_t(acts, W_dec_t, b_dec, x, x_mean, grad_scale, g_recon, g_recon_
                                  0 if ws is None else ws.numel(), B, h, n, d, dtype_code(acts.dtype), _stream(acts)))
 
 
+def decode_loss(acts, W_dec_hk, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t, row_part, col_part, ws, n, d):
+    """decode_loss_t reading W_dec [h, K] itself (cc_decode_loss, transposed LDS reads of the B operand): the same
+    bits without the W_dec^T copy.  g_recon_t may be None."""
+    B, h = acts.shape
+    check(lib().cc_decode_loss(_ptr(acts), _ptr(W_dec_hk), _ptr(b_dec), _ptr(x), _ptr(x_mean), grad_scale,
+                               _ptr(g_recon), _ptr(g_recon_t), _ptr(row_part), _ptr(col_part), _ptr(ws),
+                               0 if ws is None else ws.numel(), B, h, n, d, dtype_code(acts.dtype), _stream(acts)))
+
+
 def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_scale, B, n, d, row0=0, rows=None,
                  g_recon_t=None):
     """Loss terms + g_recon for batch rows [row0, row0 + rows) (default: all B rows);
@@ -332,6 +341,17 @@ def transpose_dec_norms(W_dec_hk, n, d, W_dec_t, part, norms, total, inv_norms=N
 def dec_norms_finalize(part, h, n, d, norms, total, inv_norms=None):
     check(lib().cc_dec_norms_finalize(_ptr(part), h, n, d, _ptr(norms), _ptr(total), _ptr(inv_norms),
                                       _stream(part)))
+
+
+def adam_dec_norms(p, g, m, v, h, K, lr, beta1, beta2, eps, step, part, coef=None, clip_sums=None, emulate=True,
+                   max_blocks=0):
+    """Adam over the decoder half p/g/m/v (flat views, W_dec [h, K] first) that also writes the decoder-norm
+    partials of the updated W_dec into `part` (cc_adam_dec_norms; dec_norms_finalize completes them).
+    coef: the clip coefficient tensor; or clip_sums = (sums, max_norm): formed in the kernel."""
+    sums, max_norm = clip_sums if clip_sums is not None else (None, 0.0)
+    check(lib().cc_adam_dec_norms(_ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(coef), _ptr(sums),
+                                  0 if sums is None else sums.numel(), float(max_norm), int(emulate), lr, beta1, beta2,
+                                  eps, int(step), int(max_blocks), _ptr(part), h, K, dtype_code(p.dtype), _stream(p)))
 
 
 def adam_dec_transposed(p, g, m, v, coef, lr, beta1, beta2, eps, step, W_dec_t, part, max_blocks=0):

@@ -173,6 +173,11 @@ int64_t cc_decode_loss_ncb(int64_t B, int64_t h, int64_t n, int64_t d, int dtype
 int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, const void* x, const float* x_mean,
                      float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
                      int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream);
+/* cc_decode_loss_t reading W_dec [h][K] itself (the parameter, no transposed copy; same bits): the GEMM's B
+ * operand goes through transposed LDS reads.  g_recon_t may be NULL here (not written then). */
+int cc_decode_loss(const void* acts, const void* W_dec, const void* b_dec, const void* x, const float* x_mean,
+                   float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
+                   int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream);
 
 /* Loss reduction (crosscoder.py:106-128, trainer.py:51-61): per-row explained variances
  * ev/ev_a/ev_b [B] (fp32) and scalars[0:8] = {l2, l1, l0, mean ev, mean ev_a, mean ev_b, 0, 0};
@@ -354,6 +359,17 @@ int cc_dec_norms_finalize(const float* part, int64_t h, int64_t n, int64_t d, fl
  * bits as cc_adam_step), in 64 x 64 tiles that also write W_dec_t = the updated W_dec^T and `part`
  * (cc_dec_norms_part_floats floats) for cc_dec_norms_finalize: the next step's decoder norms and G2
  * operand from the same HBM pass.  bf16, K % 64 == 0, h % 8 == 0; max_blocks caps the grid. */
+/* The decoder half of Adam (trainer.py:47 over W_dec and b_dec: p/g/m/v point at the decoder half of each
+ * arena, numel elements, W_dec [h][K] first; same bits as cc_adam_step / cc_adam_step_clip) that also writes
+ * `part` (cc_dec_norms_part_floats(h, n, d) floats) from the updated W_dec for cc_dec_norms_finalize: the next
+ * step's decoder norms (crosscoder.py:123-125, same bits as cc_dec_norms) without another pass over W_dec.
+ * The clip coefficient comes from `coef`, or (sums != NULL) is formed from the per-parameter squared sums as
+ * in cc_adam_step_clip.  K % 64 == 0; max_blocks caps the grid (0: 1024). */
+int cc_adam_dec_norms(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, const float* sums,
+                      int nparams, float max_norm, int emulate_bf16, double lr, double beta1, double beta2,
+                      double eps, int64_t step, int64_t max_blocks, float* part, int64_t h, int64_t K, int dtype,
+                      void* stream);
+
 int cc_adam_dec_transposed(void* p, const void* g, void* m, void* v, int64_t h, int64_t K, const float* coef,
                            double lr, double beta1, double beta2, double eps, int64_t step, int64_t max_blocks,
                            void* W_dec_t, float* part, int dtype, void* stream);
