@@ -145,7 +145,6 @@ class StepWorkspace:
         # per-(row, 64-column block) squared sums of W_dec (d % 64 == 0): written by the decoder-half Adam
         # (cc_adam_dec_norms) or by the fused W_dec^T + norms pass
         self.norm_part = E(npart) if npart else None
-        self.norms_event = None  # the side stream's decoder-norms launch the next main-stream reader waits for
         self.acts_t = E(h, B, dt=dtype) if self.tr else None
         # G1's activation mask as bits in the GEMM accumulator order: G3 reads 16 B per thread and tile instead
         # of the 128 KB acts tile (1/16 of the bytes, no LDS staging)
@@ -241,14 +240,6 @@ def _decoder_derived(ws, P):
     ops.dec_norms(P.W_dec_hk, ws.h, ws.n, ws.d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
 
 
-def wait_norms(ws):
-    """Order torch's stream after the decoder norms the side stream formed beside the decoder-half Adam (a
-    completed event by the time G2 has run: no stall)."""
-    if ws.norms_event is not None:
-        torch.cuda.current_stream(ws.x.device).wait_event(ws.norms_event)
-        ws.norms_event = None
-
-
 def decoder_norms(ws, P):
     """||W_dec[h, m]||, their sum over m and inverses (crosscoder.py:123-125), unless still fresh."""
     if getattr(ws, "norms_token", None) == _norms_token(P):
@@ -286,7 +277,6 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     decoder_norms(ws, P)  # (+ W_dec^T), unless launched already after the last Adam
     if loss and ws.fused_ncb:
         decode_loss(ws, P, grad_scale)
-        wait_norms(ws)
         ws.acts_pending = True
         if finalize:
             loss_finalize(ws)
@@ -296,7 +286,6 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
             ops.decode_partial_t(ws.acts, ws.W_dec_t, ws.recon, ws.dec_ws)
         else:
             ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
-    wait_norms(ws)
     # B * l1 = sum_h colsum_acts[h] * tn[h] (crosscoder.py:126) rides in the loss finaliser's launch
     # (loss_tail)
     ws.acts_pending = True
@@ -499,18 +488,17 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
         side_stream.wait_event(enc_done)
         if ws.W_dec_t is None and ws.norm_part is not None:
             # the decoder norms' partials come out of the Adam launch itself (no pass over W_dec of their own);
-            # G2 waits only for the updated W_dec, the finaliser runs beside it
+            # the main stream's one wait before G2 covers the updated W_dec and the norms (the finaliser takes
+            # ~6 us; a second cross-stream wait for it later cost the main stream ~5 us)
             with _span("adam_dec"):
                 ops.adam_dec_norms(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), ws.h, ws.K, lr, beta1,
                                    beta2, eps, step, ws.norm_part, coef=coef if clip_sums is None else None,
                                    clip_sums=clip_sums, emulate=emulate, max_blocks=DEC_ADAM_BLOCKS)
-            done = torch.cuda.Event()
-            done.record(side_stream)
             with _span("dec_norms"):
                 ops.dec_norms_finalize(ws.norm_part, ws.h, ws.n, ws.d, ws.norms, ws.tn, ws.inv_norms)
             ws.norms_token = _norms_token(P)
-            ws.norms_event = torch.cuda.Event()
-            ws.norms_event.record(side_stream)
+            done = torch.cuda.Event()
+            done.record(side_stream)
         else:
             with _span("adam_dec"):
                 step_(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), max_blocks=DEC_ADAM_BLOCKS)

@@ -807,6 +807,78 @@ def test_tiled_decoder_adam_matches_flat(gpu, h, max_blocks):
     assert torch.equal(nm1, nm2) and torch.equal(tn1, tn2) and torch.equal(inv1, inv2)
 
 
+@pytest.mark.parametrize("h", [2048, 200])
+@pytest.mark.parametrize("max_blocks", [0, 256])
+@pytest.mark.parametrize("clip", ["coef", "sums"])
+def test_decoder_adam_norms_matches_flat(gpu, h, max_blocks, clip):
+    """cc_adam_dec_norms (the decoder-half Adam that also writes the decoder-norm partials of the updated
+    W_dec) == cc_adam_step / cc_adam_step_clip over the same half [W_dec | b_dec] bit for bit, and
+    cc_dec_norms_finalize of its partials gives cc_dec_norms' bits on the updated W_dec."""
+    n, d = 2, 256
+    K = n * d
+    numel = h * K + K
+    g = torch.Generator().manual_seed(h + max_blocks + len(clip))
+    bf = torch.bfloat16
+    mk = lambda sc: (torch.randn(numel, generator=g) * sc).to(bf).to(gpu)  # noqa: E731
+    p0, gr, m0, v0 = mk(0.05), mk(1e-3), mk(1e-4), (torch.rand(numel, generator=g) * 1e-6).to(bf).to(gpu)
+    coef = torch.tensor([0.7], device=gpu)
+    sums = torch.tensor([40.0, 3.0, 0.5, 0.25], device=gpu)
+    hyper = (5e-5, 0.9, 0.999, 1e-8, 3)
+    pf, mf, vf = p0.clone(), m0.clone(), v0.clone()
+    if clip == "coef":
+        ops.adam_step(pf, gr.clone(), mf, vf, coef, *hyper)
+    else:
+        ops.adam_step_clip(pf, gr.clone(), mf, vf, sums, 1.0, True, *hyper)
+    pt, mt, vt = p0.clone(), m0.clone(), v0.clone()
+    part = torch.full((ops.dec_norms_part_floats(h, n, d),), float("nan"), device=gpu)
+    ops.adam_dec_norms(pt, gr.clone(), mt, vt, h, K, *hyper, part, coef=coef if clip == "coef" else None,
+                       clip_sums=(sums, 1.0) if clip == "sums" else None, max_blocks=max_blocks)
+    E = lambda *s_: torch.empty(*s_, device=gpu)  # noqa: E731
+    nm1, tn1, inv1 = E(h, n), E(h), E(h, n)
+    ops.dec_norms_finalize(part, h, n, d, nm1, tn1, inv1)
+    nm2, tn2, inv2 = E(h, n), E(h), E(h, n)
+    ops.dec_norms(pf[:h * K].view(h, K), h, n, d, norms=nm2, total=tn2, inv_norms=inv2)
+    torch.cuda.synchronize()
+    assert torch.equal(pt, pf) and torch.equal(mt, mf) and torch.equal(vt, vf)
+    assert not bool(torch.isnan(part).any())
+    assert torch.equal(nm1, nm2) and torch.equal(tn1, tn2) and torch.equal(inv1, inv2)
+
+
+@pytest.mark.parametrize("B, n, d, h", [(4096, 2, 2304, 2048), (1024, 2, 256, 1024), (1000, 4, 128, 512),
+                                        (512, 2, 64, 200)])
+def test_decode_loss_on_wdec_matches_transposed(gpu, B, n, d, h):
+    """The fused G2 + loss reading W_dec [h][K] itself (cc_decode_loss, transposed LDS reads of the B operand)
+    == the same pass over W_dec^T (cc_decode_loss_t), bit for bit in every output: both loops accumulate each
+    output in the same k order."""
+    K = n * d
+    g = torch.Generator().manual_seed(B + h)
+    bf = torch.bfloat16
+    acts = torch.relu(torch.randn(B, h, generator=g)).to(bf).to(gpu)
+    W = (torch.randn(h, K, generator=g) * 0.05).to(bf).to(gpu)
+    b_dec = (torch.randn(K, generator=g) * 0.1).to(bf).to(gpu)
+    x = torch.randn(B, K, generator=g).to(bf).to(gpu)
+    x_mean = x.float().mean(0)
+    ncb = ops.decode_loss_ncb(B, h, n, d, bf)
+    assert ncb == d // 64
+    nws = max(ops.decode_ws_floats(B, h, K, bf), 1)
+    outs = []
+    for direct in (False, True):
+        g_recon = torch.full((B, K), float("nan"), dtype=bf, device=gpu)
+        g_t = torch.full((K, B), float("nan"), dtype=bf, device=gpu)
+        rp = torch.full((2, n * ncb, B), float("nan"), device=gpu)
+        cp = torch.full((ops.col_part_rows(B), K), float("nan"), device=gpu)
+        dws = torch.empty(nws, device=gpu)
+        if direct:
+            ops.decode_loss(acts, W, b_dec, x, x_mean, 2.0 / B, g_recon, g_t, rp, cp, dws, n, d)
+        else:
+            ops.decode_loss_t(acts, W.t().contiguous(), b_dec, x, x_mean, 2.0 / B, g_recon, g_t, rp, cp, dws, n, d)
+        outs.append((g_recon, g_t, rp, cp))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert not bool(torch.isnan(a.float()).any())
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("comm", ["all_reduce", "reduce_scatter"])
 def test_sharded_trainer_world1_matches_trainer(gpu, comm):
     """ShardedTrainer over a 1-rank RCCL group (the sliced async all-reduce path, 4 slices, or the
