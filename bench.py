@@ -91,7 +91,7 @@ class EventTimer:
 SPAN_EVERY = 4  # timed steps per roofline-kernel sample (events around the launch)
 
 # span name -> kernel-name prefix in the rocprofv3 traces
-SPAN_KERNEL = {"G1_encode": "gemm_pp_kernel<true, true, 1", "G2_decode": "gemm_pp_main_splitk_kernel<true, true, 7",
+SPAN_KERNEL = {"G1_encode": "gemm_pp_kernel<true, true, 1", "G2_decode": "gemm_pp_main_splitk_kernel<true, false, 7",
                "G3_dacts": "gemm_pp_kernel<true, true, 3", "G4G5_wgrad": "gemm_pp_dual_tail_kernel<true, true, 4, 5>",
                "adam": "adam_bulk_kernel"}
 
@@ -211,7 +211,8 @@ def hbm_rows(kern, B, n, d, h_local, es=2):
             out[k] = {"ms": round(kern[k], 4), "bytes": b, "GB_s": round(gbs, 1),
                       "frac": round(gbs / PEAK_HBM_GBS, 3)}
     if "adam_dec" in out:
-        out["adam_dec"]["note"] = "side stream, concurrent with the next step's prep / G1"
+        out["adam_dec"]["note"] = ("side stream, concurrent with the next step's prep / G1; also writes the decoder "
+                                   "norms' per-block partials of the updated W_dec")
     if "dec_norms_T" in out:
         out["dec_norms_T"]["note"] = "side stream, concurrent with G1"
     return out
