@@ -200,7 +200,9 @@ def hbm_rows(kern, B, n, d, h_local, es=2):
     enc = h_local * K + h_local  # encoder half of the arena (W_enc + b_enc)
     dec = h_local * K + K
     per = 7 * es  # Adam: p, g, m, v read + p, m, v written
-    byts = {"adam": enc * per, "adam_dec": dec * per,
+    # the decoder half: W_dec's first hs rows on the side stream beside G1, the rest + b_dec after G1
+    hs = min(h_local, int(h_local * engine.DEC_SIDE_ROWS) // 8 * 8)
+    byts = {"adam": enc * per, "adam_dec": hs * K * per, "adam_dec_rest": (dec - hs * K) * per,
             "prep": B * K * es + 2 * B * K * es,            # raw batch in; x and x^T out
             "loss": B * K * 4 + B * K * es + 2 * B * K * es,  # recon fp32 + x in; g_recon and g_recon^T out
             "dec_norms_T": 2 * h_local * K * es}             # W_dec in, W_dec^T out (+ norms)
@@ -211,8 +213,10 @@ def hbm_rows(kern, B, n, d, h_local, es=2):
             out[k] = {"ms": round(kern[k], 4), "bytes": b, "GB_s": round(gbs, 1),
                       "frac": round(gbs / PEAK_HBM_GBS, 3)}
     if "adam_dec" in out:
-        out["adam_dec"]["note"] = ("side stream, concurrent with the next step's prep / G1; also writes the decoder "
-                                   "norms' per-block partials of the updated W_dec")
+        out["adam_dec"]["note"] = ("W_dec's first rows, side stream, concurrent with the next step's prep / G1; "
+                                   "also writes the decoder norms' per-block partials of the updated W_dec")
+    if "adam_dec_rest" in out:
+        out["adam_dec_rest"]["note"] = "the decoder half's remaining rows + b_dec, main stream after G1"
     if "dec_norms_T" in out:
         out["dec_norms_T"]["note"] = "side stream, concurrent with G1"
     return out

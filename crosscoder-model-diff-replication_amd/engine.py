@@ -75,6 +75,8 @@ class Arena:
         o += h * K
         self.b_dec_flat = self.data[o:o + K]
         self.pending = None  # event the decoder half's Adam (side stream) records; see clip_and_adam
+        # the decoder half's last rows, launched by the first reader on its own stream (engine.adam)
+        self.pending_rest = None
 
     def enc_part(self):
         return self.data[:self.split]
@@ -83,7 +85,11 @@ class Arena:
         return self.data[self.split:]
 
     def wait_pending(self):
-        """Order torch's current stream after the decoder half's Adam if it ran on a side stream."""
+        """Order torch's current stream after the decoder half's Adam if it ran on a side stream (launching
+        its deferred last rows first, if any)."""
+        if self.pending_rest is not None:
+            rest, self.pending_rest = self.pending_rest, None
+            rest()
         if self.pending is not None:
             torch.cuda.current_stream(self.data.device).wait_event(self.pending)
             self.pending = None
@@ -441,9 +447,14 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
     ops.reduce_rows(loss_colpart(ws), ws.loss_col_rows, K, out_t=G.b_dec_flat, sq_part=ws.sq_slice(3))
 
 
-# workgroups of the decoder-half Adam that runs beside the next step's G1 (128 / 192 / 384 measured
-# slower, DESIGN.md section 8)
+# workgroups of the decoder-half Adam that runs beside the next step's G1 (128 / 192 / 384 / 512 measured
+# slower, DESIGN.md section 3)
 DEC_ADAM_BLOCKS = 256
+# share of W_dec's rows whose Adam update runs on the side stream beside the next step's G1; the rest (and
+# b_dec) runs on the main stream after G1 with the whole chip.  Beside G1 the
+# side launch gets one wave per SIMD (G1 holds the rest of the register file), which streams slowly once
+# G1 has finished.
+DEC_SIDE_ROWS = 0.92
 
 
 def clip_and_adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, max_norm=1.0, side_stream=None):
@@ -487,18 +498,35 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
     with torch.cuda.stream(side_stream):
         side_stream.wait_event(enc_done)
         if ws.W_dec_t is None and ws.norm_part is not None:
-            # the decoder norms' partials come out of the Adam launch itself (no pass over W_dec of their own);
-            # the main stream's one wait before G2 covers the updated W_dec and the norms (the finaliser takes
-            # ~6 us; a second cross-stream wait for it later cost the main stream ~5 us)
-            with _span("adam_dec"):
-                ops.adam_dec_norms(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), ws.h, ws.K, lr, beta1,
-                                   beta2, eps, step, ws.norm_part, coef=coef if clip_sums is None else None,
-                                   clip_sums=clip_sums, emulate=emulate, max_blocks=DEC_ADAM_BLOCKS)
-            with _span("dec_norms"):
-                ops.dec_norms_finalize(ws.norm_part, ws.h, ws.n, ws.d, ws.norms, ws.tn, ws.inv_norms)
-            ws.norms_token = _norms_token(P)
+            # the decoder norms' partials come out of the Adam launches themselves (no pass over W_dec of their
+            # own).  The side stream updates the first hs rows of W_dec beside the next step's G1; the first
+            # reader of the params (the next forward, after G1) launches the rest on its stream, waits for the
+            # side part and forms the norms (P.pending_rest)
+            K, nblk = ws.K, ws.K // 64
+            hs = min(ws.h, int(ws.h * DEC_SIDE_ROWS) // 8 * 8)
+            dec = [A.dec_part() for A in (P, G, M, V)]
+            kw = dict(coef=coef if clip_sums is None else None, clip_sums=clip_sums, emulate=emulate)
+            hp = (lr, beta1, beta2, eps, step)
+            if hs > 0:
+                with _span("adam_dec"):
+                    ops.adam_dec_norms(*(t[:hs * K] for t in dec), hs, K, *hp, ws.norm_part[:hs * nblk],
+                                       max_blocks=DEC_ADAM_BLOCKS, **kw)
             done = torch.cuda.Event()
             done.record(side_stream)
+
+            def rest():
+                cur = torch.cuda.current_stream(dev)
+                with _span("adam_dec_rest"):
+                    ops.adam_dec_norms(*(t[hs * K:] for t in dec), ws.h - hs, K, *hp, ws.norm_part[hs * nblk:],
+                                       **kw)
+                cur.wait_event(done)
+                with _span("dec_norms"):
+                    ops.dec_norms_finalize(ws.norm_part, ws.h, ws.n, ws.d, ws.norms, ws.tn, ws.inv_norms)
+
+            ws.norms_token = _norms_token(P)
+            P.pending_rest = rest
+            P.pending = None
+            return
         else:
             with _span("adam_dec"):
                 step_(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), max_blocks=DEC_ADAM_BLOCKS)
