@@ -151,6 +151,7 @@ class StepWorkspace:
         # per-(row, 64-column block) squared sums of W_dec (d % 64 == 0): written by the decoder-half Adam
         # (cc_adam_dec_norms) or by the fused W_dec^T + norms pass
         self.norm_part = E(npart) if npart else None
+        self.norms_event = None  # the side stream's norm finaliser, waited for by the first main-stream reader
         self.acts_t = E(h, B, dt=dtype) if self.tr else None
         # G1's activation mask as bits in the GEMM accumulator order: G3 reads 16 B per thread and tile instead
         # of the 128 KB acts tile (1/16 of the bytes, no LDS staging)
@@ -246,6 +247,14 @@ def _decoder_derived(ws, P):
     ops.dec_norms(P.W_dec_hk, ws.h, ws.n, ws.d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
 
 
+def wait_norms(ws):
+    """Order torch's current stream after the decoder-norm finaliser the side stream ran (engine.adam); by
+    the time G3 or the loss tail read the norms it has long completed."""
+    if ws.norms_event is not None:
+        torch.cuda.current_stream(ws.x.device).wait_event(ws.norms_event)
+        ws.norms_event = None
+
+
 def decoder_norms(ws, P):
     """||W_dec[h, m]||, their sum over m and inverses (crosscoder.py:123-125), unless still fresh."""
     if getattr(ws, "norms_token", None) == _norms_token(P):
@@ -334,6 +343,7 @@ def loss_colpart(ws):
 def loss_finalize(ws, l1l0_out=None):
     """Loss scalars / EV vectors.  After a forward (which deferred the activation column sums) one
     launch does both (cc_loss_tail); a re-formed loss (same activations) only the finaliser."""
+    wait_norms(ws)
     if ws.acts_pending:
         ops.loss_tail(ws.acts_colpart, ws.h, None, ws.tn, ws.l1_part, _row_part(ws), ws.l0_part, ws.n_wave,
                       ws.ev, ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], l1l0_out=l1l0_out,
@@ -385,6 +395,7 @@ def dacts_rows(ws, P, l1_coeff, r0, r1, l1_grad_weight=1.0):
     """G3 over batch rows [r0, r1) (r0 % 256 == 0): g_pre rows + their column-sum partial rows."""
     l1_scale = float(l1_coeff) * l1_grad_weight / ws.B
     c0, c1 = ops.col_part_rows(r0), ops.col_part_rows(r1)
+    wait_norms(ws)
     with _span("G3_dacts"):
         if ws.tr:
             ops.dacts_bwd_t(ws.g_recon[r0:r1], P.W_dec_hk, ws.acts[r0:r1], ws.tn, l1_scale, ws.g_pre_t[:, r0:r1],
@@ -515,13 +526,21 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
             done.record(side_stream)
 
             def rest():
+                # the rows, then the norm finaliser on the side stream (G2 reads W_dec, not the norms: it waits
+                # only for the side stream's rows; G3 / the loss tail wait for the finaliser, wait_norms)
                 cur = torch.cuda.current_stream(dev)
                 with _span("adam_dec_rest"):
                     ops.adam_dec_norms(*(t[hs * K:] for t in dec), ws.h - hs, K, *hp, ws.norm_part[hs * nblk:],
                                        **kw)
+                rest_done = torch.cuda.Event()
+                rest_done.record(cur)
+                with torch.cuda.stream(side_stream):
+                    side_stream.wait_event(rest_done)
+                    with _span("dec_norms"):
+                        ops.dec_norms_finalize(ws.norm_part, ws.h, ws.n, ws.d, ws.norms, ws.tn, ws.inv_norms)
+                    ws.norms_event = torch.cuda.Event()
+                    ws.norms_event.record(side_stream)
                 cur.wait_event(done)
-                with _span("dec_norms"):
-                    ops.dec_norms_finalize(ws.norm_part, ws.h, ws.n, ws.d, ws.norms, ws.tn, ws.inv_norms)
 
             ws.norms_token = _norms_token(P)
             P.pending_rest = rest
