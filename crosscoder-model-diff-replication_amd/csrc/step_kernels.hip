@@ -523,6 +523,52 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   }
 }
 
+// The capped-grid (side-stream) bf16 Adam with the next chunk's loads in flight during this chunk's math.
+// Beside G1 its workgroups get one wave per SIMD (G1 holds 2 x 216 of the 512 registers), so it streams
+// only as fast as one wave's loads in flight allow: this form keeps two chunks' loads in flight in the same
+// 64 registers, the data kept packed (8 bf16 per 16 B) and unpacked one element at a time.  Same per-element
+// arithmetic (adam_elem) and norm partials as adam_kernel.  numel % 8 == 0.
+CC_DEV void adam_pipe_load(const AdamArgs& a, int64_t i, bf16x8& p, bf16x8& g, bf16x8& m, bf16x8& v) {
+  p = __builtin_nontemporal_load((const bf16x8*)((const bf16_t*)a.p + i));
+  g = __builtin_nontemporal_load((const bf16x8*)((const bf16_t*)a.g + i));
+  m = __builtin_nontemporal_load((const bf16x8*)((const bf16_t*)a.m + i));
+  v = __builtin_nontemporal_load((const bf16x8*)((const bf16_t*)a.v + i));
+}
+__global__ __launch_bounds__(256) void adam_pipe_kernel(const AdamArgs a) {
+  const float coef = adam_coef(a);
+  const int64_t stride = (int64_t)gridDim.x * 256 * 8;
+  int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i >= a.numel) return;
+  bf16x8 p, g, m, v;
+  adam_pipe_load(a, i, p, g, m, v);
+  for (; i < a.numel; i += stride) {
+    const int64_t nx = i + stride;
+    bf16x8 p2 = p, g2 = g, m2 = m, v2 = v;
+    if (nx < a.numel) adam_pipe_load(a, nx, p2, g2, m2, v2);
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float pj = bf2f((bf16_t)p[j]), mj = bf2f((bf16_t)m[j]), vj = bf2f((bf16_t)v[j]);
+      adam_elem<CC_BF16>(a, coef, pj, bf2f((bf16_t)g[j]), mj, vj);
+      p[j] = (short)f2bf(pj);
+      m[j] = (short)f2bf(mj);
+      v[j] = (short)f2bf(vj);
+      q = __fmaf_rn(pj, pj, q);
+    }
+    if (a.norm_part && i < (int64_t)a.norm_rows * a.norm_ld) {  // (as adam_kernel)
+      q = block8_sum(q);
+      if ((threadIdx.x & 7) == 0) {
+        const int row = (int)(i / a.norm_ld);
+        a.norm_part[(int64_t)row * (a.norm_ld >> 6) + ((int)(i - (int64_t)row * a.norm_ld) >> 6)] = q;
+      }
+    }
+    __builtin_nontemporal_store(p, (bf16x8*)((bf16_t*)a.p + i));
+    __builtin_nontemporal_store(m, (bf16x8*)((bf16_t*)a.m + i));
+    __builtin_nontemporal_store(v, (bf16x8*)((bf16_t*)a.v + i));
+    p = p2; g = g2; m = m2; v = v2;
+  }
+}
+
 // Decoder-half Adam over W_dec [h][K] (bf16) in 64 x 64 tiles that also emits what the next
 // step needs from the updated W_dec: W_dec^T [K][h] (LDS tile read back with ds_read_b64_tr_b16)
 // and the decoder norms' per-(row, 64-column block) squared sums in dec_norms_kernel's order
@@ -900,6 +946,11 @@ static int adam_launch(const AdamArgs& a, int64_t max_blocks, int dtype, hipStre
     int64_t work = (numel + 7) / 8;
     int64_t blocks = (work + 255) / 256;
     if (blocks > max_blocks) blocks = max_blocks;
+    if (dtype == CC_BF16 && numel % 8 == 0) {
+      hipLaunchKernelGGL(adam_pipe_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
+      CC_LAUNCH_CHECK();
+      return CC_OK;
+    }
     DISPATCH_DT(dtype, hipLaunchKernelGGL((adam_kernel<DT_>), dim3((unsigned)blocks), dim3(256), 0, st, a));
     CC_LAUNCH_CHECK();
     return CC_OK;
