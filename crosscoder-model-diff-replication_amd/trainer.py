@@ -153,8 +153,8 @@ class Trainer:
 
     def synchronize(self):
         """Order torch's current stream after every launch of the last step (the decoder half of
-        Adam may still run on the side stream; CrossCoder's accessors and optimizer.state wait by
-        themselves)."""
+        Adam may still run on the side stream, and its last rows are deferred to the next reader, which
+        launches them; CrossCoder's accessors and optimizer.state do this by themselves)."""
         self.crosscoder.arena().wait_pending()
 
     def step(self):
