@@ -530,8 +530,11 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
                 # only for the side stream's rows; G3 / the loss tail wait for the finaliser, wait_norms)
                 cur = torch.cuda.current_stream(dev)
                 with _span("adam_dec_rest"):
-                    ops.adam_dec_norms(*(t[hs * K:] for t in dec), ws.h - hs, K, *hp, ws.norm_part[hs * nblk:],
-                                       **kw)
+                    if ws.h > hs:
+                        ops.adam_dec_norms(*(t[hs * K:] for t in dec), ws.h - hs, K, *hp, ws.norm_part[hs * nblk:],
+                                           **kw)
+                    else:  # (every row on the side stream: b_dec only)
+                        step_(*(t[hs * K:] for t in dec))
                 rest_done = torch.cuda.Event()
                 rest_done.record(cur)
                 with torch.cuda.stream(side_stream):
