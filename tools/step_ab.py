@@ -1,7 +1,10 @@
 """Whole-step timing of config 2 on ONE device, for same-box A/B: schedule variants of the decoder-half
 Adam are defined HERE (monkeypatching engine.adam inside this process) -- the product keeps a single
 schedule -- and library builds via --lib.  Variants run interleaved, 20 steps per sample.
-  python tools/step_ab.py [--lib path/to/variant.so] [--spans] [--rounds R] [--only=a,b]"""
+  python tools/step_ab.py [--lib path/to/variant.so] [--spans] [--rounds R] [--only=a,b]
+The variants below are the round-2 schedule experiments behind profiles/r02_step_ab_*.txt: they assume the
+W_dec^T workspace copy (ws.W_dec_t), which the step no longer keeps since round 3 (G2 reads W_dec itself);
+round-3 A/Bs are whole source trees timed by tools/ab_trees.sh / ab_multi.sh instead."""
 import argparse
 import os
 import sys
