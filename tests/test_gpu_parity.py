@@ -490,6 +490,31 @@ def test_full_size_step_deterministic(gpu, full_size_case):
     assert outs[0][1]["l2_loss"] < outs[0][0]["l2_loss"]
 
 
+@pytest.mark.parametrize("side_rows", [0.0, 0.5, 1.0])
+def test_decoder_adam_split_is_bit_identical(gpu, side_rows, monkeypatch):
+    """The decoder half of Adam split between the side stream (W_dec's first rows, beside the next G1) and the
+    next reader's stream (the rest + b_dec, engine.DEC_SIDE_ROWS) gives the same bits for any split, including
+    every row deferred (0.0) and only b_dec deferred (1.0): params, both moments and the next step's losses."""
+    from crosscoder_amd import engine
+    B, n, d, h = 512, 2, 128, 1024
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+               num_tokens=B * 20, device=str(gpu))
+    outs = []
+    for frac in (engine.DEC_SIDE_ROWS, side_rows):
+        monkeypatch.setattr(engine, "DEC_SIDE_ROWS", frac)
+        cc = ca.CrossCoder(cfg)
+        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=4), crosscoder=cc)
+        dicts = [tr.step() for _ in range(3)]
+        st = tr.optimizer.state  # (launches the deferred rows, then orders after the side stream)
+        m = torch.cat([st[p]["exp_avg"].detach().flatten().float() for p in cc.parameters()])
+        v = torch.cat([st[p]["exp_avg_sq"].detach().flatten().float() for p in cc.parameters()])
+        torch.cuda.synchronize()
+        outs.append((dicts, cc.arena().data.clone(), m, v))
+    (d0, p0, m0, v0), (d1, p1, m1, v1) = outs
+    assert d0 == d1
+    assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+
+
 def test_full_size_config2_trainer_steps_match_oracle(gpu, full_size_case):
     """BASELINE config 2 through the shipped schedule (Trainer.step: fused G2 + loss, G4G5 + grad tail + clip
     in one launch, encoder / decoder Adam halves on two streams) vs the oracle's fp32 OracleTrainer.step
