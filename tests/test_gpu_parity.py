@@ -887,21 +887,26 @@ def test_decode_loss_on_wdec_matches_transposed(gpu, B, n, d, h):
     assert ncb == d // 64
     nws = max(ops.decode_ws_floats(B, h, K, bf), 1)
     outs = []
-    for direct in (False, True):
+    for direct in (False, True, "no_t"):
         g_recon = torch.full((B, K), float("nan"), dtype=bf, device=gpu)
         g_t = torch.full((K, B), float("nan"), dtype=bf, device=gpu)
         rp = torch.full((2, n * ncb, B), float("nan"), device=gpu)
         cp = torch.full((ops.col_part_rows(B), K), float("nan"), device=gpu)
         dws = torch.empty(nws, device=gpu)
-        if direct:
+        if direct == "no_t":  # g_recon^T not wanted: everything else the same, g_t untouched
+            ops.decode_loss(acts, W, b_dec, x, x_mean, 2.0 / B, g_recon, None, rp, cp, dws, n, d)
+        elif direct:
             ops.decode_loss(acts, W, b_dec, x, x_mean, 2.0 / B, g_recon, g_t, rp, cp, dws, n, d)
         else:
             ops.decode_loss_t(acts, W.t().contiguous(), b_dec, x, x_mean, 2.0 / B, g_recon, g_t, rp, cp, dws, n, d)
         outs.append((g_recon, g_t, rp, cp))
     torch.cuda.synchronize()
-    for a, b in zip(*outs):
+    for a, b in zip(outs[0], outs[1]):
         assert not bool(torch.isnan(a.float()).any())
         assert torch.equal(a, b)
+    g_recon, g_t, rp, cp = outs[2]
+    assert torch.equal(g_recon, outs[0][0]) and torch.equal(rp, outs[0][2]) and torch.equal(cp, outs[0][3])
+    assert bool(torch.isnan(g_t.float()).all())
 
 
 @pytest.mark.parametrize("comm", ["all_reduce", "reduce_scatter"])
