@@ -11,19 +11,19 @@ Workloads are BASELINE.json's configs (synthetic normalised activations, referen
 GPU): the FIXED dictionary of the config is split into N latent slices (strong scaling) with an RCCL
 all-reduce of the fp32 partial reconstructions; every rank processes the same batch.
 
-`value` is in the metric's own unit, activations of the 2x2304->16384 crosscoder trained per second: a batch
-row of a workload with n models of width d and h latents is 10.n.d.h FLOP of step work, i.e.
-(n.d.h) / (2.2304.16384) metric activations.  At N = 1 on config 2 (the driver's N = 1 run) that factor is 1
-and `value` = batch rows / s; a config-3 row (2^17 latents) counts 8.  So the driver's per-N values compare
-like for like (config 2 at N = 1, config 3 split over N > 1), and value_N / (N . value_1) is the scaling
-efficiency.  `rows_per_s` is the raw batch rows trained per second by the whole job, `latent_acts_per_s`
-= rows_per_s x dict_size.
+`value` is the activations (batch rows, each seen by all n models) the whole job trains per second -- the
+metric's own unit, on whatever workload runs.  At N = 1 that is config 2, the metric's config.  N > 1 runs
+config 3 (2^17 latents, as BASELINE.json's north_star asks), whose rows cost 8x a config-2 row, so its
+`value` is not comparable with the N = 1 line: the strong-scaling point of comparison is `n1_same_workload`
+(config 3 on one GPU, committed measurement), and `metric_equiv_acts_per_s` = value x n.d.h / (2.2304.16384)
+restates the throughput in config-2 rows of equal FLOP (10.n.d.h FLOP of step work per row).
+`latent_acts_per_s` = value x dict_size.
 
 The JSON line also carries `roofline` (dominant kernel's achieved TFLOP/s from HIP events around its
 launches inside the timed region, vs the bf16 dense MFMA peak), `hbm` (achieved GB/s of the
-streaming kernels: Adam halves, input prep, W_dec^T pass -- and the loss kernel where G2 does not carry the
-loss in its epilogue -- from an untimed attribution pass) and
-`cpu_baseline` (the oracle CPU step timed on this host, rank 0, N = 1 only).
+streaming kernels: Adam halves, input prep -- and the loss kernel where G2 does not carry the loss in its
+epilogue -- from an untimed attribution pass) and `cpu_baseline` (the oracle CPU step timed on this host,
+rank 0, N = 1 only).
 """
 import argparse
 import json
@@ -113,6 +113,24 @@ def pmc_traffic(span):
     return None, None
 
 
+def rocprof_average(span):
+    """The dominant kernel's average duration in the newest committed rocprofv3 --stats summary of this bench
+    (profiles/*_step_kernel_stats.csv) -- the figure the live event samples are checked against -- or None."""
+    import csv
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_step_kernel_stats.csv")))
+    if not files or span not in SPAN_KERNEL:
+        return None
+    with open(files[-1]) as f:
+        for row in csv.DictReader(f):
+            name = row["Name"].replace("void ", "").replace("cc::", "")
+            if name.startswith(SPAN_KERNEL[span]):
+                return {"avg_ms": round(float(row["AverageNs"]) * 1e-6, 4), "calls": int(row["Calls"]),
+                        "min_ms": round(float(row["MinNs"]) * 1e-6, 4), "source": os.path.relpath(files[-1], ROOT)}
+    return None
+
+
 def n1_same_workload(B, n, d, h):
     """The committed one-GPU bench line of the same workload (profiles/*_bench_configs.jsonl, measured by this
     bench with --config on one MI355X), the 1-GPU point of an N > 1 strong-scaling curve -- or None."""
@@ -129,10 +147,9 @@ def n1_same_workload(B, n, d, h):
         c = r.get("config", {})
         if r.get("n_gpus") == 1 and (c.get("global_batch"), c.get("n_models"), c.get("d_model"),
                                        c.get("dict_size")) == (B, n, d, h):
-            # (value in this bench's unit, from the line's own step time: older lines carried raw rows / s)
-            per_row = (n * d * h) / (2 * 2304 * 16384)
-            return {"value": round(B / (r["ms_per_step"] * 1e-3) * per_row, 1), "ms_per_step": r["ms_per_step"],
-                    "rows_per_s": round(B / (r["ms_per_step"] * 1e-3), 1), "source": os.path.relpath(files[-1], ROOT)}
+            # (value = rows / s, from the line's own step time)
+            return {"value": round(B / (r["ms_per_step"] * 1e-3), 1), "ms_per_step": r["ms_per_step"],
+                    "source": os.path.relpath(files[-1], ROOT)}
     return None
 
 
@@ -317,12 +334,11 @@ def main():
 
     step_s = elapsed / args.steps
     ms = step_s * 1e3
-    rows_per_s = B / step_s  # batch rows trained per second by the whole job
-    # metric activations (2x2304->16384 crosscoder rows) per row of this workload: step work is 10.n.d.h FLOP
-    # per row, so config 2 counts 1 and config 3 (2^17 latents) 8
+    rows_per_s = B / step_s  # activations (batch rows) trained per second by the whole job: `value`
+    # config-2 rows of equal step work (10.n.d.h FLOP per row): config 2 counts 1, config 3 (2^17 latents) 8
     per_row = (n * d * h_total) / (2 * 2304 * 16384)
-    value = rows_per_s * per_row
     dom_ms = timer.averages_ms()[dom]
+    samples = sorted(s_.elapsed_time(e_) for s_, e_ in timer.rec.get(dom, []))
     gemm_flop = 2.0 * B * K * h_local  # per GEMM (per rank)
     # G4G5_wgrad is one launch computing both weight gradients (cc_wgrad_both)
     dom_flop = gemm_flop * (2 if dom == "G4G5_wgrad" else 1)
@@ -341,8 +357,8 @@ def main():
     name = f"{n}x{d}->{h_total}"
     result = {
         "metric": "activations/sec per train step (fwd+bwd+Adam), 2x2304->16384; % bf16 MFMA peak",
-        "value": round(value, 1),
-        "unit": "activations/s" if per_row == 1 else "activations/s (2x2304->16384-equivalent)",
+        "value": round(rows_per_s, 1),
+        "unit": "activations/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -359,8 +375,8 @@ def main():
                    "baseline_config": None if custom else config,
                    "global_batch": B, "n_models": n, "d_model": d, "dict_size": h_total,
                    "parallelism": f"latent{world}"},
-        "rows_per_s": round(rows_per_s, 1),
-        "metric_activations_per_row": per_row,
+        "metric_equiv_acts_per_s": round(rows_per_s * per_row, 1),
+        "metric_equiv_per_row": per_row,
         "latent_acts_per_s": round(rows_per_s * h_total, 1),
         # N > 1: the same workload on one GPU (committed measurement), so the strong-scaling curve has its
         # own 1-GPU point (the driver's N = 1 run is the metric's config 2, a different dictionary)
@@ -368,7 +384,11 @@ def main():
         "step_mfma_frac": round(step_flop / step_s / 1e12 / (PEAK_BF16_TFLOPS * world), 4),
         "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items())},
         "roofline": {"bound": "mfma", "kernel": dom, "kernel_name": SPAN_KERNEL.get(dom), "kernel_ms": round(dom_ms, 4),
-                     "kernel_samples": len(timer.rec.get(dom, [])), "achieved": round(achieved, 1),
+                     "kernel_samples": len(samples),
+                     "kernel_ms_min_med_max": [round(samples[0], 4), round(samples[len(samples) // 2], 4),
+                                               round(samples[-1], 4)] if samples else None,
+                     "rocprof": rocprof_average(dom) if (config, world, custom) == (2, 1, False) else None,
+                     "achieved": round(achieved, 1),
                      "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                      "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
                      "algorithmic_bytes": dom_alg_bytes},

@@ -69,10 +69,8 @@ SIGNATURES = {
                           _p, _p]),
     "cc_grad_tail_sums": (_i, [_p, _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _i, _p, ctypes.POINTER(_i64), _i, _i, _p,
                                _p, _p]),
-    "cc_loss_tail": (_i, [_p, _i64, _i64, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _i64,
-                          _i64, _i64, _p, _p]),
-    "cc_loss_tail_nb": (_i, [_p, _i64, _i64, _p, _p, _p, _p, _i64, _p, _i64, _p, _p, _p, _p, _p, _p, ctypes.c_uint32,
-                             _i64, _i64, _i64, _p, _p]),
+    "cc_loss_tail": (_i, [_p, _p, _i64, _p, _p, _i64, _p, _i64, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _i64, _i64,
+                          _i64, _p, _p]),
     "cc_loss_finalize_nb": (_i, [_p, _i64, _p, _i64, _p, _i64, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _i64, _i64,
                                  _i64, _p]),
     "cc_decode_loss_ncb": (_i64, [_i64, _i64, _i64, _i64, _i]),
@@ -137,6 +135,8 @@ def load_debug():
             fn = getattr(lib, name)
             fn.restype = None
             fn.argtypes = [ctypes.c_int]
+        lib.cc_debug_spin.restype = _i
+        lib.cc_debug_spin.argtypes = [_i64, _i64, _i64, _p]
         _debug = lib
     return _debug
 

@@ -652,6 +652,26 @@ static int g_pp_mask = 7, g_pp_fast = 1, g_dec_one_launch = 1;
 CC_DEBUG_API void cc_debug_set_pp_mask(int mask) { g_pp_mask = mask; }
 CC_DEBUG_API void cc_debug_set_pp_fast(int on) { g_pp_fast = on; }
 CC_DEBUG_API void cc_debug_set_dec_one_launch(int on) { g_dec_one_launch = on; }
+// Test / probe kernel: `blocks` workgroups of 512 threads that each hold `lds_bytes` of LDS and spin for `ns`
+// nanoseconds of the 100 MHz wall clock (s_sleep between reads) -- a stand-in for another stream's kernel that
+// holds CUs (a delayed producer, or RCCL's collective kernel beside a GEMM).  Every wave exits on the clock.
+__global__ __launch_bounds__(NTHR) void debug_spin_kernel(int64_t ticks) {
+  extern __shared__ char hold[];
+  const uint64_t t0 = wall_clock64();
+  if (threadIdx.x == 0) hold[0] = 0;
+  while (wall_clock64() - t0 < (uint64_t)ticks) __builtin_amdgcn_s_sleep(8);
+}
+CC_DEBUG_API int cc_debug_spin(int64_t blocks, int64_t lds_bytes, int64_t ns, void* stream) {
+  if (blocks <= 0 || blocks > 4096 || lds_bytes < 0 || lds_bytes > 160 * 1024 || ns < 0 || ns > 1000000000)
+    return CC_ERR_SHAPE;
+  if (lds_bytes > 65536 && hipFuncSetAttribute((const void*)debug_spin_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes) != hipSuccess)
+    return CC_ERR_SHAPE;
+  hipLaunchKernelGGL(debug_spin_kernel, dim3((unsigned)blocks), dim3(NTHR), (unsigned)lds_bytes, (hipStream_t)stream,
+                     (int64_t)(ns / 10));
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
 #else
 constexpr int g_pp_mask = 7, g_pp_fast = 1, g_dec_one_launch = 1;
 #endif

@@ -65,9 +65,11 @@ CC_DEV void ev_phase2(const EvSeg& a, int blk, int t, float (*red)[4]) {
     a.part_out[blk * 4 + q] = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
   }
 }
-// Single block: scalars = {l2, l1, l0, mean ev, mean ev_a, mean ev_b}.  NT threads (SCAL_THREADS in the
-// stand-alone kernels, the GEMM's 512 where the d_acts launch runs the finaliser); red: LDS scratch of the caller.
-constexpr int SCAL_THREADS = 1024;
+// Single block: scalars = {l2, l1, l0, mean ev, mean ev_a, mean ev_b}.  NT threads: LOSS_THREADS in both the
+// stand-alone finaliser and the fused loss tail (the same fp64 accumulation order, so the same bits); red: LDS
+// scratch of the caller.
+constexpr int SCAL_THREADS = 1024;  // (the clip finaliser's block)
+constexpr int LOSS_THREADS = 256;
 struct ScalArgs {
   const float* ev_part;
   int nblk;
@@ -102,17 +104,18 @@ CC_DEV void loss_scalars_body(const ScalArgs& sa, double (*red)[6]) {
     acc[4] += ev_part[i * 4 + 2];
     acc[5] += ev_part[i * 4 + 3];
   }
-  // 4 independent loads in flight per trip (clamped index, no branch around a load)
+  // 8 independent loads in flight per trip (clamped index, no branch around a load); each thread still adds
+  // its elements i, i + NT, i + 2 NT, ... in order
   if (l0_part) {
-    for (int64_t i = threadIdx.x; i < n_wave; i += 4 * NT) {
-      float b[4];
+    for (int64_t i = threadIdx.x; i < n_wave; i += 8 * NT) {
+      float b[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         const int64_t j = i + u * NT;
         b[u] = j < n_wave ? l0_part[j < n_wave ? j : 0] : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc[2] += b[u];
+      for (int u = 0; u < 8; ++u) acc[2] += b[u];
     }
   }
   if (l1_part)

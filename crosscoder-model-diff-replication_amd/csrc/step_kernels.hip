@@ -269,9 +269,9 @@ __global__ __launch_bounds__(256) void ev_kernel(const EvSeg a) {
   ev_phase2(a, blockIdx.x, threadIdx.x, red);
 }
 
-__global__ __launch_bounds__(SCAL_THREADS) void loss_scalars_kernel(const ScalArgs a) {
-  __shared__ double red[SCAL_THREADS / 64][6];
-  loss_scalars_body<SCAL_THREADS>(a, red);
+__global__ __launch_bounds__(LOSS_THREADS) void loss_scalars_kernel(const ScalArgs a) {
+  __shared__ double red[LOSS_THREADS / 64][6];
+  loss_scalars_body<LOSS_THREADS>(a, red);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -282,67 +282,90 @@ __global__ __launch_bounds__(SCAL_THREADS) void clip_kernel(const ClipArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Fused step tails: one launch of 1024-thread blocks = 4 independent 256-thread groups, each
-// running one block of a column reduction (RedSeg) or of ev_kernel (EvSeg) -- the same two phases
-// as the stand-alone kernels, so the same bits -- then the last block to finish (device-scope
-// arrival counter, reset by that block for the next launch) runs the single-block finaliser
-// (clip_body or loss_scalars_body) over the partials the whole grid wrote.  Saves the finaliser's
-// launch (and, for the loss tail, one reduction launch) per step.
-//   grad tail: b_enc.grad, b_dec.grad column sums + their sq partials -> clip coefficient
-//   loss tail: sum_b acts + l1 partials, per-row EV + partials -> the loss scalars
+// Arrival count of a fused tail launch: every workgroup publishes what it wrote, and the last one to arrive
+// (device-scope counter, reset by that workgroup for the next launch) returns true with the others' writes
+// visible.  The barrier's workgroup-scope release waits for every wave's stores to reach this XCD's L2; ONE
+// agent-scope release (an L2 write-back) then publishes them all before the arrival count.  Call with every
+// thread of the workgroup; `last` is LDS scratch.
+CC_DEV bool arrive_last(unsigned* counter, int* last) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const bool is_last = atomicAdd(counter, 1u) == gridDim.x - 1;
+    if (is_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // drop stale lines before the reads
+    *last = is_last;
+  }
+  __syncthreads();
+  return *last;
+}
+
+// Fused grad tail: one launch of 1024-thread blocks = 4 independent 256-thread groups, each running one
+// block of a column reduction (RedSeg: b_enc.grad, b_dec.grad column sums + their sq partials) -- the same
+// two phases as the stand-alone kernel, so the same bits -- then the last block to finish runs clip_body
+// (or the segment sums) over the partials the whole grid wrote.  Saves the finaliser's launch per step.
 struct TailArgs {
   RedSeg red[2];
   int red_blocks[2];  // 256-thread groups per reduction (0: unused)
-  EvSeg ev;
-  int ev_blocks;      // 0: no EV segment
-  int finalize;       // 0: clip_body(clip), 1: loss_scalars_body(scal)
   ClipArgs clip;
-  ScalArgs scal;
   unsigned* counter;
 };
 template <int DT>
 __global__ __launch_bounds__(SCAL_THREADS) void tail_kernel(const TailArgs a) {
   __shared__ float red[4][4][RED_COLS];
-  __shared__ float evred[4][4][4];
   __shared__ int last;
   const int grp = threadIdx.x >> 8, t = threadIdx.x & 255;
   int b = blockIdx.x * 4 + grp;
-  // role of this group: reduction 0, reduction 1, EV block or idle (uniform per group)
-  int role = 3;
-  if (b < a.red_blocks[0]) {
-    role = 0;
-  } else if ((b -= a.red_blocks[0]) < a.red_blocks[1]) {
-    role = 1;
-  } else if ((b -= a.red_blocks[1]) < a.ev_blocks) {
-    role = 2;
-  }
+  // role of this group: reduction 0, reduction 1 or idle (uniform per group)
+  int role = 2;
+  if (b < a.red_blocks[0]) role = 0;
+  else if ((b -= a.red_blocks[0]) < a.red_blocks[1]) role = 1;
   if (role < 2) reduce_rows_phase1(a.red[role], b, t, red[grp]);
-  else if (role == 2) ev_phase1(a.ev, b, t, evred[grp]);
   __syncthreads();
   if (role < 2) reduce_rows_phase2<DT>(a.red[role], b, t, red[grp]);
-  else if (role == 2) ev_phase2(a.ev, b, t, evred[grp]);
-  // publish this block's partials, then count arrivals.  The barrier's workgroup-scope release
-  // waits for every wave's stores to reach this XCD's L2; ONE agent-scope release (an L2
-  // write-back) then publishes them all before the arrival count.
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const bool is_last = atomicAdd(a.counter, 1u) == gridDim.x - 1;
-    if (is_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // drop stale lines before the reads
-    last = is_last;
-  }
-  __syncthreads();
-  if (!last) return;
-  if (a.finalize == 0) {
-    __shared__ double cred[8][SCAL_THREADS / 64];
-    __shared__ float cnorms[8];
-    clip_body<SCAL_THREADS>(a.clip, cred, cnorms);
-  }
-  else {
-    __shared__ double sred[SCAL_THREADS / 64][6];
-    loss_scalars_body<SCAL_THREADS>(a.scal, sred);
-  }
+  if (!arrive_last(a.counter, &last)) return;
+  __shared__ double cred[8][SCAL_THREADS / 64];
+  __shared__ float cnorms[8];
+  clip_body<SCAL_THREADS>(a.clip, cred, cnorms);
   if (threadIdx.x == 0) atomicExch(a.counter, 0u);
+}
+
+// Fused loss tail (crosscoder.py:106-128): the l1 partials, the per-row EV terms and the loss scalars in one
+// launch whose workgroups fit beside a persistent GEMM workgroup -- the step runs it on a side stream during
+// G3, which holds 2 x 216 of each SIMD's 512 VGPRs and 128 KB of each CU's LDS, so a workgroup of 256 threads
+// (one wave per SIMD), few registers and < 0.5 KB of LDS starts at once instead of after G3.
+//   workgroups [0, l1_wgs): one 64-latent block per wave, B * l1's partial sum_j colsum[j] * tn[j] -- the dot
+//     reduce_rows_phase2 forms (colsum IS that reduction of G1's column slab, scale 1), so the same bits;
+//   the next ev_blocks workgroups: 256 batch rows each (ev_phase1/2);
+//   the last workgroup to arrive: loss_scalars_body<LOSS_THREADS> (the stand-alone loss_scalars_kernel's).
+struct LossTailArgs {
+  const float* colsum;
+  const float* tn;
+  int h;
+  float* l1_part;
+  int l1_wgs;
+  EvSeg ev;
+  ScalArgs scal;
+  unsigned* counter;
+};
+__global__ __launch_bounds__(LOSS_THREADS) void loss_tail_kernel(const LossTailArgs a) {
+  __shared__ float evred[4][4];
+  __shared__ double sred[LOSS_THREADS / 64][6];
+  __shared__ int last;
+  const int t = threadIdx.x;
+  if ((int)blockIdx.x < a.l1_wgs) {
+    const int lane = t & 63, blk = (int)blockIdx.x * 4 + (t >> 6), j = blk * 64 + lane;
+    float dot = j < a.h ? a.colsum[j] * a.tn[j] : 0.f;
+    dot = wave_sum(dot);
+    if (lane == 0 && blk * 64 < a.h) a.l1_part[blk] = dot;
+  } else {
+    const int b = (int)blockIdx.x - a.l1_wgs;
+    ev_phase1(a.ev, b, t, evred);
+    __syncthreads();
+    ev_phase2(a.ev, b, t, evred);
+  }
+  if (!arrive_last(a.counter, &last)) return;
+  loss_scalars_body<LOSS_THREADS>(a.scal, sred);
+  if (t == 0) atomicExch(a.counter, 0u);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -818,7 +841,7 @@ int cc_loss_finalize_nb(const float* row_part, int64_t ncb_rows, const float* l1
   const EvSeg e = {row_part, (int)B, (int)n, ncb, ev, ev_a, ev_b, ev_part};
   hipLaunchKernelGGL(ev_kernel, dim3(nblk), dim3(256), 0, st, e);
   const ScalArgs s = {ev_part, nblk, l1_part, n_l1, l0_part, n_l0, (int)B, scalars, l1l0_out, host_out, (unsigned)seq};
-  hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(SCAL_THREADS), 0, st, s);
+  hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(LOSS_THREADS), 0, st, s);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }
@@ -991,7 +1014,6 @@ static int grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* 
   a.red[1] = {loss_colpart, (int)R_dec, (int)K, K, 1.f, nullptr, g_b_dec, sq_b_dec, nullptr, nullptr};
   a.red_blocks[0] = (int)((h + RED_COLS - 1) / RED_COLS);
   a.red_blocks[1] = (int)((K + RED_COLS - 1) / RED_COLS);
-  a.finalize = 0;
   a.clip.sq = sq;
   for (int i = 0; i <= nparams; ++i) a.clip.off[i] = off[i];
   a.clip.nparams = nparams;
@@ -1024,33 +1046,26 @@ int cc_grad_tail_sums(const float* gpre_colpart, int64_t R_enc, int64_t h, void*
                    off, nparams, 0.f, 0, 1, zero_mask, out, counter, stream);
 }
 
-int cc_loss_tail(const float* acts_colpart, int64_t R, int64_t h, float* colsum_acts, const float* tn,
-                 float* l1_part, const float* row_part, const float* l0_part, int64_t n_l0, float* ev, float* ev_a,
-                 float* ev_b, float* scalars, float* l1l0_out, float* host_out, uint32_t seq, int64_t B, int64_t n,
-                 int64_t d, uint32_t* counter, void* stream) {
-  return cc_loss_tail_nb(acts_colpart, R, h, colsum_acts, tn, l1_part, row_part, cc_loss_col_blocks(d), l0_part, n_l0,
-                         ev, ev_a, ev_b, scalars, l1l0_out, host_out, seq, B, n, d, counter, stream);
-}
-
-int cc_loss_tail_nb(const float* acts_colpart, int64_t R, int64_t h, float* colsum_acts, const float* tn,
-                    float* l1_part, const float* row_part, int64_t ncb, const float* l0_part, int64_t n_l0, float* ev,
-                    float* ev_a, float* ev_b, float* scalars, float* l1l0_out, float* host_out, uint32_t seq,
-                    int64_t B, int64_t n, int64_t d, uint32_t* counter, void* stream) {
-  if (!acts_colpart || !tn || !l1_part || !row_part || !scalars || !counter) return CC_ERR_NULL;  // colsum_acts optional
-  if (R <= 0 || h <= 0 || B <= 0 || n <= 0 || d <= 0 || ncb <= 0) return CC_ERR_SHAPE;
-  TailArgs a = {};
+int cc_loss_tail(const float* colsum_acts, const float* tn, int64_t h, float* l1_part, const float* row_part,
+                 int64_t ncb, const float* l0_part, int64_t n_l0, float* ev, float* ev_a, float* ev_b, float* scalars,
+                 float* l1l0_out, float* host_out, uint32_t seq, int64_t B, int64_t n, int64_t d, uint32_t* counter,
+                 void* stream) {
+  if (!colsum_acts || !tn || !l1_part || !row_part || !scalars || !counter) return CC_ERR_NULL;
+  if (h <= 0 || B <= 0 || n <= 0 || d <= 0 || ncb <= 0) return CC_ERR_SHAPE;
+  LossTailArgs a = {};
   const int nred = (int)((h + RED_COLS - 1) / RED_COLS);
   const int nblk = (int)((B + 255) / 256);
   float* ev_part = scalars + 8;  // as cc_loss_finalize (cc_loss_scalars_len)
-  a.red[0] = {acts_colpart, (int)R, (int)h, h, 1.f, colsum_acts, nullptr, nullptr, tn, l1_part};
-  a.red_blocks[0] = nred;
+  a.colsum = colsum_acts;
+  a.tn = tn;
+  a.h = (int)h;
+  a.l1_part = l1_part;
+  a.l1_wgs = (nred + 3) / 4;
   a.ev = {row_part, (int)B, (int)n, (int)ncb, ev, ev_a, ev_b, ev_part};
-  a.ev_blocks = nblk;
-  a.finalize = 1;
   a.scal = {ev_part, nblk, l1_part, nred, l0_part, n_l0, (int)B, scalars, l1l0_out, host_out, (unsigned)seq};
   a.counter = counter;
-  dim3 grid((unsigned)((nred + nblk + 3) / 4));
-  hipLaunchKernelGGL((tail_kernel<CC_F32>), grid, dim3(SCAL_THREADS), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(loss_tail_kernel, dim3((unsigned)(a.l1_wgs + nblk)), dim3(LOSS_THREADS), 0,
+                     (hipStream_t)stream, a);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }

@@ -1,31 +1,32 @@
 """The crosscoder training step as a fixed sequence of HIP launches over resident HBM buffers.
 
 Data layout in HBM (one arena per role, all views of single allocations):
-  params  [ W_enc h-major [h][K] | W_dec [h][K] | b_enc [h] | b_dec [K] ]   (dtype)
+  params  [ W_enc h-major [h][K] | b_enc [h] | W_dec [h][K] | b_dec [K] ]   (dtype)
   grads   same layout (dtype)        exp_avg / exp_avg_sq   same layout (dtype)
-  x [B][K], acts [B][h], g_recon [B][K], g_pre [B][h] (dtype); recon [B][K] fp32.
+  x [B][K], acts [B][h], g_recon [B][K] (dtype); recon [B][K] fp32 (latent-sharded step / two-pass form only).
   bf16 (transposed_wgrad): also x^T [K][B], acts^T [h][B], g_recon^T [K][B], and g_pre only as
   g_pre^T [h][B] -- G4/G5 contract over the batch, so these make both of their operands
-  row-contiguous.  acts^T / g_pre^T come from G1's / G3's epilogues, x^T / g_recon^T from the
-  prep / loss kernels (LDS-staged transposed stores), W_dec^T [K][h] (for G2) from the pass that
-  computes the decoder norms after Adam.
+  row-contiguous.  acts^T / g_pre^T come from G1's / G3's epilogues, x^T from the prep kernel, g_recon^T
+  from G2's loss epilogue (LDS-staged transposed stores).  G2 reads W_dec [h][K] itself (transposed LDS
+  reads of its B operand); the decoder norms come from the partial sums the decoder-half Adam writes.
 W_enc's logical shape is [n, d, h] with strides (d, 1, K) exactly like the reference's
 rearranged view (crosscoder.py:55-58), so both weight matrices are [h][K] row-major and
 every GEMM streams 128-byte rows.
 
-Step (reference trainer.py:41-63 -> crosscoder.py:96-130 -> autograd -> clip -> Adam):
-  prep      x = dtype(buf * factor), column sums for x.mean(0)             buffer.py:124, crosscoder.py:99
-  norms     ||W_dec[h,m]||, sum over m                                     crosscoder.py:123-125
-  G1        acts = relu(x W_enc + b_enc) (+ l1/l0/colsum partials)         crosscoder.py:69-80,126,128
-  G2        recon = acts W_dec  (fp32)                                     crosscoder.py:82-89
-  loss      r = recon + b_dec; g_recon = 2(r-x)/B; l2/tv row terms          crosscoder.py:104-121
-  finalize  l2, l1, l0, EV vectors and means                               crosscoder.py:106-128
-  G3        g_pre = (g_recon W_dec^T + l1c tn/B) * (acts>0)                 autograd
-  G4        dW_dec = acts^T g_recon + l1c/B colsum(acts) W_dec/||W_dec||    autograd
-  G5        dW_enc = g_pre^T x                                              autograd
-  bias      db_enc = colsum(g_pre), db_dec = colsum(g_recon)               autograd
-  clip      coef = min(1, 1/(||g||+1e-6))                                  trainer.py:46
-  adam      fused over the whole arena                                     trainer.py:47
+Step (reference trainer.py:41-63 -> crosscoder.py:96-130 -> autograd -> clip -> Adam), single GPU:
+  prep      x = dtype(buf * factor), x^T, column sums for x.mean(0)          buffer.py:124, crosscoder.py:99
+  G1        acts = relu(x W_enc + b_enc), acts^T, mask bits, colsum/l0 slabs crosscoder.py:69-80,128
+  reduce    x.mean(0), sum_b acts                                           crosscoder.py:112,126
+  (rest)    the decoder-half Adam's last rows of the previous step, then the side stream's norm
+            finaliser ||W_dec[h,m]||, sum over m                            crosscoder.py:123-125
+  G2+loss   acts W_dec + b_dec - x -> l2/tv row terms, g_recon = 2(r-x)/B,
+            g_recon^T, db_dec slab (no fp32 reconstruction)                 crosscoder.py:82-89,104-121
+  [side]    loss tail: l1 partials, EV, the loss scalars (+ host copy)      crosscoder.py:106-128
+  G3        g_pre = (g_recon W_dec^T + l1c tn/B) * (acts>0), stored as g_pre^T  autograd
+  G4G5      dW_dec = acts^T g_recon + l1c/B colsum(acts) W_dec/||W_dec||,
+            dW_enc = g_pre^T x, db_enc / db_dec, the clip coefficient        autograd, trainer.py:46
+  adam      encoder half on this stream; the decoder half's first rows on the side stream beside the
+            next step's G1 (with the next step's norm partials)              trainer.py:47
 """
 import contextlib
 
@@ -151,7 +152,10 @@ class StepWorkspace:
         # per-(row, 64-column block) squared sums of W_dec (d % 64 == 0): written by the decoder-half Adam
         # (cc_adam_dec_norms) or by the fused W_dec^T + norms pass
         self.norm_part = E(npart) if npart else None
-        self.norms_event = None  # the side stream's norm finaliser, waited for by the first main-stream reader
+        # the side stream's norm finaliser and that stream: every other stream that reads the norms waits
+        # for it once (wait_norms)
+        self.norms_event = None
+        self.norms_stream = None
         self.acts_t = E(h, B, dt=dtype) if self.tr else None
         # G1's activation mask as bits in the GEMM accumulator order: G3 reads 16 B per thread and tile instead
         # of the 128 KB acts tile (1/16 of the bytes, no LDS staging)
@@ -160,10 +164,11 @@ class StepWorkspace:
         # step's slabs runs on the side stream, which nothing orders before the NEXT step's G1 on torch's
         # stream; alternating slots orders every rewrite after that tail (the step after next waits for
         # this step's decoder-half Adam before G2, and the side stream runs the tail before that Adam)
-        self._slots = [(E(ops.col_part_rows(B), h), E(ops.wave_parts(B, h))) for _ in range(2)]
+        # (and the column sums reduced from them, which the side stream's loss tail reads: the NEXT step's
+        # reduce runs on torch's stream before that step waits for the side stream)
+        self._slots = [(E(ops.col_part_rows(B), h), E(ops.wave_parts(B, h)), E(h)) for _ in range(2)]
         self._slot = 1
-        self.acts_colpart, self.l0_part = self._slots[1]
-        self.colsum_acts = E(h)
+        self.acts_colpart, self.l0_part, self.colsum_acts = self._slots[1]
         self.n_wave = ops.wave_parts(B, h)
         self.n_l1 = ops.reduce_parts(h)
         self.l1_part = E(self.n_l1)  # per 64-latent block: sum_h colsum_acts[h] * tn[h] (= B * l1)
@@ -207,9 +212,9 @@ class StepWorkspace:
         self.busy = None  # weakref to the token of an autograd graph whose backward still needs this workspace
 
     def next_slot(self):
-        """Switch G1's partial slabs (acts_colpart, l0_part) to the other slot (once per forward)."""
+        """Switch G1's partial slabs (acts_colpart, l0_part, colsum_acts) to the other slot (once per forward)."""
         self._slot ^= 1
-        self.acts_colpart, self.l0_part = self._slots[self._slot]
+        self.acts_colpart, self.l0_part, self.colsum_acts = self._slots[self._slot]
 
     def sq_slice(self, i):
         return self.sq[self.sq_off[i]:self.sq_off[i + 1]]
@@ -248,11 +253,16 @@ def _decoder_derived(ws, P):
 
 
 def wait_norms(ws):
-    """Order torch's current stream after the decoder-norm finaliser the side stream ran (engine.adam); by
-    the time G3 or the loss tail read the norms it has long completed."""
-    if ws.norms_event is not None:
-        torch.cuda.current_stream(ws.x.device).wait_event(ws.norms_event)
-        ws.norms_event = None
+    """Order torch's current stream after the decoder-norm finaliser the side stream ran (engine.adam), unless
+    it is that stream (the loss tail there is ordered by the stream itself and must not consume the wait that
+    G3 / G4G5 on the compute stream need)."""
+    if ws.norms_event is None:
+        return
+    cur = torch.cuda.current_stream(ws.x.device)
+    if cur == ws.norms_stream:
+        return
+    cur.wait_event(ws.norms_event)
+    ws.norms_event = None
 
 
 def decoder_norms(ws, P):
@@ -340,18 +350,20 @@ def loss_colpart(ws):
     return ws.loss_colpart[:ws.loss_col_rows]
 
 
-def loss_finalize(ws, l1l0_out=None):
-    """Loss scalars / EV vectors.  After a forward (which deferred the activation column sums) one
-    launch does both (cc_loss_tail); a re-formed loss (same activations) only the finaliser."""
+def loss_finalize(ws, l1l0_out=None, host=None, seq=0):
+    """Loss scalars / EV vectors.  After a forward (which left the l1 partials to be formed against the
+    decoder norms) one launch does both (cc_loss_tail); a re-formed loss (same activations) only the
+    finaliser.  host (a _hip.MappedHostBuffer): the scalars also land there, then `seq` in word 8."""
     wait_norms(ws)
     if ws.acts_pending:
-        ops.loss_tail(ws.acts_colpart, ws.h, None, ws.tn, ws.l1_part, _row_part(ws), ws.l0_part, ws.n_wave,
-                      ws.ev, ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], l1l0_out=l1l0_out,
+        ops.loss_tail(ws.colsum_acts, ws.tn, ws.l1_part, _row_part(ws), ws.l0_part, ws.n_wave, ws.ev, ws.ev_a,
+                      ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], l1l0_out=l1l0_out, host=host, seq=seq,
                       ncb=ws.row_ncb)
         ws.acts_pending = False
         return
     ops.loss_finalize(_row_part(ws), ws.l1_part, ws.n_l1, ws.l0_part, ws.n_wave, ws.ev, ws.ev_a, ws.ev_b, ws.scalars,
-                      ws.B, ws.n, ws.d, l1l0_out=l1l0_out, ncb=ws.row_ncb)
+                      ws.B, ws.n, ws.d, l1l0_out=l1l0_out, host=host, seq=seq,
+                      ncb=ws.row_ncb if ws.row_ncb is not None else ops.loss_col_blocks(ws.d))
 
 
 def loss_from_recon(ws, P, grad_scale=None):
@@ -364,20 +376,23 @@ def loss_from_recon(ws, P, grad_scale=None):
     loss_finalize(ws)
 
 
-def loss_finalize_beside(ws, side_stream, on_losses=None):
-    """loss_finalize (+ on_losses(ws.scalars), e.g. the host copy) on `side_stream`, after everything
+def loss_finalize_beside(ws, side_stream, on_losses=None, host=None, seq=0):
+    """loss_finalize (+ on_losses(ws.scalars), e.g. a host copy) on `side_stream`, after everything
     queued so far on torch's stream: the backward's G3 does not read the tail's outputs, so it starts
-    right after the loss kernel, and nothing on torch's stream reads the tail's outputs (G4's activation
-    column sums come from forward(); a cross-stream wait costs the waiting stream ~17-24 us even on a
-    completed event, profiles/r02_step_ab_prep_ahead.txt).  Returns the event that marks the tail's end."""
+    right after the loss kernel (the tail's workgroups fit beside G3's), and nothing on torch's stream
+    reads the tail's outputs (G4's activation column sums come from forward()).  host / seq: the scalars
+    go straight to mapped host memory (loss_finalize); then no event is recorded and None is returned,
+    else the event that marks the tail's end."""
     dev = ws.x.device
     ready = torch.cuda.Event()
     ready.record(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side_stream):
         side_stream.wait_event(ready)
-        loss_finalize(ws)
+        loss_finalize(ws, host=host, seq=seq)
         if on_losses is not None:
             on_losses(ws.scalars)
+        if host is not None and on_losses is None:
+            return None
         done = torch.cuda.Event()
         done.record(side_stream)
     return done
@@ -415,6 +430,8 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
     the same launch (segment_sums semantics, zero_mask), for the all-reduce."""
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
     l1_scale = float(l1_coeff) * l1_grad_weight / B
+    # (a deferred decoder-half Adam launch of the last step reads the clip coefficient this launch rewrites)
+    P.wait_pending()
     if not dacts_done:
         dacts_rows(ws, P, l1_coeff, 0, B, l1_grad_weight)
     if tail_done is not None:
@@ -485,6 +502,7 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
     overlaps the next step's prep / encoder GEMM (G1 reads only the encoder half); P.pending orders every
     later decoder-half use (forward() waits before G2; CrossCoder's accessors, FusedAdam.state and
     Trainer.synchronize() wait).  Without a side stream: one launch over the whole arena."""
+    P.wait_pending()  # (no deferred rows of an earlier step may read this step's coefficient)
     coef = ws.clip_out[0:1]
     emulate = ws.dtype == torch.bfloat16
 
@@ -543,6 +561,7 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
                         ops.dec_norms_finalize(ws.norm_part, ws.h, ws.n, ws.d, ws.norms, ws.tn, ws.inv_norms)
                     ws.norms_event = torch.cuda.Event()
                     ws.norms_event.record(side_stream)
+                    ws.norms_stream = side_stream
                 cur.wait_event(done)
 
             ws.norms_token = _norms_token(P)

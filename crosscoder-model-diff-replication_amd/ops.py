@@ -242,21 +242,16 @@ def loss_finalize(row_part, l1_part, n_l1, l0_part, n_l0, ev, ev_a, ev_b, scalar
                                  _ptr(ev_b), _ptr(scalars), _ptr(l1l0_out), B, n, d, _stream(row_part)))
 
 
-def loss_tail(acts_colpart, h, colsum_acts, tn, l1_part, row_part, l0_part, n_l0, ev, ev_a, ev_b, scalars, B, n, d,
-              counter, l1l0_out=None, host=None, seq=0, ncb=None):
-    """reduce_rows(acts_colpart, dot_w=tn, dot_part=l1_part) + loss_finalize as one launch (same bits);
-    colsum_acts None: the column sums are not stored (already formed), only the l1 dot partials."""
-    if ncb is not None:
-        check(lib().cc_loss_tail_nb(_ptr(acts_colpart), acts_colpart.shape[0], h, _ptr(colsum_acts), _ptr(tn),
-                                    _ptr(l1_part), _ptr(row_part), ncb, _ptr(l0_part), n_l0, _ptr(ev), _ptr(ev_a),
-                                    _ptr(ev_b), _ptr(scalars), _ptr(l1l0_out),
-                                    host.device_ptr if host is not None else None, seq, B, n, d, _ptr(counter),
-                                    _stream(acts_colpart)))
-        return
-    check(lib().cc_loss_tail(_ptr(acts_colpart), acts_colpart.shape[0], h, _ptr(colsum_acts), _ptr(tn), _ptr(l1_part),
-                             _ptr(row_part), _ptr(l0_part), n_l0, _ptr(ev), _ptr(ev_a), _ptr(ev_b), _ptr(scalars),
-                             _ptr(l1l0_out), host.device_ptr if host is not None else None, seq, B, n, d,
-                             _ptr(counter), _stream(acts_colpart)))
+def loss_tail(colsum_acts, tn, l1_part, row_part, l0_part, n_l0, ev, ev_a, ev_b, scalars, B, n, d, counter,
+              l1l0_out=None, host=None, seq=0, ncb=None):
+    """The l1 dot partials from the reduced activation column sums + loss_finalize as one launch whose
+    workgroups fit beside a persistent GEMM (cc_loss_tail; the same bits as reduce_rows(.., dot_part) +
+    loss_finalize).  ncb: row_part's column blocks per model (default loss_fwd_bwd's layout)."""
+    h = colsum_acts.numel()
+    check(lib().cc_loss_tail(_ptr(colsum_acts), _ptr(tn), h, _ptr(l1_part), _ptr(row_part),
+                             loss_col_blocks(d) if ncb is None else ncb, _ptr(l0_part), n_l0, _ptr(ev), _ptr(ev_a),
+                             _ptr(ev_b), _ptr(scalars), _ptr(l1l0_out), host.device_ptr if host is not None else None,
+                             seq, B, n, d, _ptr(counter), _stream(colsum_acts)))
 
 
 def grad_tail(gpre_colpart, g_b_enc, sq_b_enc, loss_colpart, g_b_dec, sq_b_dec, sq, offsets, max_norm, emulate_bf16,

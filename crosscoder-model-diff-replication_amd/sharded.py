@@ -342,15 +342,21 @@ class ShardedTrainer:
 
     def train(self):
         """trainer.py:69-82 over the shards (logging and checkpoints on rank 0).  The reference saves in a
-        `finally:`; here the final save runs only when the loop completed, because the save is a collective:
-        on an exception raised by one rank alone it would wait forever for the others."""
+        `finally:` (trainer.py:81-82).  Here the save is a collective, so it runs where every rank leaves the
+        loop the same way: on normal completion, and on KeyboardInterrupt (torchrun forwards SIGINT to every
+        rank), after which the interrupt is re-raised.  Any other exception may be one rank's alone: a save
+        would then wait forever for the others, so it propagates without the final checkpoint."""
         self.step_counter = 0
-        for i in range(self.total_steps):
-            loss_dict = self.step()
-            if i % self.cfg["log_every"] == 0:
-                self.log(loss_dict)
-            if (i + 1) % self.cfg["save_every"] == 0:
-                self.save()
+        try:
+            for i in range(self.total_steps):
+                loss_dict = self.step()
+                if i % self.cfg["log_every"] == 0:
+                    self.log(loss_dict)
+                if (i + 1) % self.cfg["save_every"] == 0:
+                    self.save()
+        except KeyboardInterrupt:
+            self.save()
+            raise
         self.save()
 
     def gather_state_dict(self, dst=None):

@@ -1,15 +1,15 @@
 """Drop-in `Trainer` (reference: trainer.py:7-82) whose `step()` is the fused HIP step.
 
 `step()` returns the reference's 9-key loss dict.  Per step it issues the fixed launch
-sequence of engine.py on one stream and copies the 6 loss scalars to the host once (the
-reference does 7 `.item()` syncs).  Adam state (exp_avg / exp_avg_sq, bf16 like the
+sequence of engine.py and reads the 6 loss scalars once, from mapped host memory the loss-tail
+kernel writes directly (the reference does 7 `.item()` syncs).  Adam state (exp_avg / exp_avg_sq, bf16 like the
 reference's) lives in arenas mirroring the parameter arena, exposed through
 `optimizer.state[param]` for inspection.
 """
 import torch
 import tqdm
 
-from . import engine
+from . import _hip, engine
 from .buffer import Buffer
 from .crosscoder import CrossCoder
 
@@ -86,7 +86,8 @@ class Trainer:
         self.scheduler = LambdaLRHost(self.optimizer, self.lr_lambda)
         self.step_counter = 0
         self.logger = logger
-        self._host = None  # pinned loss-scalar landing buffer (allocated on the first step)
+        self._mapped = None  # mapped host words the step's loss tail writes (allocated on the first step)
+        self._seq = 0
         self._side = None  # stream of the decoder half's Adam (created on the first step)
 
     def lr_lambda(self, step):
@@ -108,9 +109,10 @@ class Trainer:
         torch.cuda.current_stream(scalars.device).wait_event(done)
         return scalars
 
-    def _launch_step(self, on_losses):
-        """The step's launches; returns (ws.scalars, the event that marks the loss tail's end).  step()
-        does not order torch's stream after the tail (the host waits for the loss copy instead)."""
+    def _launch_step(self, on_losses, host=None, seq=0):
+        """The step's launches; returns (ws.scalars, the event that marks the loss tail's end, or None when
+        the tail writes the scalars to `host`, a _hip.MappedHostBuffer, and then `seq`).  step() does not
+        order torch's stream after the tail (the host waits for the sequence word instead)."""
         cc = self.crosscoder
         raw, factor = self.buffer.next_raw()
         raw = cc.pad_input(raw)  # (zero columns only when d_in % 8 != 0)
@@ -121,7 +123,7 @@ class Trainer:
         # prep, G1, G2 + the loss rows (one pass where decode_loss_t serves the shape)
         engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None, finalize=False)
         # the loss scalars (+ their host copy) on the side stream, beside G3 (read by nothing on this stream)
-        done = engine.loss_finalize_beside(ws, side, on_losses)
+        done = engine.loss_finalize_beside(ws, side, on_losses, host=host, seq=seq)
         l1c = self.get_l1_coeff()
         # clip_grad_norm_(max_norm=1.0), trainer.py:46
         engine.backward(ws, P, opt.grads, l1c, clip=1.0)
@@ -133,16 +135,6 @@ class Trainer:
         self.scheduler.step()
         self._last_l1c = l1c
         return ws.scalars, done
-
-    def _copy_losses(self, scalars):
-        # the step's single device->host copy, enqueued (on the side stream) as soon as the forward has
-        # produced the losses: the host waits for the forward only, and enqueues the next step while
-        # this step's backward / Adam still run
-        if self._host is None:
-            self._host = torch.empty(8, dtype=torch.float32, pin_memory=True)
-            self._copied = torch.cuda.Event()
-        self._host.copy_(scalars[:8], non_blocking=True)
-        self._copied.record()
 
     def _side_stream(self):
         # the decoder half of Adam (+ the next step's decoder norms / W_dec^T) runs here, beside the
@@ -158,9 +150,12 @@ class Trainer:
         self.crosscoder.arena().wait_pending()
 
     def step(self):
-        self._launch_step(self._copy_losses)
-        self._copied.synchronize()
-        s = self._host[:6].tolist()
+        if self._mapped is None:
+            self._mapped = _hip.MappedHostBuffer(16)
+        self._seq = (self._seq + 1) & 0xFFFFFFFF or 1
+        self._launch_step(None, host=self._mapped, seq=self._seq)
+        self._mapped.wait(8, self._seq)
+        s = [float(v) for v in self._mapped.f32[:6]]
         l1c = self._last_l1c
         dt = self.crosscoder.dtype
         l2, l1, l0 = s[0], rounded(s[1], dt), s[2]

@@ -166,7 +166,7 @@ int cc_loss_fwd_bwd_rows_t(const float* recon_f32, const void* b_dec, const void
  * g_recon / g_recon_t are bit-identical to the two-call form; the partial slabs use other blocks:
  *   row_part [2][n * ncb][B], ncb = cc_decode_loss_ncb(..) = d / 64 column blocks per model
  *   col_part [cc_col_part_rows(B)][K] (column sums of g_recon per 128-row group)
- * so their sums agree to fp32 reassociation (cc_loss_tail_nb / cc_loss_finalize_nb take ncb; the b_dec
+ * so their sums agree to fp32 reassociation (cc_loss_tail / cc_loss_finalize_nb take ncb; the b_dec
  * gradient sums cc_col_part_rows(B) rows).  ws: cc_decode_ws_floats(B, h, n*d, dtype) floats.
  * bf16, B % 8 == 0, d % 64 == 0; cc_decode_loss_ncb returns 0 for shapes this entry does not serve. */
 int64_t cc_decode_loss_ncb(int64_t B, int64_t h, int64_t n, int64_t d, int dtype);
@@ -195,30 +195,26 @@ int cc_loss_finalize_mapped(const float* row_part, const float* l1_part, int64_t
                             int64_t n_l0, float* ev, float* ev_a, float* ev_b, float* scalars, float* l1l0_out,
                             float* host_out, uint32_t seq, int64_t B, int64_t n, int64_t d, void* stream);
 
-/* One launch for the forward's tail (crosscoder.py:106-128): cc_reduce_rows of the activation
- * column-sum partials acts_colpart [R x h] into colsum_acts [h] (= sum_b acts) with the L1 dot
- * partials l1_part [cc_reduce_parts(h)] against tn [h], the per-row EV terms, and the loss scalars
- * -- bit-identical to cc_reduce_rows(.., dot_w = tn, dot_part = l1_part) followed by
- * cc_loss_finalize[_mapped](.., n_l1 = cc_reduce_parts(h), ..).  The last block to finish runs the
- * scalar finaliser; `counter` is one device uint32, zero before the first call, left zero by
- * every call (launches sharing a counter must be ordered, e.g. one stream).  host_out may be NULL;
- * colsum_acts may be NULL (the column sums already formed by cc_reduce_rows: only the l1 dot
- * partials, the same bits). */
-int cc_loss_tail(const float* acts_colpart, int64_t R, int64_t h, float* colsum_acts, const float* tn,
-                 float* l1_part, const float* row_part, const float* l0_part, int64_t n_l0, float* ev, float* ev_a,
-                 float* ev_b, float* scalars, float* l1l0_out, float* host_out, uint32_t seq, int64_t B, int64_t n,
-                 int64_t d, uint32_t* counter, void* stream);
-
-/* cc_loss_finalize_mapped / cc_loss_tail over a row_part of `ncb` column blocks per model (the
- * producer's layout: cc_loss_col_blocks(d) for cc_loss_fwd_bwd*, cc_decode_loss_ncb for
- * cc_decode_loss_t).  host_out may be NULL. */
+/* cc_loss_finalize_mapped over a row_part of `ncb` column blocks per model (the producer's layout:
+ * cc_loss_col_blocks(d) for cc_loss_fwd_bwd*, cc_decode_loss_ncb for cc_decode_loss_t).  host_out may
+ * be NULL. */
 int cc_loss_finalize_nb(const float* row_part, int64_t ncb, const float* l1_part, int64_t n_l1,
                         const float* l0_part, int64_t n_l0, float* ev, float* ev_a, float* ev_b, float* scalars,
                         float* l1l0_out, float* host_out, uint32_t seq, int64_t B, int64_t n, int64_t d, void* stream);
-int cc_loss_tail_nb(const float* acts_colpart, int64_t R, int64_t h, float* colsum_acts, const float* tn,
-                    float* l1_part, const float* row_part, int64_t ncb, const float* l0_part, int64_t n_l0, float* ev,
-                    float* ev_a, float* ev_b, float* scalars, float* l1l0_out, float* host_out, uint32_t seq,
-                    int64_t B, int64_t n, int64_t d, uint32_t* counter, void* stream);
+
+/* One launch for the forward's tail (crosscoder.py:106-128): the L1 dot partials
+ * l1_part[j] = sum over the 64 latents of block j of colsum_acts * tn (colsum_acts [h] = sum_b acts,
+ * formed by cc_reduce_rows from the encoder's column slab), the per-row EV terms of row_part (`ncb`
+ * column blocks per model) and the loss scalars -- bit-identical to cc_reduce_rows(.., dot_w = tn,
+ * dot_part = l1_part) followed by cc_loss_finalize_nb(.., n_l1 = cc_reduce_parts(h), ..).  Its
+ * workgroups (256 threads, few registers, < 0.5 KB of LDS) fit beside a persistent GEMM launch's, so a
+ * side stream can run it during the backward's first GEMM.  The last workgroup to finish runs the
+ * scalar finaliser; `counter` is one device uint32, zero before the first call, left zero by every
+ * call (launches sharing a counter must be ordered, e.g. one stream).  host_out may be NULL. */
+int cc_loss_tail(const float* colsum_acts, const float* tn, int64_t h, float* l1_part, const float* row_part,
+                 int64_t ncb, const float* l0_part, int64_t n_l0, float* ev, float* ev_a, float* ev_b, float* scalars,
+                 float* l1l0_out, float* host_out, uint32_t seq, int64_t B, int64_t n, int64_t d, uint32_t* counter,
+                 void* stream);
 
 /* Backward through decode + L1 + ReLU (autograd of crosscoder.py:77,84-89,126):
  * g_pre[B,h] = (g_recon . W_dec^T + l1_scale * tn[h]) * (acts > 0),  l1_scale = l1_coeff / B.

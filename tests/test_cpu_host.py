@@ -52,7 +52,7 @@ def test_library_exports_only_the_header():
     kernel handles); the test-only debug build adds only its launch-form setters."""
     syms = set(declared_symbols())
     assert _dynamic_exports(_lib.LIB_PATH) == syms
-    assert _dynamic_exports(_lib.DEBUG_LIB_PATH) == syms | set(_lib.DEBUG_SETTERS)
+    assert _dynamic_exports(_lib.DEBUG_LIB_PATH) == syms | set(_lib.DEBUG_SETTERS) | {"cc_debug_spin"}
 
 
 def test_argument_validation_without_gpu():
@@ -81,12 +81,14 @@ def test_argument_validation_without_gpu():
                             null) == 3                                                           # R_enc = 0
     assert lib.cc_grad_tail(fake, 16, 256, fake, fake, fake, 128, 64, fake, fake, 1, fake, off, 9, 1.0, 1, fake, fake,
                             null) == 3                                                           # nparams > 8
-    assert lib.cc_loss_tail(fake, 16, 256, fake, fake, fake, fake, fake, 8, fake, fake, fake, fake, null, null, 0, 64,
-                            2, 32, null, null) == 1                                              # no counter
-    assert lib.cc_loss_tail(fake, 16, 256, fake, fake, fake, fake, fake, 8, fake, fake, fake, fake, null, null, 0, 0,
-                            2, 32, fake, null) == 3                                              # empty batch
-    assert lib.cc_loss_tail_nb(fake, 16, 256, fake, fake, fake, fake, 0, fake, 8, fake, fake, fake, fake, null, null,
-                               0, 64, 2, 32, fake, null) == 3                                    # ncb = 0
+    assert lib.cc_loss_tail(fake, fake, 256, fake, fake, 36, fake, 8, fake, fake, fake, fake, null, null, 0, 64, 2,
+                            32, null, null) == 1                                                 # no counter
+    assert lib.cc_loss_tail(null, fake, 256, fake, fake, 36, fake, 8, fake, fake, fake, fake, null, null, 0, 64, 2,
+                            32, fake, null) == 1                                                 # no column sums
+    assert lib.cc_loss_tail(fake, fake, 256, fake, fake, 36, fake, 8, fake, fake, fake, fake, null, null, 0, 0, 2,
+                            32, fake, null) == 3                                                 # empty batch
+    assert lib.cc_loss_tail(fake, fake, 256, fake, fake, 0, fake, 8, fake, fake, fake, fake, null, null, 0, 64, 2,
+                            32, fake, null) == 3                                                 # ncb = 0
     assert lib.cc_loss_finalize_nb(null, 36, fake, 8, fake, 8, fake, fake, fake, fake, null, null, 0, 64, 2, 32,
                                    null) == 1
     # G2 + loss in one pass (cc_decode_loss_t): served shapes, checks before any launch

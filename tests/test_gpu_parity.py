@@ -515,6 +515,40 @@ def test_decoder_adam_split_is_bit_identical(gpu, side_rows, monkeypatch):
     assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
 
 
+def test_delayed_norm_finaliser_still_orders_g3_and_wgrad(gpu, dbg_lib, monkeypatch):
+    """The decoder norms of a step come from a finaliser on the side stream (engine.adam's deferred rest);
+    G3 (reads tn) and G4G5 (reads inv_norms) run on the compute stream.  With the finaliser held back 3 ms
+    (a spin kernel queued before it on its stream: it then ends long after G2), both must still read the new
+    norms: losses, params and both moments equal an undelayed run's bit for bit."""
+    import ctypes
+
+    from crosscoder_amd import engine, ops
+    B, n, d, h = 1024, 2, 256, 2048
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+               num_tokens=B * 20, device=str(gpu))
+    orig = ops.dec_norms_finalize
+    outs = []
+    for delay_ns in (0, 3_000_000):
+        def finalize(*a, _ns=delay_ns, **k):
+            if _ns:
+                ops.check(dbg_lib.cc_debug_spin(1, 0, _ns, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+            orig(*a, **k)
+
+        monkeypatch.setattr(ops, "dec_norms_finalize", finalize)
+        cc = ca.CrossCoder(cfg)
+        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 4, seed=5), crosscoder=cc)
+        dicts = [tr.step() for _ in range(4)]
+        assert cc.arena().pending_rest is not None and engine.wait_norms is not None
+        st = tr.optimizer.state
+        m = torch.cat([st[p]["exp_avg"].detach().flatten().float() for p in cc.parameters()])
+        v = torch.cat([st[p]["exp_avg_sq"].detach().flatten().float() for p in cc.parameters()])
+        torch.cuda.synchronize()
+        outs.append((dicts, cc.arena().data.clone(), m, v))
+    (d0, p0, m0, v0), (d1, p1, m1, v1) = outs
+    assert d0 == d1
+    assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+
+
 def test_full_size_config2_trainer_steps_match_oracle(gpu, full_size_case):
     """BASELINE config 2 through the shipped schedule (Trainer.step: fused G2 + loss, G4G5 + grad tail + clip
     in one launch, encoder / decoder Adam halves on two streams) vs the oracle's fp32 OracleTrainer.step
@@ -1219,10 +1253,10 @@ def test_baseline_config_shapes_spot_check(gpu, B, n, d, h):
 @pytest.mark.parametrize("enc_dtype,B,n,d,h", [("bf16", 1024, 2, 256, 2048), ("fp32", 96, 2, 40, 200),
                                                ("bf16", 512, 4, 64, 384), ("fp32", 256, 2, 64, 1000)])
 def test_fused_tails_match_separate_launches(gpu, enc_dtype, B, n, d, h):
-    """The one-launch loss tail (acts column sums + l1 partials + EV + loss scalars, cc_loss_tail) and
-    grad tail (bias-gradient sums + clip coefficient, cc_grad_tail) the step runs equal the separate
-    reduce_rows / loss_finalize / clip_finalize launches bit for bit, and leave their arrival counters
-    at zero; the mapped-host form of the loss finaliser delivers the same scalars + sequence word."""
+    """The one-launch loss tail (l1 partials from the activation column sums + EV + loss scalars,
+    cc_loss_tail) and grad tail (bias-gradient sums + clip coefficient, cc_grad_tail) the step runs equal
+    the separate reduce_rows / loss_finalize / clip_finalize launches bit for bit, and leave their arrival
+    counters at zero; the mapped-host forms of both loss finalisers deliver the same scalars + sequence word."""
     from crosscoder_amd import _hip
 
     cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype=enc_dtype,
@@ -1249,6 +1283,11 @@ def test_fused_tails_match_separate_launches(gpu, enc_dtype, B, n, d, h):
     sc2 = f32(ws.scalars)
     ops.loss_finalize(rp, l1p, ws.n_l1, ws.l0_part, ws.n_wave, f32(ev), f32(ev), f32(ev), sc2, B, n, d,
                       host=host, seq=7, ncb=ws.row_ncb)
+    # the fused tail again, into mapped host memory (the Trainer's path)
+    host2 = _hip.MappedHostBuffer(16)
+    l1p2, sc3 = f32(l1p), f32(ws.scalars)
+    ops.loss_tail(ws.colsum_acts, ws.tn, l1p2, rp, ws.l0_part, ws.n_wave, f32(ev), f32(ev), f32(ev), sc3, B, n, d,
+                  ws.tail_ctr[0:1], host=host2, seq=9, ncb=ws.row_ncb)
     # grad side, separately
     sq = ws.sq.clone()
     gbe, gbd = torch.empty_like(G.b_enc), torch.empty_like(G.b_dec_flat)
@@ -1259,9 +1298,14 @@ def test_fused_tails_match_separate_launches(gpu, enc_dtype, B, n, d, h):
     ops.clip_finalize(sq, o, 1.0, cc.dtype == torch.bfloat16, clip)
     torch.cuda.synchronize()
     host.wait(8, 7)
+    host2.wait(8, 9)
+    assert not bool(ws.tail_ctr.any())
     for x, y in ((colsum, ws.colsum_acts), (l1p, ws.l1_part), (ev, ws.ev), (ev_a, ws.ev_a), (ev_b, ws.ev_b),
-                 (sc[:6], ws.scalars[:6]), (sq, ws.sq), (gbe, G.b_enc), (gbd, G.b_dec_flat)):
+                 (sc[:6], ws.scalars[:6]), (sq, ws.sq), (gbe, G.b_enc), (gbd, G.b_dec_flat), (l1p2, l1p),
+                 (sc3[:6], sc[:6])):
         assert torch.equal(x, y)
+    for hb in (host, host2):
+        assert torch.equal(torch.from_numpy(hb.f32[:6].copy()), sc[:6].cpu())
     # where the step ran G4 + G5 + the grad tail as one launch (cc_wgrad_both_clip_t), its finaliser
     # accumulates the same fp64 squared sums with 512 instead of 1024 threads
     if ws.tr:

@@ -280,3 +280,40 @@ def test_sharded_init_is_reference_slice_and_gathers_back(enc_dtype, d_in, tmp_p
     ref = ca.CrossCoder(cfg).reference_state_dict()
     for k in ref:
         assert torch.equal(sd[k], ref[k]) and sd[k].stride() == ref[k].stride(), k
+
+
+def test_sharded_train_final_save_on_interrupt_only():
+    """ShardedTrainer.train keeps the reference's final save (trainer.py:81-82) where every rank leaves the loop
+    the same way: normal completion and KeyboardInterrupt (re-raised after the save); another exception, which
+    may be one rank's alone, propagates without the collective save."""
+
+    class Loop:
+        total_steps = 6
+        cfg = {"log_every": 100, "save_every": 1000}
+
+        def __init__(self, fail_at=None, exc=KeyboardInterrupt):
+            self.n, self.saved, self.fail_at, self.exc = 0, 0, fail_at, exc
+
+        def step(self):
+            self.n += 1
+            if self.n == self.fail_at:
+                raise self.exc()
+            return {}
+
+        def log(self, d):
+            pass
+
+        def save(self):
+            self.saved += 1
+
+    done = Loop()
+    sharded.ShardedTrainer.train(done)
+    assert (done.n, done.saved) == (6, 1)
+    interrupted = Loop(fail_at=3)
+    with pytest.raises(KeyboardInterrupt):
+        sharded.ShardedTrainer.train(interrupted)
+    assert (interrupted.n, interrupted.saved) == (3, 1)
+    failed = Loop(fail_at=3, exc=RuntimeError)
+    with pytest.raises(RuntimeError):
+        sharded.ShardedTrainer.train(failed)
+    assert failed.saved == 0
