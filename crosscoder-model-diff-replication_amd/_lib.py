@@ -59,10 +59,11 @@ SIGNATURES = {
     "cc_wgrad_dec": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_enc": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_both_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
+    "cc_wgrad_tile_sums": (_i64, [_i64, _i64]),
     "cc_wgrad_both_clip_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p,
-                                  _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_i64), _i, _f, _i, _p, _p, _p, _i, _p]),
+                                  _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_i64), _i, _f, _i, _p, _p, _p, _p, _i, _p]),
     "cc_wgrad_both_sums_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p,
-                                  _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_i64), _i, _i, _p, _p, _p, _i, _p]),
+                                  _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_i64), _i, _i, _p, _p, _p, _p, _i, _p]),
     "cc_wgrad_both": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_clip_finalize": (_i, [_p, ctypes.POINTER(_i64), _i, _f, _i, _p, _p]),
     "cc_grad_tail": (_i, [_p, _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _i, _p, ctypes.POINTER(_i64), _i, _f, _i, _p,
@@ -77,9 +78,9 @@ SIGNATURES = {
     "cc_decode_loss_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_decode_loss": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_transposed_ok": (_i, [_i64, _i64, _i64, _i]),
-    "cc_encode_fwd_t": (_i, [_p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_encode_fwd_t": (_i, [_p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_mask_bits_words": (_i64, [_i64, _i64]),
-    "cc_dacts_bwd_t": (_i, [_p, _p, _p, _p, _f, _p, _p, _i64, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_dacts_bwd_t": (_i, [_p, _p, _p, _p, _f, _p, _p, _i64, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_transpose_b16": (_i, [_p, _i64, _i64, _i64, _p, _i64, _p]),
     "cc_dec_norms_part_floats": (_i64, [_i64, _i64, _i64]),
     "cc_transpose_dec_norms": (_i, [_p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p]),

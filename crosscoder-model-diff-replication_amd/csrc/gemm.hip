@@ -63,6 +63,7 @@ struct GemmArgs {
   float* row_part;      // EPI_DLOSS: loss row terms [2][n * d/64][M]
   uint32_t* mask_bits;  // ping-pong EPI_ENC (out) / EPI_DACTS FAST (in): the activation mask, 1 bit per output
                         // in accumulator order: [tile tm*nbn + tn][thread][4] u32, bit 4(4i+j)+e of fragment (i,j)
+  uint32_t* tile_ctr;   // persistent ping-pong launches: 8 per-XCD tile counters (dynamic order), NULL: static
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -552,17 +553,18 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 //   (1) before its first tile, 256-thread group g of workgroup b runs bias reduction blocks
 //       2b + g, 2b + g + 2 * grid, ... (b_enc.grad / b_dec.grad column sums of the G3 / loss partial
 //       slabs + their sq partials: reduce_rows_phase1/2, the bits cc_grad_tail writes);
-//   (2) the dual tile loop of gemm_pp_dual_kernel;
-//   (3) every workgroup sums, per parameter, the squared-sum partials of its own tiles and bias blocks
-//       (fixed order) into wg_part[workgroup][4]; the last workgroup to arrive (device-scope arrival
-//       counter, reset by it for the next launch) combines those (one load per thread instead of a
-//       pass over the whole per-tile slab after its L2 invalidate) into clip_grad_norm_'s coefficient.
+//   (2) the dual tile loop of gemm_pp_dual_kernel (static or dynamic order, TileLoop); after each tile the
+//       8 waves' squared-sum partials are added in wave order through LDS into tile_sum[tile];
+//   (3) the last workgroup to arrive (device-scope arrival counter, reset by it for the next launch) sums,
+//       per parameter, tile_sum over the tiles (G5 -> W_enc, G4 -> W_dec) and the bias blocks' partials in a
+//       fixed order -- whichever workgroups ran which tiles, the same bits -- into clip_grad_norm_'s
+//       coefficient.
 struct WgradTail {
   RedSeg red[2];
   int red_blocks[2];
   ClipArgs clip;
   unsigned* counter;
-  float* wg_part;  // [grid][4]: W_enc, W_dec, b_enc, b_dec (the order of sq's segments)
+  float* tile_sum;  // [2 * nb0]: the per-tile squared sums, dW_dec's tiles first
 };
 
 template <bool AKC, bool BKC, int EPI0, int EPI1>
@@ -583,39 +585,26 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmAr
     }
   }
   const int nb0 = a0.nbm * a0.nbn;
-  for (int t = blockIdx.x; t < 2 * nb0; t += gridDim.x) {
+  float* wsum_lds = (float*)(smem + PP_SLOT + 64);  // (beside the claim word: free until the next prologue barrier)
+  const int wave = threadIdx.x >> 6;
+  for (TileLoop L(2 * nb0, a0.tile_ctr); L.more();) {
+    const int t = L.begin();
     const int tid = pp_opaque_tid();
-    if (t < nb0) pp_tile<AKC, BKC, EPI0>(a0, smem, t, tid);
-    else pp_tile<AKC, BKC, EPI1>(a1, smem, t - nb0, tid);
+    float w;
+    if (t < nb0) w = pp_tile<AKC, BKC, EPI0>(a0, smem, t, tid);
+    else w = pp_tile<AKC, BKC, EPI1>(a1, smem, t - nb0, tid);
     pp_tile_boundary();
-  }
-  // this workgroup's squared sums per parameter: its tiles' per-wave partials (G5 -> W_enc, G4 -> W_dec)
-  // and its bias blocks' partials, written by its own waves (visible after their stores drained + the barrier)
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    double s[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int k = lane >> 3;; k += 8) {  // lane: partial (lane & 7) of own tiles k = lane/8, +8, ...
-      const int t = (int)blockIdx.x + k * (int)gridDim.x;
-      if (t >= 2 * nb0) break;
-      if (t < nb0) s[1] += (double)a0.wave_part0[t * 8 + (lane & 7)];
-      else s[0] += (double)a1.wave_part0[(t - nb0) * 8 + (lane & 7)];
-    }
-    const int nred = tl.red_blocks[0] + tl.red_blocks[1];
-    for (int k = lane;; k += 64) {  // own bias blocks 2b + g + 2 * grid * i
-      const int blk = 2 * (int)blockIdx.x + (k & 1) + 2 * (int)gridDim.x * (k >> 1);
-      if (blk >= nred) break;
-      if (blk < tl.red_blocks[0]) s[2] += (double)tl.red[0].sq_part[blk];
-      else s[3] += (double)tl.red[1].sq_part[blk - tl.red_blocks[0]];
-    }
+    if ((threadIdx.x & 63) == 0) wsum_lds[wave] = w;
+    L.advance(smem);
+    if (!L.ctr) __syncthreads();  // (the dynamic advance has its own barrier)
+    if (threadIdx.x == 0) {
+      float s = 0.f;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const double v = wave_sum_d(s[p]);
-      if (lane == 0) tl.wg_part[blockIdx.x * 4 + p] = (float)v;
+      for (int k = 0; k < 8; ++k) s += wsum_lds[k];
+      tl.tile_sum[t] = s;
     }
   }
-  // publish: wave 0's stores drained, the barrier joins the waves, ONE agent-scope release writes this
+  // publish: the tile sums' stores drained, the barrier joins the waves, ONE agent-scope release writes this
   // XCD's L2 back before the arrival count
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
@@ -629,10 +618,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmAr
   __syncthreads();
   if (!*last) return;
   {
+    // fixed order: thread j adds each GEMM's tiles j, j + NTHR, ... and bias blocks j, j + NTHR, ...;
+    // clip_finish combines the threads in a fixed order
     double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int w = threadIdx.x; w < (int)gridDim.x; w += NTHR)
-#pragma unroll
-      for (int p = 0; p < 4; ++p) s[p] += (double)tl.wg_part[w * 4 + p];
+    for (int k = threadIdx.x; k < nb0; k += NTHR) s[1] += (double)tl.tile_sum[k];
+    for (int k = threadIdx.x; k < nb0; k += NTHR) s[0] += (double)tl.tile_sum[nb0 + k];
+    for (int k = threadIdx.x; k < tl.red_blocks[0]; k += NTHR) s[2] += (double)tl.red[0].sq_part[k];
+    for (int k = threadIdx.x; k < tl.red_blocks[1]; k += NTHR) s[3] += (double)tl.red[1].sq_part[k];
     clip_finish<NTHR>(tl.clip, s, (double(*)[NTHR / 64])(smem + 64),
                       (float*)(smem + 64 + 8 * (NTHR / 64) * sizeof(double)));
   }
@@ -785,6 +777,7 @@ int64_t cc_col_part_rows(int64_t M) { return 2 * ((M + BM - 1) / BM); }
 int64_t cc_wave_parts(int64_t M, int64_t N) { return 8 * n_blocks(M, N, 256); }
 // exactly the partials the weight-gradient GEMMs write (the clip sums all of them)
 int64_t cc_wgrad_parts(int64_t h, int64_t K, int dtype) { return 8 * n_blocks(h, K, pick_bn(K, false, false, dtype)); }
+int64_t cc_wgrad_tile_sums(int64_t h, int64_t K) { return 2 * n_blocks(h, K, 256); }
 
 int cc_gemm_f32out(const void* A, int a_layout, int64_t lda, const void* Bm, int b_layout, int64_t ldb, float* C,
                    int64_t ldc, int64_t M, int64_t N, int64_t K, int dtype, void* stream) {
@@ -823,8 +816,8 @@ int cc_encode_fwd(const void* x, const void* W_enc, const void* b_enc, const flo
 int64_t cc_mask_bits_words(int64_t B, int64_t h) { return n_blocks(B, h, 256) * NTHR * 4; }
 
 int cc_encode_fwd_t(const void* x, const void* W_enc, const void* b_enc, const float* tn, void* acts, void* acts_t,
-                    int apply_relu, float* colsum_part, float* l1_part, float* l0_part, uint32_t* mask_bits, int64_t B,
-                    int64_t K, int64_t h, int dtype, void* stream) {
+                    int apply_relu, float* colsum_part, float* l1_part, float* l0_part, uint32_t* mask_bits,
+                    uint32_t* tile_ctr, int64_t B, int64_t K, int64_t h, int dtype, void* stream) {
   if (!acts || !acts_t) return CC_ERR_NULL;
   if (l1_part && !tn) return CC_ERR_NULL;
   GemmArgs a = {};
@@ -832,7 +825,7 @@ int cc_encode_fwd_t(const void* x, const void* W_enc, const void* b_enc, const f
   a.M = (int)B; a.N = (int)h; a.K = (int)K;
   a.out = acts; a.ldo = h; a.bias = b_enc; a.tn = tn; a.flag = apply_relu;
   a.col_part = colsum_part; a.wave_part0 = l1_part; a.wave_part1 = l0_part;
-  a.out_t = acts_t; a.ldt = B; a.mask_bits = mask_bits;
+  a.out_t = acts_t; a.ldt = B; a.mask_bits = mask_bits; a.tile_ctr = tile_ctr;
   int rc = check_gemm(a, dtype, true, true);
   if (rc) return rc;
   if (B % 8 || !al16(acts_t) || !use_pp(a.N, true, true, dtype)) return CC_ERR_SHAPE;
@@ -1190,14 +1183,15 @@ extern "C" {
 // cc_dacts_bwd storing d pre-activations TRANSPOSED only: g_pre_t[j][b] for b < B (row stride ldt
 // >= B; a batch slice passes g_pre_t + r0).  bf16, B % 8 == 0, ldt % 8 == 0, ping-pong path only.
 int cc_dacts_bwd_t(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
-                   const uint32_t* mask_bits, void* g_pre_t, int64_t ldt, float* colsum_part, int64_t B, int64_t K,
-                   int64_t h, int dtype, void* stream) {
+                   const uint32_t* mask_bits, void* g_pre_t, int64_t ldt, float* colsum_part, uint32_t* tile_ctr,
+                   int64_t B, int64_t K, int64_t h, int dtype, void* stream) {
   if (!g_pre_t || !acts) return CC_ERR_NULL;
   GemmArgs a = {};
   a.A = g_recon; a.lda = K; a.B = W_dec; a.ldb = K;
   a.M = (int)B; a.N = (int)h; a.K = (int)K;
   a.out = nullptr; a.ldo = h; a.mask_src = acts; a.tn = tn; a.scale0 = l1_scale;
   a.col_part = colsum_part; a.out_t = g_pre_t; a.ldt = ldt; a.mask_bits = const_cast<uint32_t*>(mask_bits);
+  a.tile_ctr = tile_ctr;
   int rc = check_gemm(a, dtype, true, true);
   if (rc) return rc;
   if (mask_bits && !al16(mask_bits)) return CC_ERR_ALIGN;
@@ -1281,10 +1275,11 @@ static int wgrad_both_tail(const void* actsT, const void* g_reconT, const void* 
                            const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
                            const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
                            const int64_t* off, int nparams, float max_norm, int emulate_bf16, int sums_only,
-                           int zero_mask, float* out, uint32_t* counter, float* wg_part, int dtype, void* stream) {
+                           int zero_mask, float* out, uint32_t* counter, float* tile_sum, uint32_t* tile_ctr,
+                           int dtype, void* stream) {
   const int64_t K = n * d;
   if (!gpre_colpart || !g_b_enc || !sq_b_enc || !loss_colpart || !g_b_dec || !sq_b_dec || !sq || !off || !out ||
-      !counter || !wg_part)
+      !counter || !tile_sum)
     return CC_ERR_NULL;
   if (R_enc <= 0 || R_dec <= 0) return CC_ERR_SHAPE;
   if (nparams != 4) return CC_ERR_SHAPE;  // W_enc, W_dec, b_enc, b_dec: the segments of sq
@@ -1320,9 +1315,9 @@ static int wgrad_both_tail(const void* actsT, const void* g_reconT, const void* 
   tl.clip.sums_only = sums_only;
   tl.clip.zero_mask = zero_mask;
   tl.counter = counter;
-  tl.wg_part = wg_part;
+  tl.tile_sum = tile_sum;
+  a0.tile_ctr = tile_ctr;
   const int grid = pp_grid(2 * a0.nbm * a0.nbn);
-  if (grid > CC_WG_PART_MAX) return CC_ERR_SHAPE;
   hipLaunchKernelGGL((gemm_pp_dual_tail_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(grid), dim3(NTHR), 0,
                      (hipStream_t)stream, a0, a1, tl);
   CC_LAUNCH_CHECK();
@@ -1335,11 +1330,11 @@ int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_
                          const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
                          const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
                          const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
-                         uint32_t* counter, float* wg_part, int dtype, void* stream) {
+                         uint32_t* counter, float* tile_sum, uint32_t* tile_ctr, int dtype, void* stream) {
   return wgrad_both_tail(actsT, g_reconT, W_dec, inv_norms, colsum_acts, l1_scale, grad_W_dec, sq_dec, g_preT, xT,
                          grad_W_enc, sq_enc, B, h, n, d, gpre_colpart, R_enc, g_b_enc, sq_b_enc, loss_colpart, R_dec,
-                         g_b_dec, sq_b_dec, sq, off, nparams, max_norm, emulate_bf16, 0, 0, clip_out, counter, wg_part,
-                         dtype, stream);
+                         g_b_dec, sq_b_dec, sq, off, nparams, max_norm, emulate_bf16, 0, 0, clip_out, counter, tile_sum,
+                         tile_ctr, dtype, stream);
 }
 
 int cc_wgrad_both_sums_t(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
@@ -1347,12 +1342,12 @@ int cc_wgrad_both_sums_t(const void* actsT, const void* g_reconT, const void* W_
                          const void* xT, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
                          const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
                          const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
-                         const int64_t* off, int nparams, int zero_mask, float* out, uint32_t* counter, float* wg_part,
-                         int dtype, void* stream) {
+                         const int64_t* off, int nparams, int zero_mask, float* out, uint32_t* counter, float* tile_sum,
+                         uint32_t* tile_ctr, int dtype, void* stream) {
   return wgrad_both_tail(actsT, g_reconT, W_dec, inv_norms, colsum_acts, l1_scale, grad_W_dec, sq_dec, g_preT, xT,
                          grad_W_enc, sq_enc, B, h, n, d, gpre_colpart, R_enc, g_b_enc, sq_b_enc, loss_colpart, R_dec,
-                         g_b_dec, sq_b_dec, sq, off, nparams, 0.f, 0, 1, zero_mask, out, counter, wg_part, dtype,
-                         stream);
+                         g_b_dec, sq_b_dec, sq, off, nparams, 0.f, 0, 1, zero_mask, out, counter, tile_sum, tile_ctr,
+                         dtype, stream);
 }
 
 int cc_wgrad_both(const void* acts, const void* g_recon, const void* W_dec, const float* inv_norms,

@@ -334,8 +334,10 @@ CC_DEV void dloss_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::T
 // cols: EpiCols loaded by the caller (EPI_ENC / EPI_DACTS; otherwise unread).
 // cw: dW_dec L1-term factors loaded by the caller (wgdec_factors; EPI_WGDEC with l1_scale != 0
 // only, otherwise unread).  Passed by reference so they stay in registers.
+// Returns the wave's squared-sum partial of a weight-gradient tile (what it stores at wave_part0[wave_slot],
+// every lane), 0 for the other epilogues.
 template <int DT, int EPI, int BNT, bool FAST = false, class IO>
-CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN],
+CC_DEV float epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN],
                           const FragGeom<BNT>& fg, const IO& io, int tm, int m0, int n0, int wr, int lane,
                           int wave_slot, const EpiCols<DT, BNT>& cols,
                           const float (&cw)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN]) {
@@ -399,8 +401,10 @@ CC_DEV void epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
     if (args.wave_part0) {
       float t = wave_sum(sq);
       if (lane == 0) args.wave_part0[wave_slot] = t;
+      return t;
     }
   }
+  return 0.f;
 }
 
 template <int DT, int EPI, int BNT>

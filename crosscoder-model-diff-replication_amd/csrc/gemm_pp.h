@@ -154,7 +154,7 @@ CC_DEV void pp_store_transposed(const GemmArgs& args, const char* smem, const in
 }
 
 template <int EPI, bool FAST>
-CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char* smem, const int (&qb)[4],
+CC_DEV float pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char* smem, const int (&qb)[4],
                             bool input_staged, int tm, int m0, int n0, int wr, int wc, int lane, int wave,
                             int wave_slot, const FragGeom<256>& fg, const EpiCols<CC_BF16, 256>& ecols) {
   const int rows = args.M - m0, cols = args.N - n0, ldo = (int)args.ldo;
@@ -180,7 +180,8 @@ CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char
     __builtin_amdgcn_s_barrier();
   }
   const LdsIO io(smem, qb, wr, wc, lane);
-  epilogue_core<CC_BF16, EPI, 256, FAST>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, ecols, cw);
+  const float wsum = epilogue_core<CC_BF16, EPI, 256, FAST>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, ecols,
+                                                            cw);
   __syncthreads();
   if (args.out) {
     const __amdgpu_buffer_rsrc_t rout = tile_rsrc(args.out, args.ldo, m0, n0, args.M, args.N, 2);
@@ -193,6 +194,7 @@ CC_DEV void pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char
     }
   }
   if (args.out_t) pp_store_transposed(args, smem, qb, m0, n0, rows, cols, lane, wave);
+  return wsum;
 }
 
 constexpr int PP_LDS = 4 * 256 * 128;  // 2 buffers x (A | B) K-step images
@@ -201,8 +203,9 @@ constexpr int PP_LDS_W = PP_LDS + 256 * 128;
 
 // One output tile of one GEMM; bid = the tile's block index within that GEMM's grid.  FAST: every tile
 // of the launch lies inside the matrix and the ReLU is on (EPI_ENC / EPI_DACTS epilogue fast form).
+// Returns the wave's squared-sum partial of a weight-gradient tile (epilogue_core), else 0.
 template <bool AKC, bool BKC, int EPI, bool FAST = false>
-CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadIdx.x) {
+CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadIdx.x) {
   using WG = WaveGeom<256>;
   static_assert(WG::TM == 8 && WG::TN == 4, "ping-pong geometry");
   constexpr int TILE = 256 * 128;  // one operand's K-step image
@@ -412,15 +415,30 @@ CC_DEV void pp_tile(const GemmArgs& args, char* smem, int bid, int tid = threadI
     gemm_epilogue<CC_BF16, EPI, 256>(args, acc, tm, m0, n0, wr, wc, lane, bid * 8 + wave);
   } else {  // (the host routes N % 8 != 0 to gemm_kernel)
     __builtin_amdgcn_s_barrier();  // every wave's zero-fill DMAs landed: the LDS is free
-    pp_epilogue_lds<EPI, FAST>(args, acc, smem, qb, pf, tm, m0, n0, wr, wc, lane, wave, bid * 8 + wave, fg, evec);
+    return pp_epilogue_lds<EPI, FAST>(args, acc, smem, qb, pf, tm, m0, n0, wr, wc, lane, wave, bid * 8 + wave, fg,
+                                      evec);
   }
+  return 0.f;
 }
 
-// Persistent tile loop: grid = min(tiles, CUs) workgroups, workgroup b runs tiles b, b + grid,
-// ... -- the same tile -> XCD map as one tile per workgroup (t % 8 == b % 8), without a workgroup
-// launch per tile, and the next tile's first operand DMAs fly while this tile's epilogue stores drain.
+// Persistent tile loop: grid = min(tiles, CUs) workgroups; tile t of a launch belongs to XCD t % 8 (the
+// bijective remap tile_of_block gives each XCD a contiguous block of the grouped tile order), and the
+// workgroups of XCD x (blockIdx.x % 8 == x: the dispatcher's round-robin) run that XCD's tiles
+// t = x + 8 i, i = 0, 1, ... (ntx of them) in order of i:
+//   static (tile_ctr NULL): workgroup w of the XCD (w = blockIdx.x / 8) runs i = w, w + nwx, w + 2 nwx, ...
+//   dynamic (tile_ctr = 8 u32 per-XCD counters): i = w first, then every further tile is claimed from the XCD's
+//     counter, i = nwx + claim, until a claim runs past ntx.  A workgroup that starts late -- its CU held by
+//     another stream's kernel (the side stream's, or RCCL's collective in the latent-sharded step) -- then
+//     takes fewer tiles instead of delaying the launch by its whole static share.  Each launch makes exactly
+//     ntx claims on counter x (every claim past the end is one workgroup's last), and atomicInc wraps at
+//     ntx - 1, so the counter is back at 0 when the launch ends: no reset, but launches sharing a counter
+//     must be ordered (one stream).  The claim for the next tile is issued as a tile starts (its latency hides
+//     under the tile's first operand DMAs) and broadcast through an LDS word after the tile: buffer 1's A
+//     image, which the next tile's DMAs first write after its prologue barrier.
+// Which workgroup runs a tile does not change its results: every partial-sum slot is indexed by tile.
 // Between tiles every wave's LDS reads of the epilogue image must be done before any wave's DMAs
-// overwrite it: lgkmcnt(0) + s_barrier (no vmcnt wait: the stores keep draining).
+// overwrite it: lgkmcnt(0) + s_barrier (no vmcnt wait: the stores keep draining, the next tile's first
+// operand DMAs fly while they do).
 CC_DEV void pp_tile_boundary() {
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
   __builtin_amdgcn_s_barrier();
@@ -433,29 +451,61 @@ CC_DEV int pp_opaque_tid() {
   asm volatile("" : "+v"(t));
   return t;
 }
+constexpr int PP_SLOT = 2 * 256 * 128;  // LDS byte offset of the tile-claim broadcast word (see above)
+struct TileLoop {
+  unsigned* ctr;
+  int x, nwx, ntx, i;
+  unsigned nxt;
+  CC_DEV TileLoop(int nt, unsigned* c) : ctr(c), nxt(0) {
+    const int G = gridDim.x;
+    x = blockIdx.x & 7;
+    nwx = (G >> 3) + ((G & 7) > x);
+    ntx = (nt >> 3) + ((nt & 7) > x);
+    i = blockIdx.x >> 3;
+  }
+  CC_DEV bool more() const { return i < ntx; }
+  // the tile to run now (claims the next one in the dynamic order)
+  CC_DEV int begin() {
+    if (ctr && threadIdx.x == 0) nxt = atomicInc(ctr + x, (unsigned)(ntx - 1));
+    return x + 8 * i;
+  }
+  // after the tile and pp_tile_boundary()
+  CC_DEV void advance(char* smem) {
+    if (!ctr) {
+      i += nwx;
+      return;
+    }
+    int* slot = (int*)(smem + PP_SLOT);
+    if (threadIdx.x == 0) *slot = (int)nxt;
+    __syncthreads();
+    i = nwx + __builtin_amdgcn_readfirstlane(*slot);
+  }
+};
 
 template <bool AKC, bool BKC, int EPI, bool FAST = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(16))) char smem[EPI == EPI_WGDEC ? PP_LDS_W : PP_LDS];
-  const int nt = args.nbm * args.nbn;
-  for (int t = blockIdx.x; t < nt; t += gridDim.x) {
-    pp_tile<AKC, BKC, EPI, FAST>(args, smem, t, pp_opaque_tid());
+  for (TileLoop L(args.nbm * args.nbn, args.tile_ctr); L.more();) {
+    pp_tile<AKC, BKC, EPI, FAST>(args, smem, L.begin(), pp_opaque_tid());
     pp_tile_boundary();
+    L.advance(smem);
   }
 }
 
-// Two independent GEMMs of one layout in one launch: blocks [0, nb0) are a0's tiles, the rest
-// a1's.  dW_dec and dW_enc (1152 tiles each at config 2: 4.5 waves of 256 CUs apiece) become
+// Two independent GEMMs of one layout in one launch: tiles [0, nb0) are a0's, the rest a1's (the tile loop and
+// its counters are a0's).  dW_dec and dW_enc (1152 tiles each at config 2: 4.5 waves of 256 CUs apiece) become
 // 2304 tiles = 9 full waves, and one kernel boundary disappears.
 template <bool AKC, bool BKC, int EPI0, int EPI1>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_kernel(const GemmArgs a0, const GemmArgs a1) {
   __shared__ __attribute__((aligned(16))) char smem[EPI0 == EPI_WGDEC || EPI1 == EPI_WGDEC ? PP_LDS_W : PP_LDS];
   const int nb0 = a0.nbm * a0.nbn;
-  for (int t = blockIdx.x; t < 2 * nb0; t += gridDim.x) {
+  for (TileLoop L(2 * nb0, a0.tile_ctr); L.more();) {
+    const int t = L.begin();
     const int tid = pp_opaque_tid();
     if (t < nb0) pp_tile<AKC, BKC, EPI0>(a0, smem, t, tid);
     else pp_tile<AKC, BKC, EPI1>(a1, smem, t - nb0, tid);
     pp_tile_boundary();
+    L.advance(smem);
   }
 }
 

@@ -43,6 +43,16 @@ def _span(name):
     return TIMER.span(name) if TIMER is not None else contextlib.nullcontext()
 
 
+# The persistent GEMMs (G1, G3, G4G5) hand out their tiles from per-XCD counters, so workgroups that start late
+# (CUs held by the side stream's or RCCL's kernels) take fewer tiles; False: the static tile order.  The same
+# bits either way (every partial-sum slot is indexed by tile; tests compare the two).
+DYNAMIC_TILES = True
+
+
+def _tile_ctr(ws, k):
+    return ws.tile_ctr[k] if DYNAMIC_TILES else None
+
+
 def padded_dims(h, d):
     """Kernel dims (h, d) of a crosscoder with dict_size h and d_in d: both rounded up to a multiple of 8
     (the kernels move 16-byte rows).  The padding latents / columns are zero in every arena and stay
@@ -203,7 +213,10 @@ class StepWorkspace:
             self.sq_off.append(self.sq_off[-1] + s)
         self.sq = E(self.sq_off[-1])
         self.clip_out = E(8)
-        self.wg_part = E(ops.WG_PART_FLOATS)  # per-workgroup squared sums of the fused G4G5 + grad tail
+        self.tile_sum = E(ops.wgrad_tile_sums(h, K))  # per-tile squared sums of the fused G4G5 + grad tail
+        # per-XCD tile counters of the persistent G1 / G3 / G4G5 launches (dynamic tile order, DYNAMIC_TILES);
+        # every launch leaves its counters at zero
+        self.tile_ctr = torch.zeros(3, ops.TILE_CTR_WORDS, dtype=torch.int32, device=device)
         self.clip_ready = False  # backward(clip=...) already wrote clip_out (fused grad tail)
         self.acts_pending = False  # forward deferred the activation column sums to loss_finalize
         # arrival counters of the fused tail launches (loss tail, grad tail); each launch leaves 0
@@ -288,7 +301,7 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     with _span("G1_encode"):
         if ws.tr:
             ops.encode_fwd_t(ws.x, P.W_enc_hk, P.b_enc, ws.acts, ws.acts_t, True, colsum_part=ws.acts_colpart,
-                             l0_part=ws.l0_part, mask_bits=ws.mask_bits)
+                             l0_part=ws.l0_part, mask_bits=ws.mask_bits, tile_ctr=_tile_ctr(ws, 0))
         else:
             ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, colsum_part=ws.acts_colpart,
                            l0_part=ws.l0_part)
@@ -414,7 +427,8 @@ def dacts_rows(ws, P, l1_coeff, r0, r1, l1_grad_weight=1.0):
     with _span("G3_dacts"):
         if ws.tr:
             ops.dacts_bwd_t(ws.g_recon[r0:r1], P.W_dec_hk, ws.acts[r0:r1], ws.tn, l1_scale, ws.g_pre_t[:, r0:r1],
-                            colsum_part=ws.gpre_colpart[c0:c1], mask_bits=ops.mask_bits_rows(ws.mask_bits, ws.h, r0, r1))
+                            colsum_part=ws.gpre_colpart[c0:c1], mask_bits=ops.mask_bits_rows(ws.mask_bits, ws.h, r0, r1),
+                            tile_ctr=_tile_ctr(ws, 1))
         else:
             ops.dacts_bwd(ws.g_recon[r0:r1], P.W_dec_hk, ws.acts[r0:r1], ws.tn, l1_scale, ws.g_pre[r0:r1],
                           colsum_part=ws.gpre_colpart[c0:c1])
@@ -442,8 +456,8 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
             ops.wgrad_both_sums_t(ws.acts_t, ws.g_recon_t, P.W_dec_hk, ws.inv_norms, ws.colsum_acts, l1_scale,
                                   G.W_dec_hk, ws.sq_slice(1), ws.g_pre_t, ws.x_t, G.W_enc_hk, ws.sq_slice(0), n, d,
                                   ws.gpre_colpart, G.b_enc, ws.sq_slice(2), loss_colpart(ws), G.b_dec_flat,
-                                  ws.sq_slice(3), ws.sq, ws.sq_off, sums_out, ws.tail_ctr[1:2], ws.wg_part,
-                                  zero_mask=zero_mask)
+                                  ws.sq_slice(3), ws.sq, ws.sq_off, sums_out, ws.tail_ctr[1:2], ws.tile_sum,
+                                  zero_mask=zero_mask, tile_ctr=_tile_ctr(ws, 2))
         return
     if clip is not None and ws.tr:
         # G4 + G5 and the grad tail (bias sums + clip coefficient) in one launch
@@ -452,7 +466,7 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
                                   G.W_dec_hk, ws.sq_slice(1), ws.g_pre_t, ws.x_t, G.W_enc_hk, ws.sq_slice(0), n, d,
                                   ws.gpre_colpart, G.b_enc, ws.sq_slice(2), loss_colpart(ws), G.b_dec_flat,
                                   ws.sq_slice(3), ws.sq, ws.sq_off, clip, ws.dtype == torch.bfloat16, ws.clip_out,
-                                  ws.tail_ctr[1:2], ws.wg_part)
+                                  ws.tail_ctr[1:2], ws.tile_sum, tile_ctr=_tile_ctr(ws, 2))
         ws.clip_ready = True
         return
     with _span("G4G5_wgrad"):

@@ -36,6 +36,19 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+TILE_CTR_WORDS = 8  # CC_TILE_CTR_WORDS (include/crosscoder_hip.h)
+
+
+def _ctr(t):
+    """A persistent launch's per-XCD tile counters: int32 [TILE_CTR_WORDS] (zero; every launch leaves them zero),
+    or None (static tile order)."""
+    if t is None:
+        return None
+    if t.dtype != torch.int32 or t.numel() < TILE_CTR_WORDS:
+        raise ValueError("tile counters: int32 tensor of at least TILE_CTR_WORDS elements")
+    return _ptr(t)
+
+
 def _contig(t, name):
     if not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
@@ -143,16 +156,17 @@ def mask_bits_words(B, h):
 
 
 def encode_fwd_t(x, W_enc_hk, b_enc, acts, acts_t, apply_relu=True, tn=None, colsum_part=None, l1_part=None,
-                 l0_part=None, mask_bits=None):
+                 l0_part=None, mask_bits=None, tile_ctr=None):
     """encode_fwd that also stores acts_t [h][B] = acts^T (bf16, B % 8 == 0) and, optionally, the activation
-    mask bits (int32 [mask_bits_words(B, h)]) that dacts_bwd_t reads instead of acts."""
+    mask bits (int32 [mask_bits_words(B, h)]) that dacts_bwd_t reads instead of acts.  tile_ctr: int32
+    [TILE_CTR_WORDS] zeroed counters -> dynamic per-XCD tile order (same bits)."""
     B, K = x.shape
     h = W_enc_hk.shape[0]
     if mask_bits is not None and mask_bits.numel() < mask_bits_words(B, h):
         raise ValueError("mask_bits too small")
     check(lib().cc_encode_fwd_t(_ptr(x), _ptr(W_enc_hk), _ptr(b_enc), _ptr(tn), _ptr(acts), _ptr(acts_t),
-                                int(apply_relu), _ptr(colsum_part), _ptr(l1_part), _ptr(l0_part), _ptr(mask_bits), B,
-                                K, h, dtype_code(x.dtype), _stream(x)))
+                                int(apply_relu), _ptr(colsum_part), _ptr(l1_part), _ptr(l0_part), _ptr(mask_bits),
+                                _ctr(tile_ctr), B, K, h, dtype_code(x.dtype), _stream(x)))
     return acts
 
 
@@ -287,7 +301,7 @@ def dacts_bwd(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre, colsum_part=None):
                              _ptr(colsum_part), B, K, h, dtype_code(g_recon.dtype), _stream(g_recon)))
 
 
-def dacts_bwd_t(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre_t, colsum_part=None, mask_bits=None):
+def dacts_bwd_t(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre_t, colsum_part=None, mask_bits=None, tile_ctr=None):
     """dacts_bwd storing g_pre transposed only: g_pre_t [h][>= B] view (column slice allowed, row stride
     g_pre_t.stride(0)).  mask_bits: encode_fwd_t's bits of these rows (see mask_bits_rows)."""
     B, K = g_recon.shape
@@ -297,7 +311,7 @@ def dacts_bwd_t(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre_t, colsum_part=None
     if mask_bits is not None and mask_bits.numel() < mask_bits_words(B, h):
         raise ValueError("mask_bits too small")
     check(lib().cc_dacts_bwd_t(_ptr(g_recon), _ptr(W_dec_hk), _ptr(acts), _ptr(tn), l1_scale, _ptr(mask_bits),
-                               _ptr(g_pre_t), g_pre_t.stride(0), _ptr(colsum_part), B, K, h,
+                               _ptr(g_pre_t), g_pre_t.stride(0), _ptr(colsum_part), _ctr(tile_ctr), B, K, h,
                                dtype_code(g_recon.dtype), _stream(g_recon)))
 
 
@@ -389,12 +403,14 @@ def wgrad_both_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, grad_d
                                 h, n, d, dtype_code(actsT.dtype), _stream(actsT)))
 
 
-WG_PART_FLOATS = 4 * 1024  # CC_WG_PART_MAX x 4 (include/crosscoder_hip.h)
+def wgrad_tile_sums(h, K):
+    """floats of the per-tile squared-sum scratch of wgrad_both_clip_t / wgrad_both_sums_t"""
+    return int(lib().cc_wgrad_tile_sums(h, K))
 
 
 def wgrad_both_clip_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, grad_dec, sq_dec, g_preT, xT, grad_enc,
                       sq_enc, n, d, gpre_colpart, g_b_enc, sq_b_enc, loss_colpart, g_b_dec, sq_b_dec, sq, offsets,
-                      max_norm, emulate_bf16, out, counter, wg_part):
+                      max_norm, emulate_bf16, out, counter, tile_sum, tile_ctr=None):
     """wgrad_both_t + grad_tail in one launch (the bias sums before the GEMM tiles, the clip coefficient
     in the last workgroup); same outputs."""
     h, B = actsT.shape
@@ -404,12 +420,12 @@ def wgrad_both_clip_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, g
         _ptr(sq_dec), _ptr(g_preT), _ptr(xT), _ptr(grad_enc), _ptr(sq_enc), B, h, n, d, _ptr(gpre_colpart),
         gpre_colpart.shape[0], _ptr(g_b_enc), _ptr(sq_b_enc), _ptr(loss_colpart), loss_colpart.shape[0], _ptr(g_b_dec),
         _ptr(sq_b_dec), _ptr(sq), arr, len(offsets) - 1, max_norm, int(emulate_bf16), _ptr(out), _ptr(counter),
-        _ptr(wg_part), dtype_code(actsT.dtype), _stream(actsT)))
+        _ptr(tile_sum), _ctr(tile_ctr), dtype_code(actsT.dtype), _stream(actsT)))
 
 
 def wgrad_both_sums_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, grad_dec, sq_dec, g_preT, xT, grad_enc,
                       sq_enc, n, d, gpre_colpart, g_b_enc, sq_b_enc, loss_colpart, g_b_dec, sq_b_dec, sq, offsets, out,
-                      counter, wg_part, zero_mask=0):
+                      counter, tile_sum, zero_mask=0, tile_ctr=None):
     """wgrad_both_t + grad_tail_sums in one launch (the latent-sharded step); same outputs."""
     h, B = actsT.shape
     arr = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
@@ -417,8 +433,8 @@ def wgrad_both_sums_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, g
         _ptr(actsT), _ptr(g_reconT), _ptr(W_dec_hk), _ptr(norms), _ptr(colsum_acts), l1_scale, _ptr(grad_dec),
         _ptr(sq_dec), _ptr(g_preT), _ptr(xT), _ptr(grad_enc), _ptr(sq_enc), B, h, n, d, _ptr(gpre_colpart),
         gpre_colpart.shape[0], _ptr(g_b_enc), _ptr(sq_b_enc), _ptr(loss_colpart), loss_colpart.shape[0], _ptr(g_b_dec),
-        _ptr(sq_b_dec), _ptr(sq), arr, len(offsets) - 1, int(zero_mask), _ptr(out), _ptr(counter), _ptr(wg_part),
-        dtype_code(actsT.dtype), _stream(actsT)))
+        _ptr(sq_b_dec), _ptr(sq), arr, len(offsets) - 1, int(zero_mask), _ptr(out), _ptr(counter), _ptr(tile_sum),
+        _ctr(tile_ctr), dtype_code(actsT.dtype), _stream(actsT)))
 
 
 def clip_finalize(sq, offsets, max_norm, emulate_bf16, out):

@@ -112,10 +112,15 @@ int cc_transposed_ok(int64_t B, int64_t K, int64_t h, int dtype);
  * cc_wgrad_both_t).  bf16 with B, K, h % 8 == 0 (else CC_ERR_SHAPE).
  * mask_bits (optional, cc_mask_bits_words(B, h) u32): the activation mask (acts > 0) as 1 bit per element in
  * the GEMM's accumulator order, which cc_dacts_bwd_t reads instead of the acts tile (autograd of the ReLU,
- * crosscoder.py:77). */
+ * crosscoder.py:77).
+ * tile_ctr (optional): CC_TILE_CTR_WORDS u32, zero before the first launch that uses them and left zero by
+ * every launch: the persistent launch then hands out its output tiles dynamically, per XCD, so workgroups
+ * that start late (their CUs held by another stream's kernel) take fewer tiles; NULL: a static tile order.
+ * The results are the same bits either way.  Launches sharing tile_ctr must be ordered (one stream). */
+#define CC_TILE_CTR_WORDS 8
 int cc_encode_fwd_t(const void* x, const void* W_enc, const void* b_enc, const float* tn, void* acts, void* acts_t,
                     int apply_relu, float* colsum_part, float* l1_part, float* l0_part, uint32_t* mask_bits,
-                    int64_t B, int64_t K, int64_t h, int dtype, void* stream);
+                    uint32_t* tile_ctr, int64_t B, int64_t K, int64_t h, int dtype, void* stream);
 
 /* u32 words of cc_encode_fwd_t's mask_bits for a [B][h] activation (256 x 256 tiles x 512 threads x 4). */
 int64_t cc_mask_bits_words(int64_t B, int64_t h);
@@ -226,10 +231,10 @@ int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const
  * [r0, r1) passes g_pre_t + r0 and B = r1 - r0).  bf16 with B, K, h, ldt % 8 == 0.
  * mask_bits (optional): cc_encode_fwd_t's mask bits of these rows (a slice starting at row r0, r0 % 256 == 0,
  * passes mask_bits + (r0 / 256) * cc_mask_bits_words(256, h)); used instead of reading the acts tile when
- * the shape takes the whole-tile form (B, h % 256 == 0), same bits. */
+ * the shape takes the whole-tile form (B, h % 256 == 0), same bits.  tile_ctr: as cc_encode_fwd_t. */
 int cc_dacts_bwd_t(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
-                   const uint32_t* mask_bits, void* g_pre_t, int64_t ldt, float* colsum_part, int64_t B, int64_t K,
-                   int64_t h, int dtype, void* stream);
+                   const uint32_t* mask_bits, void* g_pre_t, int64_t ldt, float* colsum_part, uint32_t* tile_ctr,
+                   int64_t B, int64_t K, int64_t h, int dtype, void* stream);
 
 /* W_dec.grad [h][K] = acts^T . g_recon + l1_scale * sum_b(acts[:,h]) * W_dec[h,m,:]/||W_dec[h,m,:]||
  * (norm backward is 0 where the norm is 0; inv_norms from cc_dec_norms).
@@ -280,16 +285,18 @@ int cc_grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_
  * into clip_out) -- the bias sums run before the GEMM tiles, the clip finaliser in the last workgroup
  * to finish.  Same outputs as cc_wgrad_both_t followed by cc_grad_tail (the clip coefficient up to
  * the order of its fp64 squared-sum accumulation).  nparams must be 4 (sq's segments W_enc, W_dec, b_enc,
- * b_dec); wg_part: fp32 scratch of CC_WG_PART_MAX x 4 (per-workgroup squared sums).  Where the ping-pong
- * GEMM does not serve the shape (or dtype != bf16) it runs exactly those two entries. */
-#define CC_WG_PART_MAX 1024
+ * b_dec); tile_sum: fp32 scratch of cc_wgrad_tile_sums(h, n*d) floats (each output tile's squared sum, which
+ * the last workgroup adds in a fixed order: the coefficient's bits do not depend on which workgroup ran which
+ * tile); tile_ctr: as cc_encode_fwd_t.  Where the ping-pong GEMM does not serve the shape (or dtype != bf16)
+ * it runs exactly those two entries. */
+int64_t cc_wgrad_tile_sums(int64_t h, int64_t K);
 int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
                          const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_preT,
                          const void* xT, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
                          const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
                          const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
                          const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
-                         uint32_t* counter, float* wg_part, int dtype, void* stream);
+                         uint32_t* counter, float* tile_sum, uint32_t* tile_ctr, int dtype, void* stream);
 /* cc_wgrad_both_clip_t whose finaliser is cc_segment_sums instead of the clip (the latent-sharded step,
  * trainer.py:45-46 split across ranks): out[p] = the per-parameter squared sums, 0 where bit p of
  * zero_mask is set, to be all-reduced.  Equal to cc_wgrad_both_t + cc_grad_tail_sums (the sums up to the
@@ -299,8 +306,8 @@ int cc_wgrad_both_sums_t(const void* actsT, const void* g_reconT, const void* W_
                          const void* xT, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
                          const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
                          const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
-                         const int64_t* off, int nparams, int zero_mask, float* out, uint32_t* counter, float* wg_part,
-                         int dtype, void* stream);
+                         const int64_t* off, int nparams, int zero_mask, float* out, uint32_t* counter, float* tile_sum,
+                         uint32_t* tile_ctr, int dtype, void* stream);
 /* cc_grad_tail whose finaliser is cc_segment_sums instead of the clip (the latent-sharded step:
  * out[p] = the per-parameter squared sums, 0 where bit p of zero_mask is set, to be all-reduced). */
 int cc_grad_tail_sums(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,

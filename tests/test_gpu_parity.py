@@ -549,6 +549,41 @@ def test_delayed_norm_finaliser_still_orders_g3_and_wgrad(gpu, dbg_lib, monkeypa
     assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
 
 
+def test_dynamic_tile_order_is_bit_identical(gpu, dbg_lib, monkeypatch):
+    """The persistent G1 / G3 / G4G5 launches hand out tiles from per-XCD counters (engine.DYNAMIC_TILES); which
+    workgroup runs a tile must not change any bit.  Steps with the static order vs the dynamic order while 32
+    workgroups holding 96 KB of LDS each (no GEMM workgroup fits beside them) occupy CUs from another stream
+    for the first 0.6 ms of every step -- so the dynamic launches run uneven tile counts per workgroup --
+    give the same losses, params and moments, and every launch leaves its counters at zero."""
+    import ctypes
+
+    from crosscoder_amd import engine
+    B, n, d, h = 4096, 2, 512, 16384  # G1 / G3: 1024 tiles, G4G5: 512 tiles on 256 CUs
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+               num_tokens=B * 20, device=str(gpu))
+    hog = torch.cuda.Stream(device=gpu)
+    outs = []
+    for dynamic in (False, True):
+        monkeypatch.setattr(engine, "DYNAMIC_TILES", dynamic)
+        cc = ca.CrossCoder(cfg)
+        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=6), crosscoder=cc)
+        dicts = []
+        for _ in range(3):
+            hog.wait_stream(torch.cuda.current_stream(gpu))
+            ops.check(dbg_lib.cc_debug_spin(32, 96 * 1024, 600_000, ctypes.c_void_p(hog.cuda_stream)))
+            dicts.append(tr.step())
+        st = tr.optimizer.state
+        m = torch.cat([st[p]["exp_avg"].detach().flatten().float() for p in cc.parameters()])
+        v = torch.cat([st[p]["exp_avg_sq"].detach().flatten().float() for p in cc.parameters()])
+        torch.cuda.synchronize()
+        ws = cc._workspace(B, step=True)
+        assert not bool(ws.tile_ctr.any()) and not bool(ws.tail_ctr.any())
+        outs.append((dicts, cc.arena().data.clone(), m, v))
+    (d0, p0, m0, v0), (d1, p1, m1, v1) = outs
+    assert d0 == d1
+    assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+
+
 def test_full_size_config2_trainer_steps_match_oracle(gpu, full_size_case):
     """BASELINE config 2 through the shipped schedule (Trainer.step: fused G2 + loss, G4G5 + grad tail + clip
     in one launch, encoder / decoder Adam halves on two streams) vs the oracle's fp32 OracleTrainer.step
@@ -1327,7 +1362,7 @@ def test_fused_tails_match_separate_launches(gpu, enc_dtype, B, n, d, h):
         ops.wgrad_both_sums_t(ws.acts_t, ws.g_recon_t, a.W_dec_hk, ws.inv_norms, ws.colsum_acts, 2.0 / B, G3.W_dec_hk,
                               sq3[o[1]:o[2]], ws.g_pre_t, ws.x_t, G3.W_enc_hk, sq3[o[0]:o[1]], n, d, ws.gpre_colpart,
                               G3.b_enc, sq3[o[2]:o[3]], engine.loss_colpart(ws), G3.b_dec_flat, sq3[o[3]:o[4]], sq3, o,
-                              sums, ws.tail_ctr[1:2], ws.wg_part, zero_mask=0b1000)
+                              sums, ws.tail_ctr[1:2], ws.tile_sum, zero_mask=0b1000)
         ops.segment_sums(ws.sq, o, ref_sums, zero_mask=0b1000)
         torch.cuda.synchronize()
         assert torch.equal(sq3, ws.sq) and torch.equal(G3.b_enc, G.b_enc) and torch.equal(G3.b_dec_flat, G.b_dec_flat)
