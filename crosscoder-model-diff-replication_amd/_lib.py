@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcrosscoder_hip.so")
 # test-only build of the same kernels that also exports the launch-form setters (csrc/Makefile)
 DEBUG_LIB_PATH = os.path.join(_HERE, "libcrosscoder_hip_dbg.so")
-DEFAULT_PP_MASK = 5  # the ping-pong layouts both libraries default to (csrc/gemm.hip)
+DEFAULT_PP_MASK = 7  # the ping-pong layouts both libraries default to (csrc/gemm.hip: g_pp_mask)
 DEBUG_SETTERS = ("cc_debug_set_pp_mask", "cc_debug_set_pp_fast", "cc_debug_set_dec_one_launch")
 
 CC_BF16 = 1
@@ -76,7 +76,8 @@ SIGNATURES = {
                                  _i64, _p]),
     "cc_decode_loss_ncb": (_i64, [_i64, _i64, _i64, _i64, _i]),
     "cc_decode_loss_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i, _p]),
-    "cc_decode_loss": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i, _p]),
+    "cc_decode_loss": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i,
+                            _p]),
     "cc_transposed_ok": (_i, [_i64, _i64, _i64, _i]),
     "cc_encode_fwd_t": (_i, [_p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_mask_bits_words": (_i64, [_i64, _i64]),
@@ -138,6 +139,8 @@ def load_debug():
             fn.argtypes = [ctypes.c_int]
         lib.cc_debug_spin.restype = _i
         lib.cc_debug_spin.argtypes = [_i64, _i64, _i64, _p]
+        lib.cc_debug_spin_ev.restype = _i
+        lib.cc_debug_spin_ev.argtypes = [_i64, _i64, _p, _p]
         _debug = lib
     return _debug
 

@@ -165,34 +165,13 @@ __global__ __launch_bounds__(256) void transpose_b16_kernel(const char* __restri
   }
 }
 
-// norms[r][m] = sqrt(sum of part[r][m*bpm .. (m+1)*bpm) in ascending order), total, inverses:
-// the rest of dec_norms_kernel from the per-block partials.  One thread per row, one wave per
-// block (h/64 blocks spread over the CUs); each lane issues NORM_LOADS independent loads before
-// adding them in order (the sum is latency-bound: one dependent load per add took 15 us at config 2).
-constexpr int NORM_LOADS = 12;
+// The decoder norms from their per-block partials (norms_finalize_row, cc_common.h): one thread per row, one
+// wave per block (h/64 blocks spread over the CUs).
 __global__ __launch_bounds__(64) void norms_finalize_kernel(const float* __restrict__ part, int h, int n, int bpm,
                                                             float* __restrict__ norms, float* __restrict__ total,
                                                             float* __restrict__ inv_norms) {
   const int row = blockIdx.x * 64 + threadIdx.x;
-  if (row >= h) return;
-  const float* p = part + (int64_t)row * n * bpm;
-  float tot = 0.f;
-  for (int m = 0; m < n; ++m) {
-    float s = 0.f;
-    for (int b0 = 0; b0 < bpm; b0 += NORM_LOADS) {
-      float v[NORM_LOADS];
-#pragma unroll
-      for (int u = 0; u < NORM_LOADS; ++u) v[u] = b0 + u < bpm ? p[m * bpm + b0 + u] : 0.f;
-#pragma unroll
-      for (int u = 0; u < NORM_LOADS; ++u)
-        if (b0 + u < bpm) s += v[u];
-    }
-    const float nr = sqrtf(s);
-    norms[(int64_t)row * n + m] = nr;
-    if (inv_norms) inv_norms[(int64_t)row * n + m] = nr > 0.f ? 1.f / nr : 0.f;
-    tot += nr;
-  }
-  total[row] = tot;
+  if (row < h) norms_finalize_row(part, row, n, bpm, norms, total, inv_norms);
 }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }

@@ -137,6 +137,34 @@ CC_DEV double wave_sum_d(double v) {
   return v;
 }
 
+// norms[r][m] = sqrt(sum of part[r][m*bpm .. (m+1)*bpm) in ascending order), total[r] = sum_m norms, inverses
+// (0 where a norm is 0): the rest of dec_norms_kernel from the per-(row, 64-column block) partials.  Each
+// lane issues NORM_LOADS independent loads before adding them in order (the sum is latency-bound: one
+// dependent load per add took 15 us at config 2).  Shared by the stand-alone finaliser and the G2 launch
+// that carries it.
+constexpr int NORM_LOADS = 12;
+CC_DEV void norms_finalize_row(const float* __restrict__ part, int row, int n, int bpm, float* __restrict__ norms,
+                               float* __restrict__ total, float* __restrict__ inv_norms) {
+  const float* p = part + (int64_t)row * n * bpm;
+  float tot = 0.f;
+  for (int m = 0; m < n; ++m) {
+    float s = 0.f;
+    for (int b0 = 0; b0 < bpm; b0 += NORM_LOADS) {
+      float v[NORM_LOADS];
+#pragma unroll
+      for (int u = 0; u < NORM_LOADS; ++u) v[u] = b0 + u < bpm ? p[m * bpm + b0 + u] : 0.f;
+#pragma unroll
+      for (int u = 0; u < NORM_LOADS; ++u)
+        if (b0 + u < bpm) s += v[u];
+    }
+    const float nr = sqrtf(s);
+    norms[(int64_t)row * n + m] = nr;
+    if (inv_norms) inv_norms[(int64_t)row * n + m] = nr > 0.f ? 1.f / nr : 0.f;
+    tot += nr;
+  }
+  total[row] = tot;
+}
+
 }  // namespace cc
 
 #define CC_LAUNCH_CHECK()                                \

@@ -26,6 +26,8 @@
 // other stage -> MFMA on stage t.  All LDS is one __shared__ array.
 #include <mutex>
 
+#include <hip/hip_ext.h>
+
 #include "cc_common.h"
 
 namespace cc {
@@ -664,6 +666,15 @@ CC_DEBUG_API int cc_debug_spin(int64_t blocks, int64_t lds_bytes, int64_t ns, vo
   CC_LAUNCH_CHECK();
   return CC_OK;
 }
+// The same launch through hipExtLaunchKernel with a stop event (probe: whether an event recorded by the launch
+// itself costs the stream the idle gap of a separate hipEventRecord)
+CC_DEBUG_API int cc_debug_spin_ev(int64_t blocks, int64_t ns, void* stream, void* stop_event) {
+  if (blocks <= 0 || blocks > 4096 || ns < 0 || ns > 1000000000) return CC_ERR_SHAPE;
+  hipExtLaunchKernelGGL(debug_spin_kernel, dim3((unsigned)blocks), dim3(NTHR), 0, (hipStream_t)stream, nullptr,
+                        (hipEvent_t)stop_event, 0, (int64_t)(ns / 10));
+  CC_LAUNCH_CHECK();
+  return CC_OK;
+}
 #else
 constexpr int g_pp_mask = 7, g_pp_fast = 1, g_dec_one_launch = 1;
 #endif
@@ -988,6 +999,11 @@ int cc_decode_fwd_ws_t(const void* acts, const void* W_dec_t, float* recon_f32, 
 // waves: lane -> 8 columns (lane & 7) of row 8 * wave + (lane >> 3).  Row terms per 64-column block
 // (row_part[2][n * d/64][B]), column sums of g_recon per 128-row group (col_part[B/128][K]), g_recon^T
 // through an LDS tile.  B % 8 == 0, d % 64 == 0.
+// Blocks with blockIdx.y >= part_rows (= cc_col_part_rows(B)) instead finalise the decoder norms from their
+// per-block partials (norms_finalize_row, one row per thread; nf_part NULL: none): the norms are first read
+// by G3 and by the side stream's loss tail, both after this launch, and their partials (the decoder-half
+// Adam's) are complete before G2 -- the finaliser rides here at no cost on the compute stream instead of
+// running on the side stream behind an event the compute stream must wait for.
 struct LossSplitArgs {
   const float* part;
   int S, t_nbn, col0, B, K, n, d;
@@ -1000,6 +1016,12 @@ struct LossSplitArgs {
   bf16_t* g_t;
   float* row_part;
   float* col_part;
+  int part_rows;
+  const float* nf_part;  // decoder-norm partials [h][n * nf_bpm] (NULL: no finaliser blocks)
+  int nf_h, nf_n, nf_bpm;
+  float* nf_norms;
+  float* nf_total;
+  float* nf_inv;
 };
 constexpr int LSPLIT_THREADS = 1024;
 __global__ __launch_bounds__(LSPLIT_THREADS) void loss_split_kernel(const LossSplitArgs a) {
@@ -1007,6 +1029,12 @@ __global__ __launch_bounds__(LSPLIT_THREADS) void loss_split_kernel(const LossSp
   constexpr int NW = LSPLIT_THREADS / 64;
   __shared__ __attribute__((aligned(16))) bf16_t tt[64 * TP];
   __shared__ float red[NW][64];
+  if ((int)blockIdx.y >= a.part_rows) {
+    const int row = (((int)blockIdx.y - a.part_rows) * (int)gridDim.x + (int)blockIdx.x) * LSPLIT_THREADS +
+                    (int)threadIdx.x;
+    if (row < a.nf_h) norms_finalize_row(a.nf_part, row, a.nf_n, a.nf_bpm, a.nf_norms, a.nf_total, a.nf_inv);
+    return;
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int cq = lane & 7;
   const int ct = blockIdx.x * 64 + cq * 8;  // tail-relative column of this lane's 8
@@ -1092,15 +1120,21 @@ int64_t cc_decode_loss_ncb(int64_t B, int64_t h, int64_t n, int64_t d, int dtype
 template <bool BKC>
 static int decode_loss(const void* acts, const void* W_dec, const void* b_dec, const void* x, const float* x_mean,
                        float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
-                       int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, hipStream_t st) {
+                       int64_t ws_floats, const float* norm_part, float* norms, float* tn, float* inv_norms, int64_t B,
+                       int64_t h, int64_t n, int64_t d, int dtype, hipStream_t st) {
   if (!acts || !W_dec || !b_dec || !x || !x_mean || !g_recon || !row_part || !col_part) return CC_ERR_NULL;
   if (BKC && !g_recon_t) return CC_ERR_NULL;
   if (!cc_decode_loss_ncb(B, h, n, d, dtype) || !use_pp(n * d, true, BKC, dtype)) return CC_ERR_SHAPE;
   if (!al16(x) || !al16(g_recon) || !al16(g_recon_t) || !al16(x_mean) || !al16(b_dec)) return CC_ERR_ALIGN;
+  if (norm_part && (!norms || !tn)) return CC_ERR_NULL;
   const int64_t K = n * d;
   const int64_t ldb = BKC ? h : K;
   DecPlan p;
   const bool split = dec_plan(B, h, K, dtype, p);
+  if (norm_part && !split) {  // (no leftover launch to carry it: the stand-alone finaliser first)
+    const int rc = cc_dec_norms_finalize(norm_part, h, n, d, norms, tn, inv_norms, st);
+    if (rc) return rc;
+  }
   GemmArgs a = {};
   a.A = acts; a.lda = h; a.B = W_dec; a.ldb = ldb;
   a.M = (int)B; a.N = split ? p.nbn_main * 256 : (int)K; a.K = (int)h;
@@ -1141,9 +1175,18 @@ static int decode_loss(const void* acts, const void* W_dec, const void* b_dec, c
   l.b_dec = (const bf16_t*)b_dec; l.x = (const bf16_t*)x; l.x_mean = x_mean; l.gs = grad_scale;
   l.g_recon = (bf16_t*)g_recon; l.g_t = (bf16_t*)g_recon_t; l.row_part = row_part; l.col_part = col_part;
   // one block per 128-row half of every 256-row tile (cc_col_part_rows(B) groups, like the main tiles' column-sum
-  // rows): a half past B writes zero column sums, so every partial row the backward reduces is written
-  hipLaunchKernelGGL(loss_split_kernel, dim3((unsigned)(p.tail_cols / 64), (unsigned)cc_col_part_rows(B)),
-                     dim3(LSPLIT_THREADS), 0, st, l);
+  // rows): a half past B writes zero column sums, so every partial row the backward reduces is written; then
+  // the norm finaliser's rows of blocks
+  const int gx = p.tail_cols / 64;
+  l.part_rows = (int)cc_col_part_rows(B);
+  int fin_rows = 0;
+  if (norm_part) {
+    l.nf_part = norm_part; l.nf_h = (int)h; l.nf_n = (int)n; l.nf_bpm = (int)(d / 64);
+    l.nf_norms = norms; l.nf_total = tn; l.nf_inv = inv_norms;
+    fin_rows = (int)((h + (int64_t)gx * LSPLIT_THREADS - 1) / ((int64_t)gx * LSPLIT_THREADS));
+  }
+  hipLaunchKernelGGL(loss_split_kernel, dim3((unsigned)gx, (unsigned)(l.part_rows + fin_rows)), dim3(LSPLIT_THREADS), 0,
+                     st, l);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }
@@ -1154,14 +1197,15 @@ int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, c
                      float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
                      int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
   return decode_loss<true>(acts, W_dec_t, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t, row_part, col_part, ws,
-                           ws_floats, B, h, n, d, dtype, (hipStream_t)stream);
+                           ws_floats, nullptr, nullptr, nullptr, nullptr, B, h, n, d, dtype, (hipStream_t)stream);
 }
 
 int cc_decode_loss(const void* acts, const void* W_dec, const void* b_dec, const void* x, const float* x_mean,
                    float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
-                   int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
+                   int64_t ws_floats, const float* norm_part, float* norms, float* tn, float* inv_norms, int64_t B,
+                   int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
   return decode_loss<false>(acts, W_dec, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t, row_part, col_part, ws,
-                            ws_floats, B, h, n, d, dtype, (hipStream_t)stream);
+                            ws_floats, norm_part, norms, tn, inv_norms, B, h, n, d, dtype, (hipStream_t)stream);
 }
 
 int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,

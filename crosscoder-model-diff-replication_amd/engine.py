@@ -162,10 +162,9 @@ class StepWorkspace:
         # per-(row, 64-column block) squared sums of W_dec (d % 64 == 0): written by the decoder-half Adam
         # (cc_adam_dec_norms) or by the fused W_dec^T + norms pass
         self.norm_part = E(npart) if npart else None
-        # the side stream's norm finaliser and that stream: every other stream that reads the norms waits
-        # for it once (wait_norms)
-        self.norms_event = None
-        self.norms_stream = None
+        # the decoder-norm partials are complete but not yet finalised into norms / tn / inv_norms: the next G2
+        # launch carries the finaliser (decode_loss), or flush_norms runs it before the first reader
+        self.norms_fin_pending = False
         self.acts_t = E(h, B, dt=dtype) if self.tr else None
         # G1's activation mask as bits in the GEMM accumulator order: G3 reads 16 B per thread and tile instead
         # of the 128 KB acts tile (1/16 of the bytes, no LDS staging)
@@ -265,17 +264,12 @@ def _decoder_derived(ws, P):
     ops.dec_norms(P.W_dec_hk, ws.h, ws.n, ws.d, norms=ws.norms, total=ws.tn, inv_norms=ws.inv_norms)
 
 
-def wait_norms(ws):
-    """Order torch's current stream after the decoder-norm finaliser the side stream ran (engine.adam), unless
-    it is that stream (the loss tail there is ordered by the stream itself and must not consume the wait that
-    G3 / G4G5 on the compute stream need)."""
-    if ws.norms_event is None:
-        return
-    cur = torch.cuda.current_stream(ws.x.device)
-    if cur == ws.norms_stream:
-        return
-    cur.wait_event(ws.norms_event)
-    ws.norms_event = None
+def flush_norms(ws):
+    """Finalise pending decoder norms on torch's current stream (where no G2 launch carried the finaliser)."""
+    if ws.norms_fin_pending:
+        ws.norms_fin_pending = False
+        with _span("dec_norms"):
+            ops.dec_norms_finalize(ws.norm_part, ws.h, ws.n, ws.d, ws.norms, ws.tn, ws.inv_norms)
 
 
 def decoder_norms(ws, P):
@@ -314,11 +308,12 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     P.wait_pending()
     decoder_norms(ws, P)  # (+ W_dec^T), unless launched already after the last Adam
     if loss and ws.fused_ncb:
-        decode_loss(ws, P, grad_scale)
+        decode_loss(ws, P, grad_scale)  # (carries a pending norm finaliser)
         ws.acts_pending = True
         if finalize:
             loss_finalize(ws)
         return
+    flush_norms(ws)
     with _span("G2_decode"):
         if ws.W_dec_t is not None:
             ops.decode_partial_t(ws.acts, ws.W_dec_t, ws.recon, ws.dec_ws)
@@ -337,9 +332,11 @@ def decode_loss(ws, P, grad_scale=None):
     """G2 + loss rows + g_recon (and g_recon^T) in one pass over the whole batch (decode_loss: W_dec read
     directly)."""
     gs = 2.0 / ws.B if grad_scale is None else grad_scale
+    nf = (ws.norm_part, ws.norms, ws.tn, ws.inv_norms) if ws.norms_fin_pending else None
+    ws.norms_fin_pending = False
     with _span("G2_decode"):
         ops.decode_loss(ws.acts, P.W_dec_hk, P.b_dec_flat, ws.x, ws.x_mean, gs, ws.g_recon, ws.g_recon_t,
-                        ws.row_part_fused, ws.loss_colpart, ws.dec_ws, ws.n, ws.d)
+                        ws.row_part_fused, ws.loss_colpart, ws.dec_ws, ws.n, ws.d, norm_fin=nf)
     ws.row_ncb = ws.fused_ncb
     ws.loss_col_rows = ops.col_part_rows(ws.B)
 
@@ -367,7 +364,7 @@ def loss_finalize(ws, l1l0_out=None, host=None, seq=0):
     """Loss scalars / EV vectors.  After a forward (which left the l1 partials to be formed against the
     decoder norms) one launch does both (cc_loss_tail); a re-formed loss (same activations) only the
     finaliser.  host (a _hip.MappedHostBuffer): the scalars also land there, then `seq` in word 8."""
-    wait_norms(ws)
+    flush_norms(ws)  # (no-op after forward(), which ran the finaliser with or before G2)
     if ws.acts_pending:
         ops.loss_tail(ws.colsum_acts, ws.tn, ws.l1_part, _row_part(ws), ws.l0_part, ws.n_wave, ws.ev, ws.ev_a,
                       ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], l1l0_out=l1l0_out, host=host, seq=seq,
@@ -423,7 +420,7 @@ def dacts_rows(ws, P, l1_coeff, r0, r1, l1_grad_weight=1.0):
     """G3 over batch rows [r0, r1) (r0 % 256 == 0): g_pre rows + their column-sum partial rows."""
     l1_scale = float(l1_coeff) * l1_grad_weight / ws.B
     c0, c1 = ops.col_part_rows(r0), ops.col_part_rows(r1)
-    wait_norms(ws)
+    flush_norms(ws)
     with _span("G3_dacts"):
         if ws.tr:
             ops.dacts_bwd_t(ws.g_recon[r0:r1], P.W_dec_hk, ws.acts[r0:r1], ws.tn, l1_scale, ws.g_pre_t[:, r0:r1],
@@ -558,8 +555,9 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
             done.record(side_stream)
 
             def rest():
-                # the rows, then the norm finaliser on the side stream (G2 reads W_dec, not the norms: it waits
-                # only for the side stream's rows; G3 / the loss tail wait for the finaliser, wait_norms)
+                # the rows on the reader's stream, then it waits for the side stream's rows; the norm partials are
+                # then complete, and the finaliser rides in the next G2 launch (decode_loss: G3 and the loss tail,
+                # its first readers, run after G2) or runs before the first other reader (flush_norms)
                 cur = torch.cuda.current_stream(dev)
                 with _span("adam_dec_rest"):
                     if ws.h > hs:
@@ -567,16 +565,8 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
                                            **kw)
                     else:  # (every row on the side stream: b_dec only)
                         step_(*(t[hs * K:] for t in dec))
-                rest_done = torch.cuda.Event()
-                rest_done.record(cur)
-                with torch.cuda.stream(side_stream):
-                    side_stream.wait_event(rest_done)
-                    with _span("dec_norms"):
-                        ops.dec_norms_finalize(ws.norm_part, ws.h, ws.n, ws.d, ws.norms, ws.tn, ws.inv_norms)
-                    ws.norms_event = torch.cuda.Event()
-                    ws.norms_event.record(side_stream)
-                    ws.norms_stream = side_stream
                 cur.wait_event(done)
+                ws.norms_fin_pending = True
 
             ws.norms_token = _norms_token(P)
             P.pending_rest = rest

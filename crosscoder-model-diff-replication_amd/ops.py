@@ -211,13 +211,17 @@ def decode_loss_t(acts, W_dec_t, b_dec, x, x_mean, grad_scale, g_recon, g_recon_
                                  0 if ws is None else ws.numel(), B, h, n, d, dtype_code(acts.dtype), _stream(acts)))
 
 
-def decode_loss(acts, W_dec_hk, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t, row_part, col_part, ws, n, d):
+def decode_loss(acts, W_dec_hk, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t, row_part, col_part, ws, n, d,
+                norm_fin=None):
     """decode_loss_t reading W_dec [h, K] itself (cc_decode_loss, transposed LDS reads of the B operand): the same
-    bits without the W_dec^T copy.  g_recon_t may be None."""
+    bits without the W_dec^T copy.  g_recon_t may be None.  norm_fin = (part, norms, total, inv_norms): the decoder
+    norms' finaliser (dec_norms_finalize) rides in the launch."""
     B, h = acts.shape
+    part, norms, total, inv = norm_fin if norm_fin is not None else (None, None, None, None)
     check(lib().cc_decode_loss(_ptr(acts), _ptr(W_dec_hk), _ptr(b_dec), _ptr(x), _ptr(x_mean), grad_scale,
                                _ptr(g_recon), _ptr(g_recon_t), _ptr(row_part), _ptr(col_part), _ptr(ws),
-                               0 if ws is None else ws.numel(), B, h, n, d, dtype_code(acts.dtype), _stream(acts)))
+                               0 if ws is None else ws.numel(), _ptr(part), _ptr(norms), _ptr(total), _ptr(inv), B, h,
+                               n, d, dtype_code(acts.dtype), _stream(acts)))
 
 
 def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_scale, B, n, d, row0=0, rows=None,

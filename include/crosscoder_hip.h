@@ -179,10 +179,15 @@ int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, c
                      float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
                      int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream);
 /* cc_decode_loss_t reading W_dec [h][K] itself (the parameter, no transposed copy; same bits): the GEMM's B
- * operand goes through transposed LDS reads.  g_recon_t may be NULL here (not written then). */
+ * operand goes through transposed LDS reads.  g_recon_t may be NULL here (not written then).
+ * norm_part (optional, with norms / tn / inv_norms as in cc_dec_norms_finalize): the decoder norms'
+ * finaliser rides in the launch of the split-K leftover (or runs just before the GEMM where the shape has
+ * none) -- the same bits as cc_dec_norms_finalize(norm_part, h, n, d, norms, tn, inv_norms), ordered before
+ * whatever the stream runs next (crosscoder.py:123-125 for the backward and the loss tail). */
 int cc_decode_loss(const void* acts, const void* W_dec, const void* b_dec, const void* x, const float* x_mean,
                    float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
-                   int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream);
+                   int64_t ws_floats, const float* norm_part, float* norms, float* tn, float* inv_norms, int64_t B,
+                   int64_t h, int64_t n, int64_t d, int dtype, void* stream);
 
 /* Loss reduction (crosscoder.py:106-128, trainer.py:51-61): per-row explained variances
  * ev/ev_a/ev_b [B] (fp32) and scalars[0:8] = {l2, l1, l0, mean ev, mean ev_a, mean ev_b, 0, 0};

@@ -515,30 +515,30 @@ def test_decoder_adam_split_is_bit_identical(gpu, side_rows, monkeypatch):
     assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
 
 
-def test_delayed_norm_finaliser_still_orders_g3_and_wgrad(gpu, dbg_lib, monkeypatch):
-    """The decoder norms of a step come from a finaliser on the side stream (engine.adam's deferred rest);
-    G3 (reads tn) and G4G5 (reads inv_norms) run on the compute stream.  With the finaliser held back 3 ms
-    (a spin kernel queued before it on its stream: it then ends long after G2), both must still read the new
+def test_delayed_side_stream_adam_still_orders_the_norm_readers(gpu, dbg_lib, monkeypatch):
+    """A step's decoder norms come from partial sums the decoder-half Adam writes: most rows on the side stream
+    (beside the next G1), the rest on the compute stream, whose next G2 launch carries the finaliser (G3 reads
+    tn, G4G5 inv_norms, the side stream's loss tail tn).  With the side-stream launch held back 3 ms (a spin
+    kernel queued before it on its stream: it then ends long after G1), every reader must still see the new
     norms: losses, params and both moments equal an undelayed run's bit for bit."""
     import ctypes
 
-    from crosscoder_amd import engine, ops
     B, n, d, h = 1024, 2, 256, 2048
     cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
                num_tokens=B * 20, device=str(gpu))
-    orig = ops.dec_norms_finalize
+    orig = ops.adam_dec_norms
     outs = []
     for delay_ns in (0, 3_000_000):
-        def finalize(*a, _ns=delay_ns, **k):
-            if _ns:
+        def adam_dec_norms(*a, _ns=delay_ns, **k):
+            if _ns and k.get("max_blocks", 0) > 0:  # (the side-stream launch)
                 ops.check(dbg_lib.cc_debug_spin(1, 0, _ns, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
             orig(*a, **k)
 
-        monkeypatch.setattr(ops, "dec_norms_finalize", finalize)
+        monkeypatch.setattr(ops, "adam_dec_norms", adam_dec_norms)
         cc = ca.CrossCoder(cfg)
         tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 4, seed=5), crosscoder=cc)
         dicts = [tr.step() for _ in range(4)]
-        assert cc.arena().pending_rest is not None and engine.wait_norms is not None
+        assert cc.arena().pending_rest is not None  # (the deferred-rows path ran)
         st = tr.optimizer.state
         m = torch.cat([st[p]["exp_avg"].detach().flatten().float() for p in cc.parameters()])
         v = torch.cat([st[p]["exp_avg_sq"].detach().flatten().float() for p in cc.parameters()])
@@ -976,6 +976,23 @@ def test_decode_loss_on_wdec_matches_transposed(gpu, B, n, d, h):
     g_recon, g_t, rp, cp = outs[2]
     assert torch.equal(g_recon, outs[0][0]) and torch.equal(rp, outs[0][2]) and torch.equal(cp, outs[0][3])
     assert bool(torch.isnan(g_t.float()).all())
+    # the decoder norms' finaliser carried by the launch (the split-K leftover's, or before the GEMM where the
+    # shape has none): cc_dec_norms_finalize's bits, the GEMM outputs unchanged
+    part = torch.rand(ops.dec_norms_part_floats(h, n, d), generator=g).to(gpu)
+    ref = [torch.full(sh, float("nan"), device=gpu) for sh in ((h, n), (h,), (h, n))]
+    ops.dec_norms_finalize(part, h, n, d, *ref)
+    got = [torch.full_like(r, float("nan")) for r in ref]
+    g_recon = torch.full((B, K), float("nan"), dtype=bf, device=gpu)
+    g_t = torch.full((K, B), float("nan"), dtype=bf, device=gpu)
+    rp = torch.full((2, n * ncb, B), float("nan"), device=gpu)
+    cp = torch.full((ops.col_part_rows(B), K), float("nan"), device=gpu)
+    ops.decode_loss(acts, W, b_dec, x, x_mean, 2.0 / B, g_recon, g_t, rp, cp, torch.empty(nws, device=gpu), n, d,
+                    norm_fin=(part, *got))
+    torch.cuda.synchronize()
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+    for a, b in zip((g_recon, g_t, rp, cp), outs[1]):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("comm", ["all_reduce", "reduce_scatter"])
