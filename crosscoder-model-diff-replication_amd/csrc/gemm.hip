@@ -1000,7 +1000,8 @@ int cc_decode_fwd_ws_t(const void* acts, const void* W_dec_t, float* recon_f32, 
 // (row_part[2][n * d/64][B]), column sums of g_recon per 128-row group (col_part[B/128][K]), g_recon^T
 // through an LDS tile.  B % 8 == 0, d % 64 == 0.
 // Blocks with blockIdx.y >= part_rows (= cc_col_part_rows(B)) instead finalise the decoder norms from their
-// per-block partials (norms_finalize_row, one row per thread; nf_part NULL: none): the norms are first read
+// per-block partials (norms_finalize_row, 64 rows per block, one per lane of its first wave -- the stand-alone
+// finaliser's spread; 1024 rows per block took 70 us; nf_part NULL: none): the norms are first read
 // by G3 and by the side stream's loss tail, both after this launch, and their partials (the decoder-half
 // Adam's) are complete before G2 -- the finaliser rides here at no cost on the compute stream instead of
 // running on the side stream behind an event the compute stream must wait for.
@@ -1029,10 +1030,10 @@ __global__ __launch_bounds__(LSPLIT_THREADS) void loss_split_kernel(const LossSp
   constexpr int NW = LSPLIT_THREADS / 64;
   __shared__ __attribute__((aligned(16))) bf16_t tt[64 * TP];
   __shared__ float red[NW][64];
-  if ((int)blockIdx.y >= a.part_rows) {
-    const int row = (((int)blockIdx.y - a.part_rows) * (int)gridDim.x + (int)blockIdx.x) * LSPLIT_THREADS +
-                    (int)threadIdx.x;
-    if (row < a.nf_h) norms_finalize_row(a.nf_part, row, a.nf_n, a.nf_bpm, a.nf_norms, a.nf_total, a.nf_inv);
+  if ((int)blockIdx.y >= a.part_rows) {  // (64 rows per block, wave 0: the finaliser spread over many CUs)
+    const int row = (((int)blockIdx.y - a.part_rows) * (int)gridDim.x + (int)blockIdx.x) * 64 + (int)threadIdx.x;
+    if (threadIdx.x < 64 && row < a.nf_h)
+      norms_finalize_row(a.nf_part, row, a.nf_n, a.nf_bpm, a.nf_norms, a.nf_total, a.nf_inv);
     return;
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1183,7 +1184,7 @@ static int decode_loss(const void* acts, const void* W_dec, const void* b_dec, c
   if (norm_part) {
     l.nf_part = norm_part; l.nf_h = (int)h; l.nf_n = (int)n; l.nf_bpm = (int)(d / 64);
     l.nf_norms = norms; l.nf_total = tn; l.nf_inv = inv_norms;
-    fin_rows = (int)((h + (int64_t)gx * LSPLIT_THREADS - 1) / ((int64_t)gx * LSPLIT_THREADS));
+    fin_rows = (int)((h + (int64_t)gx * 64 - 1) / ((int64_t)gx * 64));
   }
   hipLaunchKernelGGL(loss_split_kernel, dim3((unsigned)gx, (unsigned)(l.part_rows + fin_rows)), dim3(LSPLIT_THREADS), 0,
                      st, l);

@@ -32,7 +32,7 @@ import contextlib
 
 import torch
 
-from . import ops
+from . import _hip, ops
 
 # Optional per-launch timer (bench.py installs one): an object with .span(name) -> context
 # manager recording HIP events on torch's current stream around the launch.
@@ -102,7 +102,7 @@ class Arena:
             rest, self.pending_rest = self.pending_rest, None
             rest()
         if self.pending is not None:
-            torch.cuda.current_stream(self.data.device).wait_event(self.pending)
+            self.pending.wait(torch.cuda.current_stream(self.data.device))
             self.pending = None
 
     def like(self, dtype=None, device=None):
@@ -165,6 +165,7 @@ class StepWorkspace:
         # the decoder-norm partials are complete but not yet finalised into norms / tn / inv_norms: the next G2
         # launch carries the finaliser (decode_loss), or flush_norms runs it before the first reader
         self.norms_fin_pending = False
+        self.fork_events = [None, None]  # the step's last stream-fork events (loss tail, decoder-half Adam)
         self.acts_t = E(h, B, dt=dtype) if self.tr else None
         # G1's activation mask as bits in the GEMM accumulator order: G3 reads 16 B per thread and tile instead
         # of the 128 KB acts tile (1/16 of the bytes, no LDS staging)
@@ -394,18 +395,18 @@ def loss_finalize_beside(ws, side_stream, on_losses=None, host=None, seq=0):
     go straight to mapped host memory (loss_finalize); then no event is recorded and None is returned,
     else the event that marks the tail's end."""
     dev = ws.x.device
-    ready = torch.cuda.Event()
-    ready.record(torch.cuda.current_stream(dev))
+    # (device-scope events for every stream-to-stream hand-off of the step: a torch event's system-scope release
+    # idles the recording stream ~1.7 us longer, profiles/r04_event_probe.txt)
+    ready = _hip.DeviceEvent().record(torch.cuda.current_stream(dev))
+    ws.fork_events[0] = ready  # (kept alive until the next step's fork: the side stream's wait references it)
     with torch.cuda.stream(side_stream):
-        side_stream.wait_event(ready)
+        ready.wait(side_stream)
         loss_finalize(ws, host=host, seq=seq)
         if on_losses is not None:
             on_losses(ws.scalars)
         if host is not None and on_losses is None:
             return None
-        done = torch.cuda.Event()
-        done.record(side_stream)
-    return done
+        return _hip.DeviceEvent().record(side_stream)
 
 
 def row_chunks(B, n_chunks):
@@ -446,7 +447,7 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
     if not dacts_done:
         dacts_rows(ws, P, l1_coeff, 0, B, l1_grad_weight)
     if tail_done is not None:
-        torch.cuda.current_stream(ws.x.device).wait_event(tail_done)
+        tail_done.wait(torch.cuda.current_stream(ws.x.device))
     if sums_out is not None and ws.tr:
         # G4 + G5 and the grad tail's per-parameter squared sums (for the all-reduce) in one launch
         with _span("G4G5_wgrad"):
@@ -533,10 +534,10 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
         step_(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), clip_out=ws.clip_out)
     # both halves are HBM-bound: the decoder half starts after the encoder half (run together they only
     # share the bandwidth), i.e. beside the next step's prep / G1 on the main stream
-    enc_done = torch.cuda.Event()
-    enc_done.record(torch.cuda.current_stream(dev))
+    enc_done = _hip.DeviceEvent().record(torch.cuda.current_stream(dev))
+    ws.fork_events[1] = enc_done
     with torch.cuda.stream(side_stream):
-        side_stream.wait_event(enc_done)
+        enc_done.wait(side_stream)
         if ws.W_dec_t is None and ws.norm_part is not None:
             # the decoder norms' partials come out of the Adam launches themselves (no pass over W_dec of their
             # own).  The side stream updates the first hs rows of W_dec beside the next step's G1; the first
@@ -551,8 +552,7 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
                 with _span("adam_dec"):
                     ops.adam_dec_norms(*(t[:hs * K] for t in dec), hs, K, *hp, ws.norm_part[:hs * nblk],
                                        max_blocks=DEC_ADAM_BLOCKS, **kw)
-            done = torch.cuda.Event()
-            done.record(side_stream)
+            done = _hip.DeviceEvent().record(side_stream)
 
             def rest():
                 # the rows on the reader's stream, then it waits for the side stream's rows; the norm partials are
@@ -565,7 +565,7 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
                                            **kw)
                     else:  # (every row on the side stream: b_dec only)
                         step_(*(t[hs * K:] for t in dec))
-                cur.wait_event(done)
+                done.wait(cur)
                 ws.norms_fin_pending = True
 
             ws.norms_token = _norms_token(P)
@@ -576,6 +576,5 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
             with _span("adam_dec"):
                 step_(P.dec_part(), G.dec_part(), M.dec_part(), V.dec_part(), max_blocks=DEC_ADAM_BLOCKS)
             norms_for_next(ws, P)
-            done = torch.cuda.Event()
-            done.record(side_stream)
+            done = _hip.DeviceEvent().record(side_stream)
     P.pending = done

@@ -106,7 +106,7 @@ class Trainer:
         on_losses(scalars): called (on the side stream) right after the loss scalars are enqueued, before
         the backward / clip / Adam launches."""
         scalars, done = self._launch_step(on_losses)
-        torch.cuda.current_stream(scalars.device).wait_event(done)
+        done.wait(torch.cuda.current_stream(scalars.device))
         return scalars
 
     def _launch_step(self, on_losses, host=None, seq=0):
