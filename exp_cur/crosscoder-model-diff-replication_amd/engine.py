@@ -495,6 +495,10 @@ DEC_ADAM_BLOCKS = 256
 # side launch gets one wave per SIMD (G1 holds the rest of the register file), which streams slowly once
 # G1 has finished.
 DEC_SIDE_ROWS = 0.92
+# False: the decoder half's Adam runs on torch's stream right after the encoder half, with the whole chip (no side
+# stream, nothing deferred) -- the alternative DESIGN.md section 3.3 measures against the overlap with G1
+DEC_ADAM_BESIDE_G1 = True
+SERIAL_DEC_BLOCKS = 0  # (0: the library's default grid for the serial form)
 
 
 def clip_and_adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, max_norm=1.0, side_stream=None):
@@ -532,6 +536,16 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
     dev = P.data.device
     with _span("adam"):
         step_(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), clip_out=ws.clip_out)
+    if not DEC_ADAM_BESIDE_G1 and ws.W_dec_t is None and ws.norm_part is not None:
+        # serial: the decoder half (+ the next step's norm partials) on this stream, the whole chip
+        dec = [A.dec_part() for A in (P, G, M, V)]
+        with _span("adam_dec"):
+            ops.adam_dec_norms(*dec, ws.h, ws.K, lr, beta1, beta2, eps, step, ws.norm_part,
+                               coef=coef if clip_sums is None else None, clip_sums=clip_sums, emulate=emulate,
+                               max_blocks=SERIAL_DEC_BLOCKS)
+        ws.norms_token = _norms_token(P)
+        ws.norms_fin_pending = True
+        return
     # both halves are HBM-bound: the decoder half starts after the encoder half (run together they only
     # share the bandwidth), i.e. beside the next step's prep / G1 on the main stream
     enc_done = _hip.DeviceEvent().record(torch.cuda.current_stream(dev))

@@ -490,18 +490,20 @@ def test_full_size_step_deterministic(gpu, full_size_case):
     assert outs[0][1]["l2_loss"] < outs[0][0]["l2_loss"]
 
 
-@pytest.mark.parametrize("side_rows", [0.0, 0.5, 1.0])
+@pytest.mark.parametrize("side_rows", [0.0, 0.5, 1.0, "serial"])
 def test_decoder_adam_split_is_bit_identical(gpu, side_rows, monkeypatch):
     """The decoder half of Adam split between the side stream (W_dec's first rows, beside the next G1) and the
     next reader's stream (the rest + b_dec, engine.DEC_SIDE_ROWS) gives the same bits for any split, including
-    every row deferred (0.0) and only b_dec deferred (1.0): params, both moments and the next step's losses."""
+    every row deferred (0.0), only b_dec deferred (1.0) and the whole half serial on the compute stream
+    (engine.DEC_ADAM_BESIDE_G1 False): params, both moments and the next step's losses."""
     from crosscoder_amd import engine
     B, n, d, h = 512, 2, 128, 1024
     cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
                num_tokens=B * 20, device=str(gpu))
     outs = []
     for frac in (engine.DEC_SIDE_ROWS, side_rows):
-        monkeypatch.setattr(engine, "DEC_SIDE_ROWS", frac)
+        monkeypatch.setattr(engine, "DEC_ADAM_BESIDE_G1", frac != "serial")
+        monkeypatch.setattr(engine, "DEC_SIDE_ROWS", engine.DEC_SIDE_ROWS if frac == "serial" else frac)
         cc = ca.CrossCoder(cfg)
         tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=4), crosscoder=cc)
         dicts = [tr.step() for _ in range(3)]
