@@ -314,12 +314,14 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
         if finalize:
             loss_finalize(ws)
         return
-    flush_norms(ws)
     with _span("G2_decode"):
         if ws.W_dec_t is not None:
             ops.decode_partial_t(ws.acts, ws.W_dec_t, ws.recon, ws.dec_ws)
         else:
             ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
+    # (G2 does not read the norms: their finaliser after it, where the latent-sharded step's collective on the
+    # reconstruction hides it)
+    flush_norms(ws)
     # B * l1 = sum_h colsum_acts[h] * tn[h] (crosscoder.py:126) rides in the loss finaliser's launch
     # (loss_tail)
     ws.acts_pending = True

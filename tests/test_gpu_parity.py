@@ -998,16 +998,19 @@ def test_decode_loss_on_wdec_matches_transposed(gpu, B, n, d, h):
 
 
 @pytest.mark.parametrize("comm", ["all_reduce", "reduce_scatter"])
-def test_sharded_trainer_world1_matches_trainer(gpu, comm):
-    """ShardedTrainer over a 1-rank RCCL group (the sliced async all-reduce path, 4 slices, or the
-    reduce-scatter + all-gather exchange) takes the same steps as the single-GPU Trainer."""
+@pytest.mark.parametrize("chunks", [1, 2])
+def test_sharded_trainer_world1_matches_trainer(gpu, comm, chunks):
+    """ShardedTrainer over a 1-rank RCCL group takes the same steps as the single-GPU Trainer, in the shipped
+    exchange forms: the all-reduce as one synchronous collective (1 slice, the world-1 default) or in the 2
+    batch slices of the world > 1 default (slice 2's exchange in flight during slice 1's loss rows + d_acts), and
+    the reduce-scatter + all-gather exchange."""
     import os
 
     import torch.distributed as dist
     from crosscoder_amd import sharded
 
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = str(29600 + os.getpid() % 1000 + (comm == "reduce_scatter"))
+    os.environ["MASTER_PORT"] = str(29600 + os.getpid() % 1000 + 2 * (comm == "reduce_scatter") + chunks)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
     try:
         B, n, d, h = 1024, 2, 256, 2048
@@ -1019,7 +1022,7 @@ def test_sharded_trainer_world1_matches_trainer(gpu, comm):
             if which == "single":
                 tr = ca.Trainer(cfg, buffer=buf, crosscoder=ca.CrossCoder(cfg))
             else:
-                tr = sharded.ShardedTrainer(cfg, buffer=buf, recon_chunks=4, comm=comm)
+                tr = sharded.ShardedTrainer(cfg, buffer=buf, recon_chunks=chunks, comm=comm)
             dicts.append([tr.step() for _ in range(3)])
             torch.cuda.synchronize()
             if which == "single":
@@ -1028,10 +1031,13 @@ def test_sharded_trainer_world1_matches_trainer(gpu, comm):
                 p_sharded = tr.crosscoder.arena().data.float().cpu()
         for a, b in zip(*dicts):
             for k in ("l2_loss", "l1_loss", "l0_loss", "explained_variance"):
-                assert math.isclose(a[k], b[k], rel_tol=1e-3, abs_tol=1e-3), (k, a[k], b[k])
+                assert math.isclose(a[k], b[k], rel_tol=2e-4, abs_tol=1e-4), (k, a[k], b[k])
             assert a["lr"] == b["lr"] and a["l1_coeff"] == b["l1_coeff"]
-        # clip sums are combined in a different order (torch sums vs the clip kernel): <= 1 bf16 ulp of drift
-        assert (p_single - p_sharded).abs().max().item() <= 4 * 5e-5 + 1e-3 * p_single.abs().max().item()
+        # the reconstruction (fp32 partial + b_dec, vs the fused G2 + loss) and the clip sums are combined in a
+        # different order: a bf16 rounding may flip, the bounds of test_gpu_sharded.py
+        d = (p_single - p_sharded).abs()
+        assert d.max().item() <= 4 * cfg["lr"] + 2 ** -7 * p_single.abs().max().item(), d.max().item()
+        assert (d == 0).float().mean().item() > 0.9
     finally:
         dist.destroy_process_group()
 
