@@ -21,6 +21,22 @@ CC_LAYOUT_KC = 0
 CC_LAYOUT_MN = 1
 
 _p = ctypes.c_void_p
+
+
+class LossTailJob(ctypes.Structure):
+    """cc_loss_tail_job (include/crosscoder_hip.h)"""
+    _fields_ = [("colsum_acts", ctypes.c_void_p), ("tn", ctypes.c_void_p), ("h", ctypes.c_int64),
+                ("l1_part", ctypes.c_void_p), ("row_part", ctypes.c_void_p), ("ncb", ctypes.c_int64),
+                ("l0_part", ctypes.c_void_p), ("n_l0", ctypes.c_int64), ("ev", ctypes.c_void_p),
+                ("ev_a", ctypes.c_void_p), ("ev_b", ctypes.c_void_p), ("scalars", ctypes.c_void_p),
+                ("l1l0_out", ctypes.c_void_p), ("host_out", ctypes.c_void_p), ("seq", ctypes.c_uint32),
+                ("B", ctypes.c_int64), ("n", ctypes.c_int64), ("counter", ctypes.c_void_p)]
+
+
+class ColsumJob(ctypes.Structure):
+    """cc_colsum_job (include/crosscoder_hip.h)"""
+    _fields_ = [("part", ctypes.c_void_p), ("rows", ctypes.c_int64), ("cols", ctypes.c_int64), ("ld", ctypes.c_int64),
+                ("scale", ctypes.c_float), ("out", ctypes.c_void_p)]
 _i64 = ctypes.c_int64
 _i = ctypes.c_int
 _f = ctypes.c_float
@@ -76,12 +92,12 @@ SIGNATURES = {
                                  _i64, _p]),
     "cc_decode_loss_ncb": (_i64, [_i64, _i64, _i64, _i64, _i]),
     "cc_decode_loss_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i, _p]),
-    "cc_decode_loss": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i,
-                            _p]),
+    "cc_decode_loss": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64,
+                            _i, _p]),
     "cc_transposed_ok": (_i, [_i64, _i64, _i64, _i]),
-    "cc_encode_fwd_t": (_i, [_p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_encode_fwd_t": (_i, [_p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_mask_bits_words": (_i64, [_i64, _i64]),
-    "cc_dacts_bwd_t": (_i, [_p, _p, _p, _p, _f, _p, _p, _i64, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "cc_dacts_bwd_t": (_i, [_p, _p, _p, _p, _f, _p, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_transpose_b16": (_i, [_p, _i64, _i64, _i64, _p, _i64, _p]),
     "cc_dec_norms_part_floats": (_i64, [_i64, _i64, _i64]),
     "cc_transpose_dec_norms": (_i, [_p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p]),

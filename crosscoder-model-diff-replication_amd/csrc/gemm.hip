@@ -32,6 +32,9 @@
 
 namespace cc {
 
+#include "grad_tail.h"
+#include "loss_tail.h"
+
 constexpr int BM = 256, NTHR = 512;
 constexpr uint32_t OOB = 0x7ffffff0u;  // voffset that the range check always rejects
 constexpr uint32_t MAX_RECORDS = 0x7fffffe0u;
@@ -66,6 +69,10 @@ struct GemmArgs {
   uint32_t* mask_bits;  // ping-pong EPI_ENC (out) / EPI_DACTS FAST (in): the activation mask, 1 bit per output
                         // in accumulator order: [tile tm*nbn + tn][thread][4] u32, bit 4(4i+j)+e of fragment (i,j)
   uint32_t* tile_ctr;   // persistent ping-pong launches: 8 per-XCD tile counters (dynamic order), NULL: static
+  RedSeg pre;           // a column reduction the launch runs before its tiles (cc_colsum_job), pre_blocks > 0
+  int pre_blocks;
+  LossTailArgs tail;    // the forward's loss tail the launch runs before its tiles (cc_loss_tail_job), tail_items > 0
+  int tail_items;
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -547,7 +554,6 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 }
 
 #include "gemm_pp.h"
-#include "grad_tail.h"
 
 // ---- G4 + G5 with the gradient tail in the same launch (the single-GPU step's backward end).
 // What the stand-alone tail kernel (cc_grad_tail) runs after the weight-gradient GEMMs, here inside
@@ -688,6 +694,27 @@ static bool use_pp(int64_t N, bool akc, bool bkc, int dtype) {
 }
 // 1 when the transposed-operand entries (cc_encode_fwd_t, cc_dacts_bwd_t, cc_wgrad_both_t's fused
 // form) serve this step shape.
+// A cc_colsum_job as the launch's prologue reduction (reduce_rows' fields: out_f32 only).
+static int set_pre(GemmArgs& a, const cc_colsum_job* job) {
+  if (!job) return CC_OK;
+  if (!job->part || !job->out) return CC_ERR_NULL;
+  if (job->rows <= 0 || job->cols <= 0 || job->ld < job->cols) return CC_ERR_SHAPE;
+  a.pre = {job->part, (int)job->rows, (int)job->cols, job->ld, job->scale, job->out, nullptr, nullptr, nullptr, nullptr};
+  a.pre_blocks = (int)((job->cols + RED_COLS - 1) / RED_COLS);
+  return CC_OK;
+}
+
+// A cc_loss_tail_job as the launch's prologue work.
+static int set_tail(GemmArgs& a, const cc_loss_tail_job* j) {
+  if (!j) return CC_OK;
+  if (!j->colsum_acts || !j->tn || !j->l1_part || !j->row_part || !j->scalars || !j->counter) return CC_ERR_NULL;
+  if (j->h <= 0 || j->B <= 0 || j->n <= 0 || j->ncb <= 0) return CC_ERR_SHAPE;
+  a.tail = make_loss_tail_args(j->colsum_acts, j->tn, j->h, j->l1_part, j->row_part, j->ncb, j->l0_part, j->n_l0, j->ev,
+                               j->ev_a, j->ev_b, j->scalars, j->l1l0_out, j->host_out, j->seq, j->B, j->n, j->counter);
+  a.tail_items = a.tail.l1_wgs + a.tail.ev.nblk;
+  return CC_OK;
+}
+
 extern "C" int cc_transposed_ok(int64_t B, int64_t K, int64_t h, int dtype) {
   return dtype == CC_BF16 && B % 8 == 0 && K % 8 == 0 && h % 8 == 0 && use_pp(h, true, true, dtype) &&
          use_pp(K, true, true, dtype);
@@ -828,7 +855,8 @@ int64_t cc_mask_bits_words(int64_t B, int64_t h) { return n_blocks(B, h, 256) * 
 
 int cc_encode_fwd_t(const void* x, const void* W_enc, const void* b_enc, const float* tn, void* acts, void* acts_t,
                     int apply_relu, float* colsum_part, float* l1_part, float* l0_part, uint32_t* mask_bits,
-                    uint32_t* tile_ctr, int64_t B, int64_t K, int64_t h, int dtype, void* stream) {
+                    uint32_t* tile_ctr, const cc_colsum_job* pre, int64_t B, int64_t K, int64_t h, int dtype,
+                    void* stream) {
   if (!acts || !acts_t) return CC_ERR_NULL;
   if (l1_part && !tn) return CC_ERR_NULL;
   GemmArgs a = {};
@@ -839,6 +867,7 @@ int cc_encode_fwd_t(const void* x, const void* W_enc, const void* b_enc, const f
   a.out_t = acts_t; a.ldt = B; a.mask_bits = mask_bits; a.tile_ctr = tile_ctr;
   int rc = check_gemm(a, dtype, true, true);
   if (rc) return rc;
+  if ((rc = set_pre(a, pre))) return rc;
   if (B % 8 || !al16(acts_t) || !use_pp(a.N, true, true, dtype)) return CC_ERR_SHAPE;
   if (mask_bits && !al16(mask_bits)) return CC_ERR_ALIGN;
   return launch_pp<true, true, EPI_ENC>(a, (hipStream_t)stream);
@@ -1121,8 +1150,8 @@ int64_t cc_decode_loss_ncb(int64_t B, int64_t h, int64_t n, int64_t d, int dtype
 template <bool BKC>
 static int decode_loss(const void* acts, const void* W_dec, const void* b_dec, const void* x, const float* x_mean,
                        float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
-                       int64_t ws_floats, const float* norm_part, float* norms, float* tn, float* inv_norms, int64_t B,
-                       int64_t h, int64_t n, int64_t d, int dtype, hipStream_t st) {
+                       int64_t ws_floats, const float* norm_part, float* norms, float* tn, float* inv_norms,
+                       const cc_colsum_job* pre, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, hipStream_t st) {
   if (!acts || !W_dec || !b_dec || !x || !x_mean || !g_recon || !row_part || !col_part) return CC_ERR_NULL;
   if (BKC && !g_recon_t) return CC_ERR_NULL;
   if (!cc_decode_loss_ncb(B, h, n, d, dtype) || !use_pp(n * d, true, BKC, dtype)) return CC_ERR_SHAPE;
@@ -1144,6 +1173,7 @@ static int decode_loss(const void* acts, const void* W_dec, const void* b_dec, c
   a.col_part = col_part; a.row_part = row_part; a.d_model = (int)d; a.n_models = (int)n;
   int rc = check_gemm(a, dtype, true, BKC);
   if (rc) return rc;
+  if ((rc = set_pre(a, pre))) return rc;
   a.nbm = (a.M + BM - 1) / BM;
   a.nbn = (a.N + 255) / 256;
   const bool fast = B % BM == 0 && a.N % 256 == 0;
@@ -1198,15 +1228,16 @@ int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, c
                      float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
                      int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
   return decode_loss<true>(acts, W_dec_t, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t, row_part, col_part, ws,
-                           ws_floats, nullptr, nullptr, nullptr, nullptr, B, h, n, d, dtype, (hipStream_t)stream);
+                           ws_floats, nullptr, nullptr, nullptr, nullptr, nullptr, B, h, n, d, dtype,
+                           (hipStream_t)stream);
 }
 
 int cc_decode_loss(const void* acts, const void* W_dec, const void* b_dec, const void* x, const float* x_mean,
                    float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
-                   int64_t ws_floats, const float* norm_part, float* norms, float* tn, float* inv_norms, int64_t B,
-                   int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
+                   int64_t ws_floats, const float* norm_part, float* norms, float* tn, float* inv_norms,
+                   const cc_colsum_job* pre, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
   return decode_loss<false>(acts, W_dec, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t, row_part, col_part, ws,
-                            ws_floats, norm_part, norms, tn, inv_norms, B, h, n, d, dtype, (hipStream_t)stream);
+                            ws_floats, norm_part, norms, tn, inv_norms, pre, B, h, n, d, dtype, (hipStream_t)stream);
 }
 
 int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
@@ -1229,7 +1260,7 @@ extern "C" {
 // >= B; a batch slice passes g_pre_t + r0).  bf16, B % 8 == 0, ldt % 8 == 0, ping-pong path only.
 int cc_dacts_bwd_t(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
                    const uint32_t* mask_bits, void* g_pre_t, int64_t ldt, float* colsum_part, uint32_t* tile_ctr,
-                   int64_t B, int64_t K, int64_t h, int dtype, void* stream) {
+                   const cc_loss_tail_job* tail, int64_t B, int64_t K, int64_t h, int dtype, void* stream) {
   if (!g_pre_t || !acts) return CC_ERR_NULL;
   GemmArgs a = {};
   a.A = g_recon; a.lda = K; a.B = W_dec; a.ldb = K;
@@ -1239,6 +1270,7 @@ int cc_dacts_bwd_t(const void* g_recon, const void* W_dec, const void* acts, con
   a.tile_ctr = tile_ctr;
   int rc = check_gemm(a, dtype, true, true);
   if (rc) return rc;
+  if ((rc = set_tail(a, tail))) return rc;
   if (mask_bits && !al16(mask_bits)) return CC_ERR_ALIGN;
   if (B % 8 || ldt % 8 || ldt < B || !al16(g_pre_t) || !use_pp(a.N, true, true, dtype)) return CC_ERR_SHAPE;
   return launch_pp<true, true, EPI_DACTS>(a, (hipStream_t)stream);

@@ -482,9 +482,61 @@ struct TileLoop {
   }
 };
 
+// The launch's prologue reduction (GemmArgs::pre: reduce_rows' two phases, the same bits as cc_reduce_rows):
+// 256-thread group g of workgroup b reduces column blocks 2b + g, 2b + g + 2 * grid, ... before b's first tile.
+// A few workgroups start their tiles ~2 us late (the dynamic tile order evens that out); the step saves a launch.
+// (nwg: the workgroups [0, nwg) that run it)
+CC_DEV void pp_prologue_reduce(const GemmArgs& a, char* smem, int nwg) {
+  if (a.pre_blocks <= 0) return;
+  const int grp = threadIdx.x >> 8, t = threadIdx.x & 255;
+  float(*red)[RED_COLS] = (float(*)[RED_COLS])(smem + grp * 4 * RED_COLS * sizeof(float));
+  for (int base = 2 * (int)blockIdx.x; base < a.pre_blocks; base += 2 * nwg) {  // uniform per workgroup
+    const int b = base + grp;
+    if (b < a.pre_blocks) reduce_rows_phase1(a.pre, b, t, red);
+    __syncthreads();
+    if (b < a.pre_blocks) reduce_rows_phase2<CC_F32>(a.pre, b, t, red);
+    __syncthreads();
+  }
+}
+
+// The forward's loss tail as prologue work of the launch (GemmArgs::tail, tail_items > 0; LossTailArgs items,
+// loss_tail.h): 256-thread group g of workgroup b runs items 2b + g, 2b + g + 2 P, ... (P participating
+// workgroups); the participants then count arrivals and the last one runs the loss-scalar finaliser.  That
+// workgroup starts its tiles ~10 us late; the dynamic tile order evens it out.  The step saves the side
+// stream's loss-tail launch and the stream fork before it.
+CC_DEV void pp_prologue_loss_tail(const GemmArgs& a, char* smem) {
+  if (a.tail_items <= 0) return;
+  const int np = min((int)gridDim.x, (a.tail_items + 1) / 2);
+  if ((int)blockIdx.x >= np) return;  // (uniform per workgroup)
+  const int grp = threadIdx.x >> 8, t = threadIdx.x & 255;
+  float(*evred)[4] = (float(*)[4])(smem + grp * 64);
+  for (int base = 2 * (int)blockIdx.x; base < a.tail_items; base += 2 * np) {
+    const int item = base + grp;
+    loss_tail_item(a.tail, item < a.tail_items ? item : -1, t, evred);
+    __syncthreads();
+  }
+  int* last = (int*)(smem + 256);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const bool is_last = atomicAdd(a.tail.counter, 1u) == (unsigned)(np - 1);
+    if (is_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    *last = is_last;
+  }
+  __syncthreads();
+  if (*last) {
+    loss_scalars_body<LOSS_THREADS>(a.tail.scal, (double(*)[6])(smem + 512));
+    if (threadIdx.x == 0) atomicExch(a.tail.counter, 0u);
+  }
+  __syncthreads();  // (the tiles reuse the LDS)
+}
+
 template <bool AKC, bool BKC, int EPI, bool FAST = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(16))) char smem[EPI == EPI_WGDEC ? PP_LDS_W : PP_LDS];
+  pp_prologue_reduce(args, smem, gridDim.x);
+  pp_prologue_loss_tail(args, smem);
   for (TileLoop L(args.nbm * args.nbn, args.tile_ctr); L.more();) {
     pp_tile<AKC, BKC, EPI, FAST>(args, smem, L.begin(), pp_opaque_tid());
     pp_tile_boundary();
@@ -520,6 +572,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_main_splitk_kernel(const Gemm
   __shared__ __attribute__((aligned(16))) char smem[PP_LDS];
   const int nb0 = a0.nbm * a0.nbn;
   if ((int)blockIdx.x < nb0) {
+    pp_prologue_reduce(a0, smem, nb0);
     pp_tile<AKC, BKC, EPI, FAST>(a0, smem, blockIdx.x);
     return;
   }

@@ -1,6 +1,6 @@
-// Loss-tail building blocks shared by the stand-alone finaliser kernels (step_kernels.hip) and the d_acts
-// GEMM that runs the loss tail in its own launch (gemm.hip): per-row explained variances + their partial
-// sums, and the single-block loss-scalar finaliser.  Included inside namespace cc.
+// Loss-tail building blocks shared by the stand-alone kernels (step_kernels.hip) and the d_acts GEMM that
+// carries the loss tail in its launch (gemm.hip): per-row explained variances + their partial sums, the l1
+// partials, and the single-block loss-scalar finaliser.  Included inside namespace cc.
 #pragma once
 
 // Per-row explained variances (crosscoder.py:110-121) + per-block partial sums of the row terms.
@@ -12,6 +12,7 @@ struct EvSeg {
   float* ev_a;
   float* ev_b;
   float* part_out;
+  int nblk;  // ceil(B / 256) blocks (used by the fused tails)
 };
 CC_DEV void ev_phase1(const EvSeg& a, int blk, int t, float (*red)[4]) {
   const int r = blk * 256 + t;
@@ -83,6 +84,7 @@ struct ScalArgs {
   float* host_out;
   unsigned seq;
 };
+// (Called by every thread of a block of >= NT threads; threads from NT on take no part but the barriers.)
 template <int NT>
 CC_DEV void loss_scalars_body(const ScalArgs& sa, double (*red)[6]) {
   const float* __restrict__ ev_part = sa.ev_part;
@@ -97,8 +99,9 @@ CC_DEV void loss_scalars_body(const ScalArgs& sa, double (*red)[6]) {
   float* __restrict__ host_out = sa.host_out;
   const unsigned seq = sa.seq;
   constexpr int NW = NT / 64;
+  const int tid = threadIdx.x < NT ? (int)threadIdx.x : (1 << 30);  // (no element for threads >= NT)
   double acc[6] = {0, 0, 0, 0, 0, 0};
-  for (int i = threadIdx.x; i < nblk; i += NT) {
+  for (int i = tid; i < nblk; i += NT) {
     acc[0] += ev_part[i * 4 + 0];
     acc[3] += ev_part[i * 4 + 1];
     acc[4] += ev_part[i * 4 + 2];
@@ -107,7 +110,7 @@ CC_DEV void loss_scalars_body(const ScalArgs& sa, double (*red)[6]) {
   // 8 independent loads in flight per trip (clamped index, no branch around a load); each thread still adds
   // its elements i, i + NT, i + 2 NT, ... in order
   if (l0_part) {
-    for (int64_t i = threadIdx.x; i < n_wave; i += 8 * NT) {
+    for (int64_t i = tid; i < n_wave; i += 8 * NT) {
       float b[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -119,11 +122,11 @@ CC_DEV void loss_scalars_body(const ScalArgs& sa, double (*red)[6]) {
     }
   }
   if (l1_part)
-    for (int64_t i = threadIdx.x; i < n_l1; i += NT) acc[1] += l1_part[i];
+    for (int64_t i = tid; i < n_l1; i += NT) acc[1] += l1_part[i];
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
     double s = wave_sum_d(acc[q]);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = s;
+    if ((threadIdx.x & 63) == 0 && threadIdx.x < NT) red[threadIdx.x >> 6][q] = s;
   }
   __syncthreads();
   if (threadIdx.x < 6) {
@@ -148,3 +151,54 @@ CC_DEV void loss_scalars_body(const ScalArgs& sa, double (*red)[6]) {
   }
 }
 
+
+// The forward's loss tail (crosscoder.py:106-128) as work items of a launch:
+//   items [0, l1_wgs): 4 blocks of 64 latents, one per wave: B * l1's partial sum_j colsum[j] * tn[j] -- the dot
+//     reduce_rows_phase2 forms (colsum IS that reduction of the encoder's column slab, scale 1): the same bits;
+//   items [l1_wgs, l1_wgs + ev_blocks): 256 batch rows each (ev_phase1/2);
+// then the last participant to arrive runs loss_scalars_body<LOSS_THREADS>.
+struct LossTailArgs {
+  const float* colsum;
+  const float* tn;
+  int h;
+  float* l1_part;
+  int l1_wgs;
+  EvSeg ev;
+  ScalArgs scal;
+  unsigned* counter;
+};
+// One item by a 256-thread group (t = thread in the group, evred: 16 floats of the group's LDS).  The EV item
+// has a barrier between its phases: every 256-thread group of the workgroup calls this the same number of times
+// (item < 0: none, barriers only).
+CC_DEV void loss_tail_item(const LossTailArgs& a, int item, int t, float (*evred)[4]) {
+  if (item >= 0 && item < a.l1_wgs) {
+    const int lane = t & 63, blk = item * 4 + (t >> 6), j = blk * 64 + lane;
+    float dot = j < a.h ? a.colsum[j] * a.tn[j] : 0.f;
+    dot = wave_sum(dot);
+    if (lane == 0 && blk * 64 < a.h) a.l1_part[blk] = dot;
+  }
+  const bool ev = item >= a.l1_wgs && item < a.l1_wgs + a.ev.nblk;
+  if (ev) ev_phase1(a.ev, item - a.l1_wgs, t, evred);
+  __syncthreads();
+  if (ev) ev_phase2(a.ev, item - a.l1_wgs, t, evred);
+}
+
+// LossTailArgs of cc_loss_tail / a cc_loss_tail_job (host side).
+static inline LossTailArgs make_loss_tail_args(const float* colsum_acts, const float* tn, int64_t h, float* l1_part,
+                                               const float* row_part, int64_t ncb, const float* l0_part, int64_t n_l0,
+                                               float* ev, float* ev_a, float* ev_b, float* scalars, float* l1l0_out,
+                                               float* host_out, uint32_t seq, int64_t B, int64_t n, uint32_t* counter) {
+  LossTailArgs a = {};
+  const int nred = (int)((h + 63) / 64);
+  const int nblk = (int)((B + 255) / 256);
+  float* ev_part = scalars + 8;  // as cc_loss_finalize (cc_loss_scalars_len)
+  a.colsum = colsum_acts;
+  a.tn = tn;
+  a.h = (int)h;
+  a.l1_part = l1_part;
+  a.l1_wgs = (nred + 3) / 4;
+  a.ev = {row_part, (int)B, (int)n, (int)ncb, ev, ev_a, ev_b, ev_part, nblk};
+  a.scal = {ev_part, nblk, l1_part, nred, l0_part, n_l0, (int)B, scalars, l1l0_out, host_out, (unsigned)seq};
+  a.counter = counter;
+  return a;
+}

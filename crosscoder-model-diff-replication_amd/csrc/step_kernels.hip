@@ -330,42 +330,17 @@ __global__ __launch_bounds__(SCAL_THREADS) void tail_kernel(const TailArgs a) {
 }
 
 // Fused loss tail (crosscoder.py:106-128): the l1 partials, the per-row EV terms and the loss scalars in one
-// launch whose workgroups fit beside a persistent GEMM workgroup -- the step runs it on a side stream during
-// G3, which holds 2 x 216 of each SIMD's 512 VGPRs and 128 KB of each CU's LDS, so a workgroup of 256 threads
-// (one wave per SIMD), few registers and < 0.5 KB of LDS starts at once instead of after G3.
-//   workgroups [0, l1_wgs): one 64-latent block per wave, B * l1's partial sum_j colsum[j] * tn[j] -- the dot
-//     reduce_rows_phase2 forms (colsum IS that reduction of G1's column slab, scale 1), so the same bits;
-//   the next ev_blocks workgroups: 256 batch rows each (ev_phase1/2);
-//   the last workgroup to arrive: loss_scalars_body<LOSS_THREADS> (the stand-alone loss_scalars_kernel's).
-struct LossTailArgs {
-  const float* colsum;
-  const float* tn;
-  int h;
-  float* l1_part;
-  int l1_wgs;
-  EvSeg ev;
-  ScalArgs scal;
-  unsigned* counter;
-};
+// launch of the LossTailArgs items (loss_tail.h), one 256-thread workgroup per item, whose workgroups fit beside a
+// persistent GEMM workgroup (256 threads, few registers, < 0.5 KB of LDS); the last workgroup to arrive runs
+// loss_scalars_body<LOSS_THREADS> (the stand-alone loss_scalars_kernel's).
 __global__ __launch_bounds__(LOSS_THREADS) void loss_tail_kernel(const LossTailArgs a) {
   __shared__ float evred[4][4];
   __shared__ double sred[LOSS_THREADS / 64][6];
   __shared__ int last;
-  const int t = threadIdx.x;
-  if ((int)blockIdx.x < a.l1_wgs) {
-    const int lane = t & 63, blk = (int)blockIdx.x * 4 + (t >> 6), j = blk * 64 + lane;
-    float dot = j < a.h ? a.colsum[j] * a.tn[j] : 0.f;
-    dot = wave_sum(dot);
-    if (lane == 0 && blk * 64 < a.h) a.l1_part[blk] = dot;
-  } else {
-    const int b = (int)blockIdx.x - a.l1_wgs;
-    ev_phase1(a.ev, b, t, evred);
-    __syncthreads();
-    ev_phase2(a.ev, b, t, evred);
-  }
+  loss_tail_item(a, blockIdx.x, threadIdx.x, evred);
   if (!arrive_last(a.counter, &last)) return;
   loss_scalars_body<LOSS_THREADS>(a.scal, sred);
-  if (t == 0) atomicExch(a.counter, 0u);
+  if (threadIdx.x == 0) atomicExch(a.counter, 0u);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -838,7 +813,7 @@ int cc_loss_finalize_nb(const float* row_part, int64_t ncb_rows, const float* l1
   int nblk = (int)((B + 255) / 256);
   float* ev_part = scalars + 8;
   hipStream_t st = (hipStream_t)stream;
-  const EvSeg e = {row_part, (int)B, (int)n, ncb, ev, ev_a, ev_b, ev_part};
+  const EvSeg e = {row_part, (int)B, (int)n, ncb, ev, ev_a, ev_b, ev_part, nblk};
   hipLaunchKernelGGL(ev_kernel, dim3(nblk), dim3(256), 0, st, e);
   const ScalArgs s = {ev_part, nblk, l1_part, n_l1, l0_part, n_l0, (int)B, scalars, l1l0_out, host_out, (unsigned)seq};
   hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(LOSS_THREADS), 0, st, s);
@@ -1052,18 +1027,9 @@ int cc_loss_tail(const float* colsum_acts, const float* tn, int64_t h, float* l1
                  void* stream) {
   if (!colsum_acts || !tn || !l1_part || !row_part || !scalars || !counter) return CC_ERR_NULL;
   if (h <= 0 || B <= 0 || n <= 0 || d <= 0 || ncb <= 0) return CC_ERR_SHAPE;
-  LossTailArgs a = {};
-  const int nred = (int)((h + RED_COLS - 1) / RED_COLS);
-  const int nblk = (int)((B + 255) / 256);
-  float* ev_part = scalars + 8;  // as cc_loss_finalize (cc_loss_scalars_len)
-  a.colsum = colsum_acts;
-  a.tn = tn;
-  a.h = (int)h;
-  a.l1_part = l1_part;
-  a.l1_wgs = (nred + 3) / 4;
-  a.ev = {row_part, (int)B, (int)n, (int)ncb, ev, ev_a, ev_b, ev_part};
-  a.scal = {ev_part, nblk, l1_part, nred, l0_part, n_l0, (int)B, scalars, l1l0_out, host_out, (unsigned)seq};
-  a.counter = counter;
+  const LossTailArgs a = make_loss_tail_args(colsum_acts, tn, h, l1_part, row_part, ncb, l0_part, n_l0, ev, ev_a, ev_b,
+                                             scalars, l1l0_out, host_out, seq, B, n, counter);
+  const int nblk = a.ev.nblk;
   hipLaunchKernelGGL(loss_tail_kernel, dim3((unsigned)(a.l1_wgs + nblk)), dim3(LOSS_THREADS), 0,
                      (hipStream_t)stream, a);
   CC_LAUNCH_CHECK();

@@ -49,6 +49,12 @@ def _span(name):
 DYNAMIC_TILES = True
 
 
+# The Trainer's loss tail rides in the backward's G3 launch (its first workgroups run it before their tiles, the
+# dynamic tile order evens out their late start; cc_dacts_bwd_t's tail job), instead of a side-stream launch
+# forked from the compute stream before G3.  The same bits either way.
+LOSS_TAIL_IN_G3 = True
+
+
 def _tile_ctr(ws, k):
     return ws.tile_ctr[k] if DYNAMIC_TILES else None
 
@@ -166,6 +172,7 @@ class StepWorkspace:
         # launch carries the finaliser (decode_loss), or flush_norms runs it before the first reader
         self.norms_fin_pending = False
         self.fork_events = [None, None]  # the step's last stream-fork events (loss tail, decoder-half Adam)
+        self.tail_deferred = None  # (host, seq) of a loss tail the next whole-batch G3 launch carries
         self.acts_t = E(h, B, dt=dtype) if self.tr else None
         # G1's activation mask as bits in the GEMM accumulator order: G3 reads 16 B per thread and tile instead
         # of the 128 KB acts tile (1/16 of the bytes, no LDS staging)
@@ -292,24 +299,28 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     ws.next_slot()
     with _span("prep"):
         ops.prep_input(x_in, factor, ws.dtype, out=ws.x, colsum_part=ws.x_colpart, out_t=ws.x_t)
-    # G1 reads only the encoder half: it may overlap the previous step's decoder-half Adam
+    # G1 reads only the encoder half: it may overlap the previous step's decoder-half Adam.  x.mean(0) (first
+    # read by the loss) and sum_b acts (G4's L1 term and the l1 loss, crosscoder.py:112,126): column reductions
+    # of the prep / G1 partial slabs -- carried in the prologues of G1 and G2 where the step's fused path runs
+    # (cc_colsum_job: no launches of their own), else two reduce_rows launches after G1
+    fused = bool(loss and ws.fused_ncb)  # (fused_ncb: the transposed-operand step only)
+    x_job = ops.colsum_job(ws.x_colpart, ws.x_colpart.shape[0], K, 1.0 / B, ws.x_mean) if fused else None
     with _span("G1_encode"):
         if ws.tr:
             ops.encode_fwd_t(ws.x, P.W_enc_hk, P.b_enc, ws.acts, ws.acts_t, True, colsum_part=ws.acts_colpart,
-                             l0_part=ws.l0_part, mask_bits=ws.mask_bits, tile_ctr=_tile_ctr(ws, 0))
+                             l0_part=ws.l0_part, mask_bits=ws.mask_bits, tile_ctr=_tile_ctr(ws, 0), pre=x_job)
         else:
             ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, colsum_part=ws.acts_colpart,
                            l0_part=ws.l0_part)
-    # x.mean(0) is first read by the loss kernel: reduced here it runs while the stream would
-    # otherwise idle waiting for the side stream's decoder-half Adam (G1 starts 8 us earlier)
-    ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
-    # sum_b acts (G4's L1 term, crosscoder.py:126) likewise, in the same wait; the l1 dots against the
-    # decoder norms (not known before the side stream's pass) stay in the loss tail
-    ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts)
+    if not fused:
+        ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
+        ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts)
     P.wait_pending()
     decoder_norms(ws, P)  # (+ W_dec^T), unless launched already after the last Adam
     if loss and ws.fused_ncb:
-        decode_loss(ws, P, grad_scale)  # (carries a pending norm finaliser)
+        # (carries a pending norm finaliser and, fused, the activation column sums)
+        decode_loss(ws, P, grad_scale, pre=ops.colsum_job(ws.acts_colpart, ws.acts_colpart.shape[0], h, 1.0,
+                                                          ws.colsum_acts) if fused else None)
         ws.acts_pending = True
         if finalize:
             loss_finalize(ws)
@@ -331,15 +342,15 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
             loss_finalize(ws)
 
 
-def decode_loss(ws, P, grad_scale=None):
+def decode_loss(ws, P, grad_scale=None, pre=None):
     """G2 + loss rows + g_recon (and g_recon^T) in one pass over the whole batch (decode_loss: W_dec read
-    directly)."""
+    directly).  pre: an ops.colsum_job the launch runs first."""
     gs = 2.0 / ws.B if grad_scale is None else grad_scale
     nf = (ws.norm_part, ws.norms, ws.tn, ws.inv_norms) if ws.norms_fin_pending else None
     ws.norms_fin_pending = False
     with _span("G2_decode"):
         ops.decode_loss(ws.acts, P.W_dec_hk, P.b_dec_flat, ws.x, ws.x_mean, gs, ws.g_recon, ws.g_recon_t,
-                        ws.row_part_fused, ws.loss_colpart, ws.dec_ws, ws.n, ws.d, norm_fin=nf)
+                        ws.row_part_fused, ws.loss_colpart, ws.dec_ws, ws.n, ws.d, norm_fin=nf, pre=pre)
     ws.row_ncb = ws.fused_ncb
     ws.loss_col_rows = ops.col_part_rows(ws.B)
 
@@ -368,6 +379,7 @@ def loss_finalize(ws, l1l0_out=None, host=None, seq=0):
     decoder norms) one launch does both (cc_loss_tail); a re-formed loss (same activations) only the
     finaliser.  host (a _hip.MappedHostBuffer): the scalars also land there, then `seq` in word 8."""
     flush_norms(ws)  # (no-op after forward(), which ran the finaliser with or before G2)
+    ws.tail_deferred = None
     if ws.acts_pending:
         ops.loss_tail(ws.colsum_acts, ws.tn, ws.l1_part, _row_part(ws), ws.l0_part, ws.n_wave, ws.ev, ws.ev_a,
                       ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], l1l0_out=l1l0_out, host=host, seq=seq,
@@ -411,6 +423,16 @@ def loss_finalize_beside(ws, side_stream, on_losses=None, host=None, seq=0):
         return _hip.DeviceEvent().record(side_stream)
 
 
+def loss_finalize_with_g3(ws, side_stream, host=None, seq=0):
+    """The loss tail of loss_finalize(ws, host=host, seq=seq), carried by the backward's G3 launch where it serves the
+    shape (LOSS_TAIL_IN_G3, the transposed-operand step); otherwise loss_finalize_beside on `side_stream`.  Returns
+    None (G3 carries it; the host reads the scalars through `host`) or loss_finalize_beside's event."""
+    if LOSS_TAIL_IN_G3 and ws.tr and ws.acts_pending and host is not None:
+        ws.tail_deferred = (host, seq)
+        return None
+    return loss_finalize_beside(ws, side_stream, host=host, seq=seq)
+
+
 def row_chunks(B, n_chunks):
     """Batch slices [r0, r1) for the chunked (comm-overlapped) step: boundaries on 256-row GEMM
     tiles, so each slice's d_acts launch owns whole column-partial rows."""
@@ -424,11 +446,22 @@ def dacts_rows(ws, P, l1_coeff, r0, r1, l1_grad_weight=1.0):
     l1_scale = float(l1_coeff) * l1_grad_weight / ws.B
     c0, c1 = ops.col_part_rows(r0), ops.col_part_rows(r1)
     flush_norms(ws)
+    tail = None
+    if ws.tail_deferred is not None:
+        host, seq = ws.tail_deferred
+        ws.tail_deferred = None
+        if ws.tr and (r0, r1) == (0, ws.B):
+            tail = ops.loss_tail_job(ws.colsum_acts, ws.tn, ws.l1_part, _row_part(ws), ws.l0_part, ws.n_wave, ws.ev,
+                                     ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], host=host,
+                                     seq=seq, ncb=ws.row_ncb)
+            ws.acts_pending = False
+        else:
+            loss_finalize(ws, host=host, seq=seq)
     with _span("G3_dacts"):
         if ws.tr:
             ops.dacts_bwd_t(ws.g_recon[r0:r1], P.W_dec_hk, ws.acts[r0:r1], ws.tn, l1_scale, ws.g_pre_t[:, r0:r1],
                             colsum_part=ws.gpre_colpart[c0:c1], mask_bits=ops.mask_bits_rows(ws.mask_bits, ws.h, r0, r1),
-                            tile_ctr=_tile_ctr(ws, 1))
+                            tile_ctr=_tile_ctr(ws, 1), tail=tail)
         else:
             ops.dacts_bwd(ws.g_recon[r0:r1], P.W_dec_hk, ws.acts[r0:r1], ws.tn, l1_scale, ws.g_pre[r0:r1],
                           colsum_part=ws.gpre_colpart[c0:c1])

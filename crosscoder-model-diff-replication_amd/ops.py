@@ -155,18 +155,26 @@ def mask_bits_words(B, h):
     return int(lib().cc_mask_bits_words(B, h))
 
 
+def colsum_job(part, rows, cols, scale=1.0, out=None):
+    """A column reduction a GEMM launch carries in its prologue (cc_colsum_job: reduce_rows(part, rows, cols,
+    scale=scale, out_f32=out) with the same bits), passed by reference."""
+    return ctypes.byref(_lib.ColsumJob(part.data_ptr(), rows, cols, part.stride(0) if part.dim() == 2 else cols,
+                                       scale, out.data_ptr()))
+
+
 def encode_fwd_t(x, W_enc_hk, b_enc, acts, acts_t, apply_relu=True, tn=None, colsum_part=None, l1_part=None,
-                 l0_part=None, mask_bits=None, tile_ctr=None):
+                 l0_part=None, mask_bits=None, tile_ctr=None, pre=None):
     """encode_fwd that also stores acts_t [h][B] = acts^T (bf16, B % 8 == 0) and, optionally, the activation
     mask bits (int32 [mask_bits_words(B, h)]) that dacts_bwd_t reads instead of acts.  tile_ctr: int32
-    [TILE_CTR_WORDS] zeroed counters -> dynamic per-XCD tile order (same bits)."""
+    [TILE_CTR_WORDS] zeroed counters -> dynamic per-XCD tile order (same bits).  pre: a colsum_job the launch
+    runs first."""
     B, K = x.shape
     h = W_enc_hk.shape[0]
     if mask_bits is not None and mask_bits.numel() < mask_bits_words(B, h):
         raise ValueError("mask_bits too small")
     check(lib().cc_encode_fwd_t(_ptr(x), _ptr(W_enc_hk), _ptr(b_enc), _ptr(tn), _ptr(acts), _ptr(acts_t),
                                 int(apply_relu), _ptr(colsum_part), _ptr(l1_part), _ptr(l0_part), _ptr(mask_bits),
-                                _ctr(tile_ctr), B, K, h, dtype_code(x.dtype), _stream(x)))
+                                _ctr(tile_ctr), pre, B, K, h, dtype_code(x.dtype), _stream(x)))
     return acts
 
 
@@ -212,7 +220,7 @@ def decode_loss_t(acts, W_dec_t, b_dec, x, x_mean, grad_scale, g_recon, g_recon_
 
 
 def decode_loss(acts, W_dec_hk, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t, row_part, col_part, ws, n, d,
-                norm_fin=None):
+                norm_fin=None, pre=None):
     """decode_loss_t reading W_dec [h, K] itself (cc_decode_loss, transposed LDS reads of the B operand): the same
     bits without the W_dec^T copy.  g_recon_t may be None.  norm_fin = (part, norms, total, inv_norms): the decoder
     norms' finaliser (dec_norms_finalize) rides in the launch."""
@@ -220,8 +228,8 @@ def decode_loss(acts, W_dec_hk, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t
     part, norms, total, inv = norm_fin if norm_fin is not None else (None, None, None, None)
     check(lib().cc_decode_loss(_ptr(acts), _ptr(W_dec_hk), _ptr(b_dec), _ptr(x), _ptr(x_mean), grad_scale,
                                _ptr(g_recon), _ptr(g_recon_t), _ptr(row_part), _ptr(col_part), _ptr(ws),
-                               0 if ws is None else ws.numel(), _ptr(part), _ptr(norms), _ptr(total), _ptr(inv), B, h,
-                               n, d, dtype_code(acts.dtype), _stream(acts)))
+                               0 if ws is None else ws.numel(), _ptr(part), _ptr(norms), _ptr(total), _ptr(inv), pre, B,
+                               h, n, d, dtype_code(acts.dtype), _stream(acts)))
 
 
 def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_scale, B, n, d, row0=0, rows=None,
@@ -305,7 +313,18 @@ def dacts_bwd(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre, colsum_part=None):
                              _ptr(colsum_part), B, K, h, dtype_code(g_recon.dtype), _stream(g_recon)))
 
 
-def dacts_bwd_t(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre_t, colsum_part=None, mask_bits=None, tile_ctr=None):
+def loss_tail_job(colsum_acts, tn, l1_part, row_part, l0_part, n_l0, ev, ev_a, ev_b, scalars, B, n, d, counter,
+                  l1l0_out=None, host=None, seq=0, ncb=None):
+    """loss_tail's arguments as a cc_loss_tail_job a d_acts launch carries (dacts_bwd_t(tail=...)), by reference."""
+    p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    return ctypes.byref(_lib.LossTailJob(
+        p(colsum_acts), p(tn), colsum_acts.numel(), p(l1_part), p(row_part), loss_col_blocks(d) if ncb is None else ncb,
+        p(l0_part), n_l0, p(ev), p(ev_a), p(ev_b), p(scalars), p(l1l0_out),
+        host.device_ptr.value if host is not None else None, seq, B, n, p(counter)))
+
+
+def dacts_bwd_t(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre_t, colsum_part=None, mask_bits=None, tile_ctr=None,
+                tail=None):
     """dacts_bwd storing g_pre transposed only: g_pre_t [h][>= B] view (column slice allowed, row stride
     g_pre_t.stride(0)).  mask_bits: encode_fwd_t's bits of these rows (see mask_bits_rows)."""
     B, K = g_recon.shape
@@ -315,7 +334,7 @@ def dacts_bwd_t(g_recon, W_dec_hk, acts, tn, l1_scale, g_pre_t, colsum_part=None
     if mask_bits is not None and mask_bits.numel() < mask_bits_words(B, h):
         raise ValueError("mask_bits too small")
     check(lib().cc_dacts_bwd_t(_ptr(g_recon), _ptr(W_dec_hk), _ptr(acts), _ptr(tn), l1_scale, _ptr(mask_bits),
-                               _ptr(g_pre_t), g_pre_t.stride(0), _ptr(colsum_part), _ctr(tile_ctr), B, K, h,
+                               _ptr(g_pre_t), g_pre_t.stride(0), _ptr(colsum_part), _ctr(tile_ctr), tail, B, K, h,
                                dtype_code(g_recon.dtype), _stream(g_recon)))
 
 

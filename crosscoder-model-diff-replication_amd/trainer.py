@@ -122,8 +122,12 @@ class Trainer:
         side = self._side_stream()
         # prep, G1, G2 + the loss rows (one pass where decode_loss_t serves the shape)
         engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None, finalize=False)
-        # the loss scalars (+ their host copy) on the side stream, beside G3 (read by nothing on this stream)
-        done = engine.loss_finalize_beside(ws, side, on_losses, host=host, seq=seq)
+        # the loss scalars: into mapped host memory from the G3 launch (host given), or on the side stream beside
+        # G3 (read by nothing on this stream) with on_losses
+        if on_losses is None:
+            done = engine.loss_finalize_with_g3(ws, side, host=host, seq=seq)
+        else:
+            done = engine.loss_finalize_beside(ws, side, on_losses, host=host, seq=seq)
         l1c = self.get_l1_coeff()
         # clip_grad_norm_(max_norm=1.0), trainer.py:46
         engine.backward(ws, P, opt.grads, l1c, clip=1.0)

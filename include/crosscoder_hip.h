@@ -105,6 +105,15 @@ int cc_encode_fwd(const void* x, const void* W_enc, const void* b_enc, const flo
                   int apply_relu, float* colsum_part, float* l1_part, float* l0_part, int64_t B, int64_t K,
                   int64_t h, int dtype, void* stream);
 
+/* A column reduction a GEMM launch can carry before its tiles -- cc_reduce_rows(part, rows, cols, ld, scale,
+ * out_f32 = out) with the same bits -- so the step saves that launch: out[j] = scale * sum_{i<rows} part[i*ld + j]. */
+typedef struct cc_colsum_job {
+  const float* part;
+  int64_t rows, cols, ld;
+  float scale;
+  float* out;
+} cc_colsum_job;
+
 /* 1 when cc_encode_fwd_t / cc_dacts_bwd_t / cc_wgrad_both_t serve a step of this shape and dtype. */
 int cc_transposed_ok(int64_t B, int64_t K, int64_t h, int dtype);
 
@@ -116,11 +125,14 @@ int cc_transposed_ok(int64_t B, int64_t K, int64_t h, int dtype);
  * tile_ctr (optional): CC_TILE_CTR_WORDS u32, zero before the first launch that uses them and left zero by
  * every launch: the persistent launch then hands out its output tiles dynamically, per XCD, so workgroups
  * that start late (their CUs held by another stream's kernel) take fewer tiles; NULL: a static tile order.
- * The results are the same bits either way.  Launches sharing tile_ctr must be ordered (one stream). */
+ * The results are the same bits either way.  Launches sharing tile_ctr must be ordered (one stream).
+ * pre (optional): a column reduction the launch runs first (the step: x.mean(0) from cc_prep_input_t's
+ * column partials, crosscoder.py:112). */
 #define CC_TILE_CTR_WORDS 8
 int cc_encode_fwd_t(const void* x, const void* W_enc, const void* b_enc, const float* tn, void* acts, void* acts_t,
                     int apply_relu, float* colsum_part, float* l1_part, float* l0_part, uint32_t* mask_bits,
-                    uint32_t* tile_ctr, int64_t B, int64_t K, int64_t h, int dtype, void* stream);
+                    uint32_t* tile_ctr, const cc_colsum_job* pre, int64_t B, int64_t K, int64_t h, int dtype,
+                    void* stream);
 
 /* u32 words of cc_encode_fwd_t's mask_bits for a [B][h] activation (256 x 256 tiles x 512 threads x 4). */
 int64_t cc_mask_bits_words(int64_t B, int64_t h);
@@ -183,11 +195,13 @@ int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, c
  * norm_part (optional, with norms / tn / inv_norms as in cc_dec_norms_finalize): the decoder norms'
  * finaliser rides in the launch of the split-K leftover (or runs just before the GEMM where the shape has
  * none) -- the same bits as cc_dec_norms_finalize(norm_part, h, n, d, norms, tn, inv_norms), ordered before
- * whatever the stream runs next (crosscoder.py:123-125 for the backward and the loss tail). */
+ * whatever the stream runs next (crosscoder.py:123-125 for the backward and the loss tail).
+ * pre (optional): a column reduction the launch runs before its tiles (the step: sum_b acts from the
+ * encoder's column partials, which G4 and the l1 loss read, crosscoder.py:126). */
 int cc_decode_loss(const void* acts, const void* W_dec, const void* b_dec, const void* x, const float* x_mean,
                    float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
-                   int64_t ws_floats, const float* norm_part, float* norms, float* tn, float* inv_norms, int64_t B,
-                   int64_t h, int64_t n, int64_t d, int dtype, void* stream);
+                   int64_t ws_floats, const float* norm_part, float* norms, float* tn, float* inv_norms,
+                   const cc_colsum_job* pre, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream);
 
 /* Loss reduction (crosscoder.py:106-128, trainer.py:51-61): per-row explained variances
  * ev/ev_a/ev_b [B] (fp32) and scalars[0:8] = {l2, l1, l0, mean ev, mean ev_a, mean ev_b, 0, 0};
@@ -236,10 +250,32 @@ int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const
  * [r0, r1) passes g_pre_t + r0 and B = r1 - r0).  bf16 with B, K, h, ldt % 8 == 0.
  * mask_bits (optional): cc_encode_fwd_t's mask bits of these rows (a slice starting at row r0, r0 % 256 == 0,
  * passes mask_bits + (r0 / 256) * cc_mask_bits_words(256, h)); used instead of reading the acts tile when
- * the shape takes the whole-tile form (B, h % 256 == 0), same bits.  tile_ctr: as cc_encode_fwd_t. */
+ * the shape takes the whole-tile form (B, h % 256 == 0), same bits.  tile_ctr: as cc_encode_fwd_t.
+ * tail (optional): the forward's loss tail -- cc_loss_tail with these arguments, the same bits -- run by the
+ * launch's first workgroups before their tiles (the last of them to finish runs the loss-scalar finaliser;
+ * the tile counters then even out its late start). */
+typedef struct cc_loss_tail_job {
+  const float* colsum_acts;
+  const float* tn;
+  int64_t h;
+  float* l1_part;
+  const float* row_part;
+  int64_t ncb;
+  const float* l0_part;
+  int64_t n_l0;
+  float* ev;
+  float* ev_a;
+  float* ev_b;
+  float* scalars;
+  float* l1l0_out;
+  float* host_out;
+  uint32_t seq;
+  int64_t B, n;
+  uint32_t* counter;
+} cc_loss_tail_job;
 int cc_dacts_bwd_t(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,
                    const uint32_t* mask_bits, void* g_pre_t, int64_t ldt, float* colsum_part, uint32_t* tile_ctr,
-                   int64_t B, int64_t K, int64_t h, int dtype, void* stream);
+                   const cc_loss_tail_job* tail, int64_t B, int64_t K, int64_t h, int dtype, void* stream);
 
 /* W_dec.grad [h][K] = acts^T . g_recon + l1_scale * sum_b(acts[:,h]) * W_dec[h,m,:]/||W_dec[h,m,:]||
  * (norm backward is 0 where the norm is 0; inv_norms from cc_dec_norms).

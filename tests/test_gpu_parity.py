@@ -551,6 +551,30 @@ def test_delayed_side_stream_adam_still_orders_the_norm_readers(gpu, dbg_lib, mo
     assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
 
 
+@pytest.mark.parametrize("B,n,d,h", [(1024, 2, 256, 2048), (512, 4, 128, 1024)])
+def test_loss_tail_in_g3_matches_side_stream(gpu, B, n, d, h, monkeypatch):
+    """Trainer.step's loss tail carried by the backward's G3 launch (engine.LOSS_TAIL_IN_G3: its first workgroups
+    run it before their tiles, the last of them the finaliser, into mapped host memory) == the side-stream
+    launch forked before G3: the same loss dicts, params and moments, bit for bit; the arrival counters end at 0."""
+    from crosscoder_amd import engine
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+               num_tokens=B * 20, device=str(gpu))
+    outs = []
+    for in_g3 in (False, True):
+        monkeypatch.setattr(engine, "LOSS_TAIL_IN_G3", in_g3)
+        cc = ca.CrossCoder(cfg, n_models=n)
+        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 4, n_models=n, seed=7), crosscoder=cc)
+        dicts = [tr.step() for _ in range(4)]
+        tr.synchronize()
+        torch.cuda.synchronize()
+        ws = cc._workspace(B, step=True)
+        assert not bool(ws.tail_ctr.any()) and ws.tail_deferred is None
+        outs.append((dicts, cc.arena().data.clone(), tr.optimizer.exp_avg.data.clone()))
+    (d0, p0, m0), (d1, p1, m1) = outs
+    assert d0 == d1
+    assert torch.equal(p0, p1) and torch.equal(m0, m1)
+
+
 def test_dynamic_tile_order_is_bit_identical(gpu, dbg_lib, monkeypatch):
     """The persistent G1 / G3 / G4G5 launches hand out tiles from per-XCD counters (engine.DYNAMIC_TILES); which
     workgroup runs a tile must not change any bit.  Steps with the static order vs the dynamic order while 32
@@ -1336,6 +1360,9 @@ def test_fused_tails_match_separate_launches(gpu, enc_dtype, B, n, d, h):
     # loss side, separately
     colsum, l1p = f32(ws.colsum_acts), f32(ws.l1_part)
     ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=colsum, dot_w=ws.tn, dot_part=l1p)
+    # (x.mean(0) and sum_b acts: where the step carries them in the G1 / G2 prologues, reduce_rows' bits)
+    xm = f32(ws.x_mean)
+    ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], n * d, scale=1.0 / B, out_f32=xm)
     ev, ev_a, ev_b, sc = f32(ws.ev), f32(ws.ev_a), f32(ws.ev_b), f32(ws.scalars)
     rp = engine._row_part(ws)  # (the layout of the pass that wrote the row terms)
     ops.loss_finalize(rp, l1p, ws.n_l1, ws.l0_part, ws.n_wave, ev, ev_a, ev_b, sc, B, n, d, ncb=ws.row_ncb)
@@ -1360,7 +1387,8 @@ def test_fused_tails_match_separate_launches(gpu, enc_dtype, B, n, d, h):
     host.wait(8, 7)
     host2.wait(8, 9)
     assert not bool(ws.tail_ctr.any())
-    for x, y in ((colsum, ws.colsum_acts), (l1p, ws.l1_part), (ev, ws.ev), (ev_a, ws.ev_a), (ev_b, ws.ev_b),
+    for x, y in ((colsum, ws.colsum_acts), (xm, ws.x_mean), (l1p, ws.l1_part), (ev, ws.ev), (ev_a, ws.ev_a),
+                 (ev_b, ws.ev_b),
                  (sc[:6], ws.scalars[:6]), (sq, ws.sq), (gbe, G.b_enc), (gbd, G.b_dec_flat), (l1p2, l1p),
                  (sc3[:6], sc[:6])):
         assert torch.equal(x, y)
