@@ -69,12 +69,12 @@ def main():
             "G1_encode": lambda: L.cc_encode_fwd(P(x), P(W), P(b_enc), P(tn), P(acts), 1, P(parts), P(parts), P(parts),
                                                  B, K, h, 1, st),
             "G1_encode_T": lambda: L.cc_encode_fwd_t(P(x), P(W), P(b_enc), P(tn), P(acts), P(actsT2), 1, P(parts),
-                                                     P(parts), P(parts), P(mbits), B, K, h, 1, st),
+                                                     P(parts), P(parts), P(mbits), N0, N0, B, K, h, 1, st),
             "G2_decode": lambda: L.cc_decode_fwd(P(acts), P(W2), N0, P(recon), N0, B, h, K, 1, st),
             "G2_decode_ws": lambda: L.cc_decode_fwd_ws(P(acts), P(W2), P(recon), P(dws), nws, B, h, K, 1, st),
             "G2_decode_ws_T": lambda: L.cc_decode_fwd_ws_t(P(acts), P(W2T), P(recon), P(dws), nws, B, h, K, 1, st),
             "G3_dacts_T": lambda: L.cc_dacts_bwd_t(P(g_recon), P(W2), P(acts), P(tn), 1e-4, P(mbits), P(gpT2), B,
-                                                   P(parts), B, K, h, 1, st),
+                                                   P(parts), N0, N0, B, K, h, 1, st),
             "G3_dacts": lambda: L.cc_dacts_bwd(P(g_recon), P(W2), P(acts), P(tn), 1e-4, P(g_pre), P(parts), B, K, h, 1,
                                                st),
             "G4_wgrad_dec": lambda: L.cc_wgrad_dec(P(acts), P(g_recon), P(W2), P(norms), P(colsum), 1e-4, P(gW),
