@@ -1,0 +1,407 @@
+"""Benchmark: activations/sec of the full crosscoder training step (fwd + bwd + clip + Adam).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C] [--batch B] [--n-models n]
+                  [--d-model d] [--dict-size h] [--no-cpu-baseline]
+
+Workloads are BASELINE.json's configs (synthetic normalised activations, reference init seed 49, bf16):
+  config 2  CrossCoder 2x2304->16384, batch 4096          -- the default at N = 1 (the metric's config)
+  config 3  2x2304->131072 (2^17), batch 4096, latent-sharded over the N ranks -- the default at N > 1
+  config 4  2x3584->65536, batch 8192                       config 5  4x2304->32768, batch 4096
+(--batch / --n-models / --d-model / --dict-size override single fields).  N > 1 (torchrun, one rank per
+GPU): the FIXED dictionary of the config is split into N latent slices (strong scaling) with an RCCL
+all-reduce of the fp32 partial reconstructions; every rank processes the same batch.
+
+`value` is the activations (batch rows, each seen by all n models) the whole job trains per second -- the
+metric's own unit, on whatever workload runs.  At N = 1 that is config 2, the metric's config.  N > 1 runs
+config 3 (2^17 latents, as BASELINE.json's north_star asks), whose rows cost 8x a config-2 row, so its
+`value` is not comparable with the N = 1 line: the strong-scaling point of comparison is `n1_same_workload`
+(config 3 on one GPU, committed measurement), and `metric_equiv_acts_per_s` = value x n.d.h / (2.2304.16384)
+restates the throughput in config-2 rows of equal FLOP (10.n.d.h FLOP of step work per row).
+`latent_acts_per_s` = value x dict_size.
+
+The JSON line also carries `roofline` (dominant kernel's achieved TFLOP/s from HIP events around its
+launches inside the timed region, vs the bf16 dense MFMA peak), `hbm` (achieved GB/s of the
+streaming kernels: Adam halves, input prep -- and the loss kernel where G2 does not carry the loss in its
+epilogue -- from an untimed attribution pass) and `cpu_baseline` (the oracle CPU step timed on this host,
+rank 0, N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+# one HIP hardware queue per stream (HIP's default is 4 per process): the latent-sharded step uses the
+# compute stream, the side stream and RCCL's streams, and on a shared queue the side stream's decoder-half
+# Adam serialises behind the compute stream instead of running beside G1 (+0.2 ms per step, DESIGN.md
+# section 6; neutral for the single-GPU step).  Must be set before the process touches the GPU.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import crosscoder_amd as ca  # noqa: E402
+from crosscoder_amd import engine  # noqa: E402
+
+CONFIGS = {2: (4096, 2, 2304, 16384), 3: (4096, 2, 2304, 131072), 4: (8192, 2, 3584, 65536),
+           5: (4096, 4, 2304, 32768)}  # (batch, n_models, d_model, dict_size)
+PEAK_BF16_TFLOPS = 256 * 2.4e9 * 4096 / 1e12  # 256 CU x 2.4 GHz x 4096 bf16 FLOP/clk/CU (dense)
+PEAK_HBM_GBS = 8000.0  # HBM3E spec (MI355X_MICROARCH.md; ~6300 measured for a float4 copy)
+
+
+class EventTimer:
+    """HIP events on torch's current stream (the stream every launch uses) around named spans.
+
+    `only` restricts recording to one span name: inside the timed region only the roofline kernel
+    is bracketed (each timing event costs the stream a few microseconds); the per-kernel breakdown
+    comes from an attribution pass of its own."""
+
+    def __init__(self):
+        self.rec = {}
+        self.enabled = False
+        self.only = None
+
+    class _Span:
+        def __init__(self, t, name):
+            self.t, self.name = t, name
+            self.on = t.enabled and (t.only is None or t.only == name)
+
+        def __enter__(self):
+            if self.on:
+                self.s = torch.cuda.Event(enable_timing=True)
+                self.s.record()
+
+        def __exit__(self, *a):
+            if self.on:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record()
+                self.t.rec.setdefault(self.name, []).append((self.s, e))
+
+    def span(self, name):
+        return EventTimer._Span(self, name)
+
+    def averages_ms(self):
+        return {k: sum(s.elapsed_time(e) for s, e in v) / len(v) for k, v in self.rec.items()}
+
+
+SPAN_EVERY = 4  # timed steps per roofline-kernel sample (events around the launch)
+
+# span name -> kernel-name prefix in the rocprofv3 traces
+SPAN_KERNEL = {"G1_encode": "gemm_pp_kernel<true, true, 1", "G2_decode": "gemm_pp_main_splitk_kernel<true, false, 7",
+               "G3_dacts": "gemm_pp_kernel<true, true, 3", "G4G5_wgrad": "gemm_pp_dual_tail_kernel<true, true, 4, 5>",
+               "adam": "adam_bulk_kernel"}
+
+
+def pmc_traffic(span):
+    """HBM bytes per launch of the span's kernel from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate FETCH_SIZE /
+    WRITE_SIZE passes of this bench), or None."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files or span not in SPAN_KERNEL:
+        return None, None
+    with open(files[-1]) as f:
+        doc = json.load(f)
+    for name, v in doc["kernels"].items():
+        if name.startswith(SPAN_KERNEL[span]):
+            return v["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
+def rocprof_average(span):
+    """The dominant kernel's average duration in the newest committed rocprofv3 --stats summary of this bench
+    (profiles/*_step_kernel_stats.csv) -- the figure the live event samples are checked against -- or None."""
+    import csv
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_step_kernel_stats.csv")))
+    if not files or span not in SPAN_KERNEL:
+        return None
+    with open(files[-1]) as f:
+        for row in csv.DictReader(f):
+            name = row["Name"].replace("void ", "").replace("cc::", "")
+            if name.startswith(SPAN_KERNEL[span]):
+                return {"avg_ms": round(float(row["AverageNs"]) * 1e-6, 4), "calls": int(row["Calls"]),
+                        "min_ms": round(float(row["MinNs"]) * 1e-6, 4), "source": os.path.relpath(files[-1], ROOT)}
+    return None
+
+
+def n1_same_workload(B, n, d, h):
+    """The committed one-GPU bench line of the same workload (profiles/*_bench_configs.jsonl, measured by this
+    bench with --config on one MI355X), the 1-GPU point of an N > 1 strong-scaling curve -- or None."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_bench_configs.jsonl")))
+    if not files:
+        return None
+    for line in open(files[-1]):
+        line = line.strip()
+        if not line.startswith("{"):
+            continue
+        r = json.loads(line)
+        c = r.get("config", {})
+        if r.get("n_gpus") == 1 and (c.get("global_batch"), c.get("n_models"), c.get("d_model"),
+                                       c.get("dict_size")) == (B, n, d, h):
+            # (value = rows / s, from the line's own step time)
+            return {"value": round(B / (r["ms_per_step"] * 1e-3), 1), "ms_per_step": r["ms_per_step"],
+                    "source": os.path.relpath(files[-1], ROOT)}
+    return None
+
+
+def make_cfg(B, n, d, h):
+    return {
+        "seed": 49, "batch_size": B, "buffer_mult": 128, "lr": 5e-5, "num_tokens": 400_000_000, "l1_coeff": 2,
+        "beta1": 0.9, "beta2": 0.999, "dict_size": h, "seq_len": 1024, "enc_dtype": "bf16", "model_name": "synthetic",
+        "device": f"cuda:{torch.cuda.current_device()}", "model_batch_size": 4, "log_every": 100,
+        "save_every": 30000, "dec_init_norm": 0.08, "d_in": d, "n_models": n,
+    }
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(B, n, d, h):
+    """Oracle (the reference's PyTorch fp32 step restated, CPU) on a bounded sample of the same workload:
+    `rows` batch rows of normalised synthetic activations (Buffer.next scaling, buffer.py:115-125) for the
+    config's crosscoder, median of 5 steps after 1 warm-up; the per-step cost is linear in the rows."""
+    from oracle import cpu_reference as O
+
+    # this process's CPU share: OMP_NUM_THREADS (16 per GPU on the box), else the affinity mask
+    cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    # ~3 s per oracle step on the box's 16 threads at config 2 (4096 rows): keep every config near that
+    rows = max(256, min(B, int(B * (2 * 2304 * 16384) / (n * d * h)) // 256 * 256))
+    cfg = {"seed": 49, "dict_size": h, "d_in": d, "enc_dtype": "fp32", "dec_init_norm": 0.08,
+           "batch_size": rows, "num_tokens": 400_000_000, "lr": 5e-5, "beta1": 0.9, "beta2": 0.999, "l1_coeff": 2}
+    P = O.init_params(cfg, n_models=n)
+    tr = O.OracleTrainer(cfg, P, n_models=n)
+    g = torch.Generator().manual_seed(0)
+    scales = torch.tensor([(1 / 0.2759, 1 / 0.2442, 1 / 0.31, 1 / 0.27)[i % 4] for i in range(n)])
+    buf = (torch.randn(rows, n, d, generator=g) * scales[None, :, None]).to(torch.bfloat16)
+    factor = torch.tensor([(d ** 0.5) / buf[:, i].float().norm(dim=-1).mean().item() for i in range(n)]).to(
+        torch.bfloat16)
+    x = O.buffer_next(buf, factor)  # normalised: ||x_n|| ~ sqrt(d)
+    tr.step(x)  # warm-up
+    times = []
+    t_start = time.perf_counter()
+    while len(times) < 5 and (time.perf_counter() - t_start) < 25.0:
+        t0 = time.perf_counter()
+        tr.step(x)
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    med = times[len(times) // 2]
+    return {"value": round(rows / med, 1), "unit": "activations/s", "cores": cores, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"oracle fp32 Trainer.step on {rows} normalised rows of the {n}x{d}->{h} crosscoder "
+                      f"(bench batch {B}; cost is linear in rows), median of {len(times)} steps after 1 "
+                      f"warm-up, {med:.2f} s/step"}
+
+
+def hbm_rows(kern, B, n, d, h_local, es=2):
+    """Achieved HBM rate of the streaming kernels from the attribution pass (algorithmic bytes: every
+    operand read once, every output written once)."""
+    K = n * d
+    enc = h_local * K + h_local  # encoder half of the arena (W_enc + b_enc)
+    dec = h_local * K + K
+    per = 7 * es  # Adam: p, g, m, v read + p, m, v written
+    # the decoder half: W_dec's first hs rows on the side stream beside G1, the rest + b_dec after G1
+    hs = min(h_local, int(h_local * engine.DEC_SIDE_ROWS) // 8 * 8)
+    byts = {"adam": enc * per, "adam_dec": hs * K * per, "adam_dec_rest": (dec - hs * K) * per,
+            "prep": B * K * es + 2 * B * K * es,            # raw batch in; x and x^T out
+            "loss": B * K * 4 + B * K * es + 2 * B * K * es,  # recon fp32 + x in; g_recon and g_recon^T out
+            "dec_norms_T": 2 * h_local * K * es}             # W_dec in, W_dec^T out (+ norms)
+    out = {}
+    for k, b in byts.items():
+        if k in kern and kern[k] > 0:
+            gbs = b / (kern[k] * 1e-3) / 1e9
+            out[k] = {"ms": round(kern[k], 4), "bytes": b, "GB_s": round(gbs, 1),
+                      "frac": round(gbs / PEAK_HBM_GBS, 3)}
+    if "adam_dec" in out:
+        out["adam_dec"]["note"] = ("W_dec's first rows, side stream, concurrent with the next step's prep / G1; "
+                                   "also writes the decoder norms' per-block partials of the updated W_dec")
+    if "adam_dec_rest" in out:
+        out["adam_dec_rest"]["note"] = "the decoder half's remaining rows + b_dec, main stream after G1"
+    if "dec_norms_T" in out:
+        out["dec_norms_T"]["note"] = "side stream, concurrent with G1"
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, choices=sorted(CONFIGS), default=None,
+                    help="BASELINE.json config (default: 2 on one GPU, 3 when sharded over N > 1)")
+    ap.add_argument("--batch", type=int)
+    ap.add_argument("--n-models", type=int)
+    ap.add_argument("--d-model", type=int)
+    ap.add_argument("--dict-size", type=int, help="the WHOLE dictionary (split over the ranks when N > 1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--comm", choices=("all_reduce", "reduce_scatter"), default="all_reduce",
+                    help="latent-sharded step: the partial-reconstruction exchange")
+    ap.add_argument("--recon-chunks", type=int, default=None,
+                    help="latent-sharded step: batch slices the exchange is overlapped by (default 2)")
+    ap.add_argument("--force-sharded", action="store_true",
+                    help="diagnostic: run the latent-sharded step even on one rank (1-rank RCCL group)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 flow on a one-GPU box (never a measurement): every rank on cuda:0, gloo
+    # collectives (RCCL refuses two ranks on one device)
+    one_device = os.environ.get("CC_BENCH_ONE_DEVICE") == "1"
+    if one_device:
+        local = 0
+    torch.cuda.set_device(local)
+    sharded_path = world > 1 or args.force_sharded
+    if sharded_path:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        if one_device:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), rank=rank, world_size=world)
+    config = args.config if args.config is not None else (2 if world == 1 else 3)
+    B, n, d, h_total = CONFIGS[config]
+    B = args.batch or B
+    n = args.n_models or n
+    d = args.d_model or d
+    h_total = args.dict_size or h_total
+    custom = (B, n, d, h_total) != CONFIGS[config]
+    h_local = h_total // world
+    K = n * d
+    cfg = make_cfg(B, n, d, h_total)
+
+    if not sharded_path:
+        cc = ca.CrossCoder(cfg)
+        buf = ca.SyntheticBuffer(cfg, rows=B * 8, n_models=n, seed=0)
+        tr = ca.Trainer(cfg, buffer=buf, crosscoder=cc)
+    else:
+        from crosscoder_amd import sharded
+
+        buf = ca.SyntheticBuffer(cfg, rows=B * 8, n_models=n, seed=0)  # same seed on every rank: replicated batch
+        tr = sharded.ShardedTrainer(cfg, buffer=buf, comm=args.comm, recon_chunks=args.recon_chunks)
+
+    timer = EventTimer()
+    engine.TIMER = timer
+    for _ in range(args.warmup):
+        tr.step()
+    # attribution pass (not timed): every kernel bracketed by events
+    attrib = EventTimer()
+    engine.TIMER = attrib
+    attrib.enabled = True
+    for _ in range(max(3, min(args.steps, 10))):
+        tr.step()
+    torch.cuda.synchronize()
+    kern = attrib.averages_ms()
+    gemms = {k: v for k, v in kern.items() if k.startswith("G")}
+    dom = max(gemms, key=gemms.get)
+    engine.TIMER = timer
+    timer.only = dom  # the roofline kernel, measured live inside the timed region
+    if sharded_path:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        # the roofline launch is bracketed on every SPAN_EVERY-th timed step (each event record
+        # idles the stream ~6 us, tools/event_cost.py: sampling keeps that out of most steps)
+        timer.enabled = i % SPAN_EVERY == 0
+        last = tr.step()
+    torch.cuda.synchronize()
+    if sharded_path:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    timer.enabled = False
+    if sharded_path:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    step_s = elapsed / args.steps
+    ms = step_s * 1e3
+    rows_per_s = B / step_s  # activations (batch rows) trained per second by the whole job: `value`
+    # config-2 rows of equal step work (10.n.d.h FLOP per row): config 2 counts 1, config 3 (2^17 latents) 8
+    per_row = (n * d * h_total) / (2 * 2304 * 16384)
+    dom_ms = timer.averages_ms()[dom]
+    samples = sorted(s_.elapsed_time(e_) for s_, e_ in timer.rec.get(dom, []))
+    gemm_flop = 2.0 * B * K * h_local  # per GEMM (per rank)
+    # G4G5_wgrad is one launch computing both weight gradients (cc_wgrad_both)
+    dom_flop = gemm_flop * (2 if dom == "G4G5_wgrad" else 1)
+    achieved = dom_flop / (dom_ms * 1e-3) / 1e12
+    step_flop = 5 * 2.0 * B * K * h_total  # whole job
+    if not engine.transposed_wgrad(B, K, h_local, torch.bfloat16):  # batch-major MN/MN form (cc_wgrad_both)
+        SPAN_KERNEL["G4G5_wgrad"] = "gemm_pp_dual_kernel<false, false, 4, 5>"
+    traffic, traffic_src = pmc_traffic(dom) if (config, world, custom) == (2, 1, False) else (None, None)
+    # algorithmic operand/output bytes of the dominant launch (each input read once, output written once)
+    es = 2  # bf16
+    alg = {"G1_encode": (B * K + h_local * K + 2 * B * h_local) * es,
+           "G2_decode": (B * h_local + h_local * K + 3 * B * K) * es,  # + x in, g_recon / g_recon^T out (fused loss)
+           "G3_dacts": (B * K + h_local * K + B * h_local) * es + B * h_local // 8,  # (+ G1's mask bits, g_pre^T out)
+           "G4G5_wgrad": (2 * B * h_local + 2 * B * K + 3 * h_local * K) * es}
+    dom_alg_bytes = alg.get(dom)
+    name = f"{n}x{d}->{h_total}"
+    result = {
+        "metric": "activations/sec per train step (fwd+bwd+Adam), 2x2304->16384; % bf16 MFMA peak",
+        "value": round(rows_per_s, 1),
+        "unit": "activations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (seeded N(0,1) activations scaled per model, normalised as Buffer.next; reference "
+                "init seed 49)",
+        "config": {"workload": f"crosscoder train step {name}, batch {B}"
+                               + (f", latent-sharded over {world} GPUs ({h_local} latents per GPU)" if world > 1
+                                  else ""),
+                   "baseline_config": None if custom else config,
+                   "global_batch": B, "n_models": n, "d_model": d, "dict_size": h_total,
+                   "parallelism": f"latent{world}"},
+        "metric_equiv_acts_per_s": round(rows_per_s * per_row, 1),
+        "metric_equiv_per_row": per_row,
+        "latent_acts_per_s": round(rows_per_s * h_total, 1),
+        # N > 1: the same workload on one GPU (committed measurement), so the strong-scaling curve has its
+        # own 1-GPU point (the driver's N = 1 run is the metric's config 2, a different dictionary)
+        "n1_same_workload": n1_same_workload(B, n, d, h_total) if world > 1 else None,
+        "step_mfma_frac": round(step_flop / step_s / 1e12 / (PEAK_BF16_TFLOPS * world), 4),
+        "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items())},
+        "roofline": {"bound": "mfma", "kernel": dom, "kernel_name": SPAN_KERNEL.get(dom), "kernel_ms": round(dom_ms, 4),
+                     "kernel_samples": len(samples),
+                     "kernel_ms_min_med_max": [round(samples[0], 4), round(samples[len(samples) // 2], 4),
+                                               round(samples[-1], 4)] if samples else None,
+                     "rocprof": rocprof_average(dom) if (config, world, custom) == (2, 1, False) else None,
+                     "achieved": round(achieved, 1),
+                     "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                     "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
+                     "algorithmic_bytes": dom_alg_bytes},
+        "hbm": hbm_rows(kern, B, n, d, h_local),
+        "last_loss": {k: round(v, 6) for k, v in last.items()},
+    }
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(B, n, d, h_total)
+        print(json.dumps(result), flush=True)
+    if sharded_path:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

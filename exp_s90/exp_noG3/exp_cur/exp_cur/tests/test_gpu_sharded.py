@@ -1,0 +1,97 @@
+"""Latent-sharded training step (sharded.py) with the HIP backend at world size 2: two processes on
+ONE GPU over gloo (RCCL refuses two ranks on one device), against the single-GPU Trainer on the full
+dictionary.  Every rank starts from its slice of the reference init of the whole dictionary, so the
+two runs train the same crosscoder: loss dicts and the gathered parameters must agree to bf16
+rounding (the partial reconstructions and the clip sums are combined in a different order)."""
+import math
+import os
+import random
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+B, N, D, H, STEPS = 1024, 2, 256, 2048, 3
+
+
+def _cfg(device):
+    return {"seed": 49, "batch_size": B, "buffer_mult": 128, "lr": 5e-5, "num_tokens": B * 20, "l1_coeff": 2,
+            "beta1": 0.9, "beta2": 0.999, "dict_size": H, "seq_len": 1024, "enc_dtype": "bf16", "device": device,
+            "dec_init_norm": 0.08, "d_in": D, "log_every": 100, "save_every": 30000}
+
+
+def _rank(rank, world, port, q, comm, tmpdir, received):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import crosscoder_amd as ca
+        from crosscoder_amd import crosscoder as ccmod, sharded
+
+        cfg = _cfg("cuda:0")
+        buf = ca.SyntheticBuffer(cfg, rows=B * 3, seed=1)
+        tr = sharded.ShardedTrainer(cfg, buffer=buf, recon_chunks=2, comm=comm)
+        dicts = [tr.step() for _ in range(STEPS)]
+        sd = {k: v.detach().cpu() for k, v in tr.gather_state_dict().items()}
+        ccmod.SAVE_DIR = __import__("pathlib").Path(tmpdir) / "checkpoints"
+        tr.save()
+        q.put((rank, dicts, sd if rank == 0 else None))
+        # CPU tensors travel as shared-memory fds this process serves: stay alive until the
+        # parent has unpickled them
+        received.wait(240)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("comm", ["all_reduce", "reduce_scatter"])
+def test_sharded_world2_on_one_gpu_matches_trainer(gpu, comm, tmp_path):
+    import torch.multiprocessing as mp
+
+    import crosscoder_amd as ca
+
+    world = 2
+    port = 29000 + random.randint(0, 900)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    received = ctx.Event()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q, comm, str(tmp_path), received))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, dicts, sd = q.get(timeout=240)
+        res[r] = (dicts, sd)
+    received.set()
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # the single-GPU Trainer on the whole dictionary, same batches
+    cfg = _cfg(str(gpu))
+    tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=1), crosscoder=ca.CrossCoder(cfg))
+    ref = [tr.step() for _ in range(STEPS)]
+    ref_sd = {k: v.detach().cpu() for k, v in tr.crosscoder.state_dict().items()}
+    for r in range(world):
+        for a, b in zip(res[r][0], ref):
+            assert list(a) == list(b)
+            for k in ("loss", "l2_loss", "l1_loss", "l0_loss", "explained_variance"):
+                assert math.isclose(a[k], b[k], rel_tol=2e-3, abs_tol=2e-3), (r, k, a[k], b[k])
+            assert a["lr"] == b["lr"] and a["l1_coeff"] == b["l1_coeff"]
+    sd = res[0][1]
+    assert list(sd) == list(ref_sd)
+    for k, v in ref_sd.items():
+        assert sd[k].shape == v.shape and sd[k].stride() == v.stride(), k
+        d = (sd[k].float() - v.float()).abs()
+        # Adam moves each element by ~lr per step; combine-order differences may flip a bf16 rounding
+        assert d.max().item() <= 4 * cfg["lr"] + 2 ** -7 * v.float().abs().max().item(), (k, d.max().item())
+        assert (d == 0).float().mean().item() > 0.9, k
+    # rank 0 wrote one reference-format checkpoint of the whole dictionary
+    ck = tmp_path / "checkpoints" / "version_0"
+    assert sorted(os.listdir(ck)) == ["0.pt", "0_cfg.json"]
+    saved = torch.load(ck / "0.pt", weights_only=True)
+    for k in ref_sd:
+        assert torch.equal(saved[k], sd[k])

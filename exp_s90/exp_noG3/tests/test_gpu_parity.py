@@ -1,0 +1,1577 @@
+"""GPU parity: the HIP path (through the C-ABI library) against the oracle and the
+reference's golden fixtures.
+
+Tolerance contract (BASELINE.json north_star):
+  * fp32 mode: relative Frobenius error <= 2e-5 vs an fp64 evaluation of the same inputs;
+    the active set (acts > 0) and, on the dyadic known-answer test, pre/acts/recon/l0 are
+    bit-exact.
+  * bf16 mode: every tensor's error vs fp64 is at most 2x the reference's own bf16 error
+    (computed here from the fixture) plus a floor of 2e-3; active-set flips <= 0.2 %.
+"""
+import math
+
+import pytest
+import torch
+
+import crosscoder_amd as ca
+from crosscoder_amd import engine, ops
+from oracle import cpu_reference as O
+from tests._golden import load, step_fixtures
+
+pytestmark = pytest.mark.gpu
+
+STEP_FIXTURES = step_fixtures()
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return (a - b).norm().item() / max(b.norm().item(), 1e-30)
+
+
+def truth_fp64(x, P, l1c):
+    """fp64 evaluation (oracle math) on the exact same (dtype-rounded) inputs."""
+    dt = P["W_dec"].dtype
+    P64 = {k: v.detach().to(torch.float64).clone().requires_grad_(True) for k, v in P.items()}
+    x64 = x.to(dt).to(torch.float64)
+    lo = O.get_losses(x64, P64, torch.float64)
+    (lo["l2_loss"] + l1c * lo["l1_loss"]).backward()
+    with torch.no_grad():
+        pre = O.encode(x64, P64, apply_relu=False)
+    return lo, {k: P64[k].grad for k in O.PARAM_ORDER}, pre
+
+
+def envelope_ok(ours, ref, truth, floor=2e-3):
+    e_ours, e_ref = rel(ours, truth), rel(ref, truth)
+    return e_ours <= 2 * e_ref + floor, (e_ours, e_ref)
+
+
+def assert_fused_loss_path(cc, cfg):
+    """bf16 fixtures with d % 64 == 0 must reach the shipped fused G2 + loss kernel (cc_decode_loss_t)."""
+    if cfg["enc_dtype"] == "bf16" and cfg["d_in"] % 64 == 0:
+        ws = cc._ws
+        assert ws is not None and ws.fused_ncb == cfg["d_in"] // 64 and ws.row_ncb == ws.fused_ncb
+
+
+def make_cc(cfg, P, device, n_models):
+    cfg = dict(cfg, device=str(device))
+    cc = ca.CrossCoder(cfg, n_models=n_models)
+    cc.load_state_dict({k: v for k, v in P.items()})
+    return cc
+
+
+# ----------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(256, 256, 64), (296, 520, 72), (96, 200, 80), (512, 768, 1000)])
+@pytest.mark.parametrize("layouts", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_layouts(gpu, dtype, shape, layouts):
+    M, N, K = shape
+    al, bl = layouts
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, generator=g).to(dtype)  # logical A[m][k]
+    Bm = torch.randn(K, N, generator=g).to(dtype)  # logical B[k][n]
+    A_st = A.contiguous() if al == 0 else A.t().contiguous()
+    B_st = Bm.t().contiguous() if bl == 0 else Bm.contiguous()
+    C = ops.gemm_f32out(A_st.to(gpu), al, B_st.to(gpu), bl, M, N, K)
+    torch.cuda.synchronize()
+    ref = A.double() @ Bm.double()
+    assert rel(C, ref) < 1e-5
+
+
+@pytest.fixture
+def dbg_lib():
+    """ops.* routed through the test-only debug build (launch-form setters); product defaults afterwards."""
+    from crosscoder_amd import _lib
+    with _lib.debug_library() as lib:
+        yield lib
+
+
+@pytest.fixture
+def pp_mask(dbg_lib):
+    """Selects which layouts run the ping-pong main loop (debug build); restored afterwards."""
+    yield dbg_lib.cc_debug_set_pp_mask
+
+
+@pytest.mark.parametrize("shape", [(256, 256, 64), (296, 520, 72), (96, 200, 80), (512, 768, 1000),
+                                   (1024, 4608, 4096), (4096, 2304, 640)])
+@pytest.mark.parametrize("layouts", [(0, 0), (0, 1), (1, 1)])
+def test_gemm_pingpong_matches_two_stage(gpu, pp_mask, shape, layouts):
+    """Both bf16 main loops accumulate each output in the same k order, so they agree bitwise;
+    and both match fp64 (ragged M/N/K tails included)."""
+    M, N, K = shape
+    al, bl = layouts
+    g = torch.Generator().manual_seed(M + 3 * N + 7 * K)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    Bm = torch.randn(K, N, generator=g).to(torch.bfloat16)
+    A_st = (A.contiguous() if al == 0 else A.t().contiguous()).to(gpu)
+    B_st = (Bm.t().contiguous() if bl == 0 else Bm.contiguous()).to(gpu)
+    outs = []
+    for mask in (0, 7):
+        pp_mask(mask)
+        outs.append(ops.gemm_f32out(A_st, al, B_st, bl, M, N, K))
+    torch.cuda.synchronize()
+    ref = A.double() @ Bm.double()
+    assert rel(outs[1], ref) < 1e-5
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("shape", [(512, 768, 2, 200), (1024, 1000, 2, 96)])
+def test_wgrad_both_matches_separate(gpu, shape):
+    """The single-launch dW_dec + dW_enc (cc_wgrad_both) equals the two separate launches bitwise."""
+    B, h, n, d = shape
+    K = n * d
+    g = torch.Generator().manual_seed(B + h)
+    bf = torch.bfloat16
+    mk = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).to(bf).to(gpu)  # noqa: E731
+    acts = torch.relu(mk(B, h)).contiguous()
+    g_recon, g_pre, x = mk(B, K, sc=1e-2), mk(B, h, sc=1e-2), mk(B, K)
+    W = mk(h, K, sc=0.05)
+    inv = torch.rand(h, n, generator=g).to(gpu) + 0.5
+    colsum = acts.float().sum(0)
+    parts = ops.wgrad_parts(h, K, bf)
+    outs = []
+    for both in (False, True, "T"):
+        gd, ge = torch.empty(h, K, dtype=bf, device=gpu), torch.empty(h, K, dtype=bf, device=gpu)
+        sd, se = torch.zeros(parts, device=gpu), torch.zeros(parts, device=gpu)
+        if both == "T":  # transposed (KC/KC) operands: same k order per output element -> same bits
+            T = lambda t: t.t().contiguous()  # noqa: E731
+            ops.wgrad_both_t(T(acts), T(g_recon), W, inv, colsum, 3e-4, gd, sd, T(g_pre), T(x), ge, se, n, d)
+        elif both:
+            ops.wgrad_both(acts, g_recon, W, inv, colsum, 3e-4, gd, sd, g_pre, x, ge, se, n, d)
+        else:
+            ops.wgrad_dec(acts, g_recon, W, inv, colsum, 3e-4, gd, sd, n, d)
+            ops.wgrad_enc(g_pre, x, ge, se)
+        outs.append((gd, ge, sd, se))
+    torch.cuda.synchronize()
+    for a, b, c in zip(*outs):
+        assert torch.equal(a, b)
+        assert torch.equal(a, c)
+    ref = (acts.double().t() @ g_recon.double())
+    assert rel(outs[1][0].double() - 3e-4 * colsum.double()[:, None] * (W.double().view(h, n, d) *
+               inv.double()[:, :, None]).view(h, K), ref) < 1e-2
+
+
+@pytest.mark.parametrize("mask", [0, 7])
+def test_step_gemm_paths(gpu, pp_mask, mask):
+    """One fused fwd+bwd at a mid size through each main loop vs the fp32 oracle."""
+    pp_mask(mask)
+    n, d, h, B = 2, 576, 2048, 1024
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16", seed=11,
+               device=str(gpu))
+    cc = ca.CrossCoder(cfg, n_models=n)
+    g = torch.Generator().manual_seed(5)
+    buf = torch.randn(B, n, d, generator=g) * 3
+    factor = torch.tensor([0.7, 1.3]).to(torch.bfloat16)
+    ws = cc._workspace(B)
+    a = cc.arena()
+    G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+    engine.forward(ws, a, buf.to(gpu), factor.to(gpu))
+    engine.backward(ws, a, G, l1_coeff=2.0)
+    torch.cuda.synchronize()
+    P32 = {k: v.detach().float().cpu().clone().requires_grad_(True) for k, v in cc.state_dict().items()}
+    x32 = ws.x.cpu().float().view(B, n, d)
+    lo = O.get_losses(x32, P32, torch.float32)
+    (lo["l2_loss"] + 2.0 * lo["l1_loss"]).backward()
+    s = ws.scalars[:6].cpu()
+    assert math.isclose(s[0].item(), lo["l2_loss"].item(), rel_tol=1e-2)
+    Gv = G.views()
+    bounds = {"W_enc": 1e-1, "W_dec": 1e-2, "b_enc": 1e-2, "b_dec": 1e-2}
+    for k in O.PARAM_ORDER:
+        e = rel(Gv[k].cpu(), P32[k].grad)
+        assert e <= bounds[k], (k, e)
+
+
+# ----------------------------------------------------------------------------- forward
+@pytest.mark.parametrize("name", STEP_FIXTURES)
+def test_forward_parity(gpu, name):
+    r = load(name)
+    cfg, P, x = r["cfg"], r["init"], r["x"][0]
+    n = r["n_models"]
+    dt = O.DTYPES[cfg["enc_dtype"]]
+    cc = make_cc(cfg, P, gpu, n)
+    xg = x.to(gpu)
+    with torch.no_grad():
+        acts = cc.encode(xg.to(dt)).cpu()
+        pre = cc.encode(xg.to(dt), apply_relu=False).cpu()
+        recon = cc.decode(acts.to(gpu)).cpu()
+        lo = cc.get_losses(xg)
+    torch.cuda.synchronize()
+    assert_fused_loss_path(cc, cfg)
+    tlo, _, tpre = truth_fp64(x, P, 0.0)
+    fw = r["fwd"]
+    if dt == torch.float32:
+        assert rel(pre, tpre) < 2e-5
+        assert rel(recon, fw["recon"]) < 2e-5
+        # active set bit-exact outside a 1e-5 guard band around 0 (fp32 rounding of the sum)
+        band = tpre.abs() > 1e-5 * tpre.abs().max()
+        assert torch.equal((acts > 0)[band], (fw["acts"] > 0)[band])
+        assert band.float().mean().item() > (0.99 if "dyadic" in name else 0.999)
+        for k in ("l2_loss", "l1_loss", "l0_loss", "explained_variance"):
+            assert rel(getattr(lo, k), tlo[k]) < 2e-5, k
+    else:
+        ok, e = envelope_ok(pre, fw["pre"], tpre)
+        assert ok, ("pre", e)
+        flips = ((acts > 0) != (tpre > 0)).float().mean().item()
+        assert flips <= 2e-3
+        for k in ("l2_loss", "l1_loss", "explained_variance", "explained_variance_A", "explained_variance_B"):
+            ok, e = envelope_ok(getattr(lo, k).float(), fw[k].float(), tlo[k])
+            assert ok, (k, e)
+        assert abs(lo.l0_loss.item() - fw["l0_loss"].item()) <= 2e-3 * cfg["dict_size"] + 1
+    for k in ("l2_loss", "l1_loss", "l0_loss", "explained_variance", "explained_variance_A", "explained_variance_B"):
+        assert getattr(lo, k).dtype == fw[k].dtype, k
+        assert getattr(lo, k).shape == fw[k].shape, k
+
+
+def test_dyadic_known_answer_bit_exact(gpu):
+    """Dyadic data: every fp32 sum is exact, so the GPU must match the reference bit for bit."""
+    r = load("dyadic_b64_n2_d32_h128_fp32")
+    cc = make_cc(r["cfg"], r["init"], gpu, 2)
+    xg = r["x"][0].to(gpu)
+    with torch.no_grad():
+        pre = cc.encode(xg, apply_relu=False).cpu()
+        acts = cc.encode(xg).cpu()
+        recon = cc.decode(acts.to(gpu)).cpu()
+        lo = cc.get_losses(xg)
+    fw = r["fwd"]
+    assert torch.equal(pre, fw["pre"])
+    assert torch.equal(acts, fw["acts"])
+    assert torch.equal(recon, fw["recon"])
+    assert torch.equal(lo.l0_loss.cpu(), fw["l0_loss"])
+    assert torch.equal(lo.l2_loss.cpu(), fw["l2_loss"])
+
+
+# ----------------------------------------------------------------------------- backward
+@pytest.mark.parametrize("name", STEP_FIXTURES)
+def test_backward_parity(gpu, name):
+    r = load(name)
+    cfg, P, x = r["cfg"], r["init"], r["x"][0]
+    dt = O.DTYPES[cfg["enc_dtype"]]
+    cc = make_cc(cfg, P, gpu, r["n_models"])
+    lo = cc.get_losses(x.to(gpu))
+    assert_fused_loss_path(cc, cfg)
+    (lo.l2_loss + 2.0 * lo.l1_loss).backward()
+    torch.cuda.synchronize()
+    _, tg, _ = truth_fp64(x, P, 2.0)
+    for k in O.PARAM_ORDER:
+        g = getattr(cc, k).grad
+        ref = r["grads_l1c2"][k]
+        assert g.shape == ref.shape and g.dtype == ref.dtype and g.stride() == ref.stride(), k
+        if dt == torch.float32:
+            assert rel(g, tg[k]) < 2e-5, (k, rel(g, tg[k]))
+        else:
+            ok, e = envelope_ok(g, ref, tg[k], floor=5e-3)
+            assert ok, (k, e)
+
+
+# ----------------------------------------------------------------------------- trainer
+class _Replay:
+    normalize = True
+
+    def __init__(self, bufs, factors, device):
+        self.bufs = [b.to(device) for b in bufs]
+        self.factors = [f.to(device) for f in factors]
+        self.i = 0
+
+    def next_raw(self):
+        b, f = self.bufs[self.i], self.factors[self.i]
+        self.i += 1
+        return b, f
+
+
+def _bf16_ulp(t):
+    t = t.float().abs()
+    return torch.where(t > 0, 2.0 ** (torch.floor(torch.log2(t.clamp_min(1e-38))) - 7), torch.zeros_like(t))
+
+
+@pytest.mark.parametrize("name", [f for f in STEP_FIXTURES if f.startswith("step_")])
+def test_trainer_steps(gpu, name):
+    """Trainer.step over the reference's stored trajectories (tools/gen_golden.py: 2 or 10 reference
+    Trainer.step calls, warm-up and decay branches included; n_models 2 and 4): all 9 loss-dict keys
+    every step, and params, exp_avg and exp_avg_sq after every stored step.  Bounds (measured by
+    tools/trainer_parity_stats.py; a Trainer whose Adam never runs fails every one of them):
+      fp32  params within 0.01 lr elementwise (measured <= 0.001 lr); moments rel <= 1e-5 (~3e-7);
+            l2 / loss / l1 rel 1e-6, EVs 1e-6 abs, l0 exact
+      bf16  W_enc / W_dec bit-identical on >= 94 % of elements (measured >= 96.4 %; without Adam 27-31 %)
+            and within 2 bf16 ulps + 3 lr everywhere (measured <= 2.44 lr); biases bit-identical on >= 50 % (>= 58 %; without Adam
+            0 %) and within 0.25 lr; moments rel <= 0.05 (<= 0.023); l2 rel 1e-4, l1 one bf16 ulp,
+            l0 within 1e-3 h + 1/B, EV 2e-3, EV_A / EV_B 4e-3 abs, loss to the sum of those."""
+    r = load(name)
+    cfg = dict(r["cfg"], device=str(gpu))
+    dt = O.DTYPES[cfg["enc_dtype"]]
+    n = r["n_models"]
+    cc = make_cc(cfg, r["init"], gpu, n)
+    tr = ca.Trainer(cfg, buffer=_Replay(r["buf"], r["factor"], gpu), crosscoder=cc)
+    steps = len(r["x"])
+    lr = cfg["lr"]
+    B, h = cfg["batch_size"], cfg["dict_size"]
+    fp32 = dt == torch.float32
+    for s in range(steps):
+        d = tr.step()
+        assert_fused_loss_path(cc, cfg)
+        ref = r["steps"]["loss_dicts"][s]
+        assert list(d) == list(ref)
+        assert d["l1_coeff"] == ref["l1_coeff"] and d["lr"] == ref["lr"]
+        l1_tol = 1e-6 * abs(ref["l1_loss"]) + 1e-7 if fp32 else 2 ** -7 * abs(ref["l1_loss"])
+        checks = {"l2_loss": 1e-6 * abs(ref["l2_loss"]) if fp32 else 1e-4 * abs(ref["l2_loss"]),
+                  "l1_loss": l1_tol,
+                  "l0_loss": 0.0 if fp32 else 1e-3 * h + 1.0 / B,
+                  "explained_variance": 1e-6 if fp32 else 2e-3,
+                  "explained_variance_A": 1e-6 if fp32 else 4e-3,
+                  "explained_variance_B": 1e-6 if fp32 else 4e-3}
+        checks["loss"] = checks["l2_loss"] + d["l1_coeff"] * l1_tol * (1 if fp32 else 2) + 1e-6 * abs(ref["loss"])
+        for k, tol in checks.items():
+            assert abs(d[k] - ref[k]) <= tol, (s, k, d[k], ref[k], tol)
+        if s not in r["steps"]["after"]:
+            continue
+        want = r["steps"]["after"][s]
+        st = tr.optimizer.state  # (waits for the side-stream decoder half)
+        for k in O.PARAM_ORDER:
+            p = getattr(cc, k).detach().cpu()
+            pr = want["params"][k]
+            diff = (p.float() - pr.float()).abs()
+            if fp32:
+                assert diff.max().item() <= 0.01 * lr, (s, k, diff.max().item() / lr)
+            else:
+                exact = (diff == 0).float().mean().item()
+                print(f"{name} step {s} {k}: bit-identical {exact:.4f}, max diff / lr {diff.max().item() / lr:.3f}")
+                # (biases start at 0, so after a few steps their bf16 ulp is far below lr: the exact share
+                # drops with the step count, 0.41-0.60 measured; 0 without Adam)
+                assert exact >= (0.94 if k.startswith("W") else 0.30), (s, k, exact)
+                if k.startswith("W"):  # (near-zero params: the update's own rounding, ~lr)
+                    assert (diff <= 2 * _bf16_ulp(pr) + 3 * lr).all(), (s, k, (diff / lr).max().item())
+                else:
+                    assert diff.max().item() <= 0.25 * lr, (s, k, diff.max().item() / lr)
+            for mom in ("exp_avg", "exp_avg_sq"):
+                e = rel(st[getattr(cc, k)][mom].cpu(), want[mom][k])
+                assert e <= (1e-5 if fp32 else 0.05), (s, k, mom, e)
+
+
+# ----------------------------------------------------------------------------- adam / clip
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_adam_matches_torch(gpu, dtype):
+    g = torch.Generator().manual_seed(3)
+    n = 100003
+    p = (torch.randn(n, generator=g) * 0.05).to(dtype)
+    gr = (torch.randn(n, generator=g) * 1e-3).to(dtype)
+    m = (torch.randn(n, generator=g) * 1e-4).to(dtype)
+    v = (torch.rand(n, generator=g) * 1e-6).to(dtype)
+    coef = torch.tensor([0.5])
+    step, lr = 7, 5e-5
+    # reference: clip multiply then Adam (trainer.py:46-47)
+    pr, gref, mr, vr = p.clone(), gr.clone(), m.clone(), v.clone()
+    gref.mul_(coef.to(dtype))
+    O.adam_update(pr, gref, mr, vr, float(step), lr, 0.9, 0.999, 1e-8)
+    pg, gg, mg, vg = (t.to(gpu) for t in (p, gr, m, v))
+    ops.adam_step(pg, gg, mg, vg, coef.to(gpu), lr, 0.9, 0.999, 1e-8, step)
+    torch.cuda.synchronize()
+    for ours, ref in ((pg, pr), (mg, mr), (vg, vr)):
+        ours = ours.cpu()
+        if dtype == torch.float32:
+            assert rel(ours, ref) < 1e-6
+        else:
+            exact = (ours == ref).float().mean().item()
+            assert exact > 0.999, exact
+            ulp = ref.float().abs() * 2 ** -7 + 1e-30
+            assert ((ours.float() - ref.float()).abs() <= ulp).all()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("scale", [1e-3, 3.0])  # clip inactive / active
+def test_adam_with_in_kernel_clip_matches_clip_then_adam(gpu, dtype, scale):
+    """cc_adam_step_clip (the clip coefficient formed in the Adam launch from per-parameter squared sums, the
+    latent-sharded step's form) == cc_clip_finalize over the same sums + cc_adam_step, bit for bit (params,
+    moments and the clip outputs), in the one-pass and the capped grid-stride launch forms."""
+    g = torch.Generator().manual_seed(7)
+    n = 50021
+    mk = lambda sc: (torch.randn(n, generator=g) * sc).to(dtype).to(gpu)  # noqa: E731
+    p0, gr, m0 = mk(0.05), mk(1e-3), mk(1e-4)
+    v0 = (torch.rand(n, generator=g) * 1e-6).to(dtype).to(gpu)
+    sums = (torch.rand(4, generator=g) * scale).to(gpu)
+    outs = []
+    for fused in (False, True):
+        for max_blocks in (0, 64):
+            p, m, v = p0.clone(), m0.clone(), v0.clone()
+            clip = torch.zeros(8, device=gpu)
+            if fused:
+                ops.adam_step_clip(p, gr, m, v, sums, 1.0, dtype == torch.bfloat16, 5e-5, 0.9, 0.999, 1e-8, 3,
+                                   max_blocks=max_blocks, clip_out=clip)
+            else:
+                ops.clip_finalize(sums, [0, 1, 2, 3, 4], 1.0, dtype == torch.bfloat16, clip)
+                ops.adam_step(p, gr, m, v, clip[0:1], 5e-5, 0.9, 0.999, 1e-8, 3, max_blocks=max_blocks)
+            outs.append((p, m, v, clip[:6]))
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        for a, b in zip(o, outs[0]):
+            assert torch.equal(a, b)
+    assert (outs[0][3][0].item() < 1.0) == (scale > 1.0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_clip_matches_torch(gpu, dtype):
+    g = torch.Generator().manual_seed(5)
+    grads = [torch.randn(s, generator=g).to(dtype) for s in (1000, 3000, 16, 40)]
+    total = O.clip_grad_norm([t.clone() for t in grads])
+    sq = torch.cat([t.float().pow(2) for t in grads]).to(gpu)
+    off = [0]
+    for t in grads:
+        off.append(off[-1] + t.numel())
+    out = torch.empty(8, device=gpu)
+    ops.clip_finalize(sq, off, 1.0, dtype == torch.bfloat16, out)
+    torch.cuda.synchronize()
+    assert math.isclose(out[1].item(), total.float().item(), rel_tol=1e-6 if dtype == torch.float32 else 8e-3)
+    coef = min(1.0, 1.0 / (total.float().item() + 1e-6))
+    assert math.isclose(out[0].item(), coef, rel_tol=1e-6 if dtype == torch.float32 else 8e-3)
+
+
+# ----------------------------------------------------------------------------- full size
+@pytest.fixture(scope="module")
+def full_size_case():
+    B, n, d, h = 4096, 2, 2304, 16384
+    cfg = {"seed": 49, "dict_size": h, "d_in": d, "enc_dtype": "bf16", "dec_init_norm": 0.08, "device": "cpu"}
+    P = O.init_params(cfg)
+    g = torch.Generator().manual_seed(0)
+    raw = torch.randn(B, n, d, generator=g) * torch.tensor([1 / 0.2759, 1 / 0.2442])[None, :, None]
+    buf = raw.to(torch.bfloat16)
+    factor = torch.tensor([(d ** 0.5) / buf[:, i].float().norm(dim=-1).mean().item() for i in range(n)]).to(
+        torch.bfloat16)
+    x = O.buffer_next(buf, factor)
+    return cfg, P, buf, factor, x
+
+
+def test_full_size_config2_bf16(gpu, full_size_case):
+    """BASELINE config 2 (2x2304->16384, batch 4096, bf16): one fwd+bwd vs the oracle in fp32
+    on the same bf16-valued inputs (fp32 stands in for fp64 at this size)."""
+    cfg, P, buf, factor, x = full_size_case
+    cc = make_cc(cfg, P, gpu, 2)
+    ws = cc._workspace(buf.shape[0])
+    a = cc.arena()
+    G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+    engine.forward(ws, a, buf.to(gpu), factor.to(gpu))
+    engine.backward(ws, a, G, l1_coeff=2.0)
+    torch.cuda.synchronize()
+    acts_ours = ws.acts.cpu()
+    x_ours = ws.x.cpu()
+    # oracle in fp32 on the same rounded inputs
+    torch.set_num_threads(max(1, torch.get_num_threads()))
+    P32 = {k: v.float().clone().requires_grad_(True) for k, v in P.items()}
+    x32 = x.to(torch.bfloat16).float()
+    assert torch.equal(x_ours.float().view_as(x32), x32)
+    lo = O.get_losses(x32, P32, torch.float32)
+    (lo["l2_loss"] + 2.0 * lo["l1_loss"]).backward()
+    with torch.no_grad():
+        pre32 = O.encode(x32, P32, apply_relu=False)
+    flips = ((acts_ours > 0) != (pre32 > 0)).float().mean().item()
+    assert flips <= 2e-3, flips
+    s = ws.scalars[:6].cpu()
+    assert math.isclose(s[0].item(), lo["l2_loss"].item(), rel_tol=1e-2)
+    assert math.isclose(s[1].item(), lo["l1_loss"].item(), rel_tol=1e-2)
+    assert abs(s[2].item() - lo["l0_loss"].item()) <= 2e-3 * cfg["dict_size"]
+    assert math.isclose(s[3].item(), lo["explained_variance"].mean().item(), rel_tol=1e-2, abs_tol=1e-2)
+    Gv = G.views()
+    bounds = {"W_enc": 1e-1, "W_dec": 1e-2, "b_enc": 1e-2, "b_dec": 1e-2}
+    for k in O.PARAM_ORDER:
+        e = rel(Gv[k].cpu(), P32[k].grad)
+        assert e <= bounds[k], (k, e)
+
+
+def test_full_size_step_deterministic(gpu, full_size_case):
+    """Two identical fused steps produce bit-identical params (no atomics anywhere)."""
+    cfg, P, buf, factor, _ = full_size_case
+    outs = []
+    for _ in range(2):
+        cc = make_cc(dict(cfg, batch_size=4096, num_tokens=4096 * 100, lr=5e-5, beta1=0.9, beta2=0.999,
+                          l1_coeff=2), P, gpu, 2)
+        tr = ca.Trainer(dict(cc.cfg), buffer=_Replay([buf, buf], [factor, factor], gpu), crosscoder=cc)
+        d0 = tr.step()
+        d1 = tr.step()
+        torch.cuda.synchronize()
+        outs.append((d0, d1, cc.arena().data.clone()))
+    assert outs[0][0] == outs[1][0] and outs[0][1] == outs[1][1]
+    assert torch.equal(outs[0][2], outs[1][2])
+    assert outs[0][1]["l2_loss"] < outs[0][0]["l2_loss"]
+
+
+@pytest.mark.parametrize("side_rows", [0.0, 0.5, 1.0, "serial"])
+def test_decoder_adam_split_is_bit_identical(gpu, side_rows, monkeypatch):
+    """The decoder half of Adam split between the side stream (W_dec's first rows, beside the next G1) and the
+    next reader's stream (the rest + b_dec, engine.DEC_SIDE_ROWS) gives the same bits for any split, including
+    every row deferred (0.0), only b_dec deferred (1.0) and the whole half serial on the compute stream
+    (engine.DEC_ADAM_BESIDE_G1 False): params, both moments and the next step's losses."""
+    from crosscoder_amd import engine
+    B, n, d, h = 512, 2, 128, 1024
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+               num_tokens=B * 20, device=str(gpu))
+    outs = []
+    for frac in (engine.DEC_SIDE_ROWS, side_rows):
+        monkeypatch.setattr(engine, "DEC_ADAM_BESIDE_G1", frac != "serial")
+        monkeypatch.setattr(engine, "DEC_SIDE_ROWS", engine.DEC_SIDE_ROWS if frac == "serial" else frac)
+        cc = ca.CrossCoder(cfg)
+        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=4), crosscoder=cc)
+        dicts = [tr.step() for _ in range(3)]
+        st = tr.optimizer.state  # (launches the deferred rows, then orders after the side stream)
+        m = torch.cat([st[p]["exp_avg"].detach().flatten().float() for p in cc.parameters()])
+        v = torch.cat([st[p]["exp_avg_sq"].detach().flatten().float() for p in cc.parameters()])
+        torch.cuda.synchronize()
+        outs.append((dicts, cc.arena().data.clone(), m, v))
+    (d0, p0, m0, v0), (d1, p1, m1, v1) = outs
+    assert d0 == d1
+    assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+
+
+def test_delayed_side_stream_adam_still_orders_the_norm_readers(gpu, dbg_lib, monkeypatch):
+    """A step's decoder norms come from partial sums the decoder-half Adam writes: most rows on the side stream
+    (beside the next G1), the rest on the compute stream, whose next G2 launch carries the finaliser (G3 reads
+    tn, G4G5 inv_norms, the side stream's loss tail tn).  With the side-stream launch held back 3 ms (a spin
+    kernel queued before it on its stream: it then ends long after G1), every reader must still see the new
+    norms: losses, params and both moments equal an undelayed run's bit for bit."""
+    import ctypes
+
+    B, n, d, h = 1024, 2, 256, 2048
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+               num_tokens=B * 20, device=str(gpu))
+    orig = ops.adam_dec_norms
+    outs = []
+    for delay_ns in (0, 3_000_000):
+        def adam_dec_norms(*a, _ns=delay_ns, **k):
+            if _ns and k.get("max_blocks", 0) > 0:  # (the side-stream launch)
+                ops.check(dbg_lib.cc_debug_spin(1, 0, _ns, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+            orig(*a, **k)
+
+        monkeypatch.setattr(ops, "adam_dec_norms", adam_dec_norms)
+        cc = ca.CrossCoder(cfg)
+        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 4, seed=5), crosscoder=cc)
+        dicts = [tr.step() for _ in range(4)]
+        assert cc.arena().pending_rest is not None  # (the deferred-rows path ran)
+        st = tr.optimizer.state
+        m = torch.cat([st[p]["exp_avg"].detach().flatten().float() for p in cc.parameters()])
+        v = torch.cat([st[p]["exp_avg_sq"].detach().flatten().float() for p in cc.parameters()])
+        torch.cuda.synchronize()
+        outs.append((dicts, cc.arena().data.clone(), m, v))
+    (d0, p0, m0, v0), (d1, p1, m1, v1) = outs
+    assert d0 == d1
+    assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+
+
+@pytest.mark.parametrize("B,n,d,h", [(1024, 2, 256, 2048), (512, 4, 128, 1024)])
+def test_loss_tail_in_g3_matches_side_stream(gpu, B, n, d, h, monkeypatch):
+    """Trainer.step's loss tail carried by the backward's G3 launch (engine.LOSS_TAIL_IN_G3: its first workgroups
+    run it before their tiles, the last of them the finaliser, into mapped host memory) == the side-stream
+    launch forked before G3: the same loss dicts, params and moments, bit for bit; the arrival counters end at 0."""
+    from crosscoder_amd import engine
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+               num_tokens=B * 20, device=str(gpu))
+    outs = []
+    for in_g3 in (False, True):
+        monkeypatch.setattr(engine, "LOSS_TAIL_IN_G3", in_g3)
+        cc = ca.CrossCoder(cfg, n_models=n)
+        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 4, n_models=n, seed=7), crosscoder=cc)
+        dicts = [tr.step() for _ in range(4)]
+        tr.synchronize()
+        torch.cuda.synchronize()
+        ws = cc._workspace(B, step=True)
+        assert not bool(ws.tail_ctr.any()) and ws.tail_deferred is None
+        outs.append((dicts, cc.arena().data.clone(), tr.optimizer.exp_avg.data.clone()))
+    (d0, p0, m0), (d1, p1, m1) = outs
+    assert d0 == d1
+    assert torch.equal(p0, p1) and torch.equal(m0, m1)
+
+
+def test_dynamic_tile_order_is_bit_identical(gpu, dbg_lib, monkeypatch):
+    """The persistent G1 / G3 / G4G5 launches hand out tiles from per-XCD counters (engine.DYNAMIC_TILES); which
+    workgroup runs a tile must not change any bit.  Steps with the static order vs the dynamic order while 32
+    workgroups holding 96 KB of LDS each (no GEMM workgroup fits beside them) occupy CUs from another stream
+    for the first 0.6 ms of every step -- so the dynamic launches run uneven tile counts per workgroup --
+    give the same losses, params and moments, and every launch leaves its counters at zero."""
+    import ctypes
+
+    from crosscoder_amd import engine
+    B, n, d, h = 4096, 2, 512, 16384  # G1 / G3: 1024 tiles, G4G5: 512 tiles on 256 CUs
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+               num_tokens=B * 20, device=str(gpu))
+    hog = torch.cuda.Stream(device=gpu)
+    outs = []
+    for dynamic in (False, True):
+        monkeypatch.setattr(engine, "DYNAMIC_TILES", dynamic)
+        cc = ca.CrossCoder(cfg)
+        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=6), crosscoder=cc)
+        dicts = []
+        for _ in range(3):
+            hog.wait_stream(torch.cuda.current_stream(gpu))
+            ops.check(dbg_lib.cc_debug_spin(32, 96 * 1024, 600_000, ctypes.c_void_p(hog.cuda_stream)))
+            dicts.append(tr.step())
+        st = tr.optimizer.state
+        m = torch.cat([st[p]["exp_avg"].detach().flatten().float() for p in cc.parameters()])
+        v = torch.cat([st[p]["exp_avg_sq"].detach().flatten().float() for p in cc.parameters()])
+        torch.cuda.synchronize()
+        ws = cc._workspace(B, step=True)
+        assert not bool(ws.tile_ctr.any()) and not bool(ws.tail_ctr.any())
+        outs.append((dicts, cc.arena().data.clone(), m, v))
+    (d0, p0, m0, v0), (d1, p1, m1, v1) = outs
+    assert d0 == d1
+    assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+
+
+def test_full_size_config2_trainer_steps_match_oracle(gpu, full_size_case):
+    """BASELINE config 2 through the shipped schedule (Trainer.step: fused G2 + loss, G4G5 + grad tail + clip
+    in one launch, encoder / decoder Adam halves on two streams) vs the oracle's fp32 OracleTrainer.step
+    (trainer.py:41-63) on the same bf16-valued inputs and init, two steps (l1_coeff 0 then 2): the 9-key loss
+    dicts, the clip total norm / coefficient, and params + both Adam moments after each step, within the
+    SURVEY 8c bf16 envelope (bounds ~2x the values measured on MI355X)."""
+    cfg, P, buf, factor, x = full_size_case
+    cfg = dict(cfg, batch_size=4096, num_tokens=4096 * 20, lr=5e-5, beta1=0.9, beta2=0.999, l1_coeff=2)
+    cc = make_cc(cfg, P, gpu, 2)
+    tr = ca.Trainer(dict(cc.cfg), buffer=_Replay([buf, buf], [factor, factor], gpu), crosscoder=cc)
+    torch.set_num_threads(max(1, torch.get_num_threads()))
+    orc = O.OracleTrainer(dict(cfg, enc_dtype="fp32"), {k: v.float() for k, v in P.items()})
+    x32 = x.to(torch.bfloat16).float()
+    lr = cfg["lr"]
+    for s in range(2):
+        d = tr.step()
+        clip = cc._ws.clip_out[:2].cpu()
+        st = tr.optimizer.state  # (orders after the side-stream decoder half)
+        ours = {k: (getattr(cc, k).detach().float().cpu(), st[getattr(cc, k)]["exp_avg"].float().cpu(),
+                    st[getattr(cc, k)]["exp_avg_sq"].float().cpu()) for k in O.PARAM_ORDER}
+        ref = orc.step(x32)
+        assert list(d) == list(ref)
+        assert d["l1_coeff"] == ref["l1_coeff"] and d["lr"] == ref["lr"], s
+        for k, tol in (("l2_loss", 1e-2), ("l1_loss", 1e-2), ("loss", 1e-2)):
+            assert math.isclose(d[k], ref[k], rel_tol=tol, abs_tol=1e-6), (s, k, d[k], ref[k])
+        for k in ("explained_variance", "explained_variance_A", "explained_variance_B"):
+            assert abs(d[k] - ref[k]) <= 1e-2, (s, k, d[k], ref[k])
+        assert abs(d["l0_loss"] - ref["l0_loss"]) <= 2e-3 * cfg["dict_size"], (s, d["l0_loss"], ref["l0_loss"])
+        tn = orc.last_total_norm.item()
+        assert math.isclose(clip[1].item(), tn, rel_tol=2e-2), (s, clip[1].item(), tn)
+        assert math.isclose(clip[0].item(), min(1.0, 1.0 / (tn + 1e-6)), rel_tol=2e-2), (s, clip[0].item())
+        stats = {}
+        for k in O.PARAM_ORDER:
+            p, m, v = ours[k]
+            pr = orc.P[k].detach()
+            # Adam's update is ~lr * sign(m): params agree to the bf16 rounding of the result except where a
+            # small gradient's sign or the m / sqrt(v) ratio differs between the two precisions (<= ~2 lr)
+            diff = (p - pr).abs()
+            close = (diff <= _bf16_ulp(pr) + 0.05 * lr).float().mean().item()
+            worst = ((diff - 2 * _bf16_ulp(pr)).clamp_min(0) / lr).max().item()
+            stats[k] = (close, worst, rel(m, orc.m[k]), rel(v, orc.v[k]))
+            print(f"step {s} {k}: params close {close:.4f}, worst (diff - 2 ulp) / lr {worst:.3f}, "
+                  f"exp_avg rel {stats[k][2]:.2e}, exp_avg_sq rel {stats[k][3]:.2e}")
+        for k, (close, worst, em, ev) in stats.items():
+            tol = 0.2 if k == "W_enc" else 3e-2
+            assert close >= (0.93 if k == "W_enc" else 0.97), (s, k, close)  # (measured >= 0.965 / 0.9885)
+            assert worst <= 5.0, (s, k, worst)  # (measured <= 3.5: W_enc at step 2)
+            assert em <= tol and ev <= 2 * tol, (s, k, em, ev)
+
+
+# ----------------------------------------------------------------------------- batch slices / sharded
+@pytest.mark.parametrize("B,n,d,h", [(4096, 2, 2304, 1024),   # config-2 columns: 256 main tiles + 8-way split
+                                     (4000, 2, 2304, 512),    # split, ragged last row block
+                                     (1000, 2, 256, 1024),    # whole-tile grid only, ragged rows
+                                     (512, 4, 64, 384),       # n = 4, d = 64
+                                     (3968, 2, 2304, 512),    # split, last 256-row tile half empty
+                                     (8, 2, 64, 256),         # B <= 32: more fused partial rows than loss rows
+                                     (32, 2, 128, 256)])
+def test_fused_decode_loss_matches_two_pass(gpu, B, n, d, h):
+    """G2 + loss in one pass (cc_decode_loss_t: the loss as the GEMM epilogue, the split-K leftover summed
+    in reduce_splits' order) vs the two-pass form (cc_decode_fwd_ws_t + cc_loss_fwd_bwd_rows_t):
+    g_recon / g_recon^T and everything downstream of them (g_pre, W gradients) bit for bit; the
+    per-row loss terms, EV, loss scalars and the b_dec gradient to fp32 reassociation."""
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16", seed=5,
+               device=str(gpu))
+    cc = ca.CrossCoder(cfg, n_models=n)
+    g = torch.Generator().manual_seed(B + d)
+    raw = (torch.randn(B, n, d, generator=g) * 3).to(gpu)
+    factor = torch.tensor([0.7, 1.3, 0.9, 1.1][:n]).to(torch.bfloat16).to(gpu)
+    a = cc.arena()
+    res = []
+    for fused in (True, False):
+        ws = engine.StepWorkspace(B, n, d, h, torch.bfloat16, gpu)
+        assert ws.fused_ncb == d // 64
+        G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+        ws.g_recon.fill_(float("nan"))
+        ws.g_recon_t.fill_(float("nan"))
+        ws.loss_colpart.fill_(float("nan"))  # every partial row the backward reduces must be written
+        if fused:
+            engine.forward(ws, a, raw, factor)
+            assert ws.row_ncb == d // 64
+        else:
+            engine.forward(ws, a, raw, factor, loss=False)
+            engine.loss_rows(ws, a, 0, B)
+            engine.loss_finalize(ws)
+        engine.backward(ws, a, G, 2.0, clip=1.0)
+        torch.cuda.synchronize()
+        rp = engine._row_part(ws)
+        per_row = rp.view(2, n, -1, B).sum(2)  # [l2 / tv][model][row]
+        res.append(dict(g_recon=ws.g_recon.clone(), g_recon_t=ws.g_recon_t.clone(), g_pre_t=ws.g_pre_t.clone(),
+                        W=G.data[:2 * h * n * d + h].clone(), b_dec=G.b_dec_flat.clone(), per_row=per_row.clone(),
+                        ev=torch.stack([ws.ev, ws.ev_a, ws.ev_b]).clone(), scalars=ws.scalars[:6].clone(),
+                        clip=ws.clip_out[:2].clone()))
+    f, t = res
+    assert not bool(torch.isnan(f["g_recon"]).any())
+    for k in ("g_recon", "g_recon_t", "g_pre_t", "W"):
+        assert torch.equal(f[k], t[k]), k
+    assert torch.equal(f["g_recon_t"], f["g_recon"].t())
+    assert rel(f["per_row"], t["per_row"]) < 1e-5
+    assert (f["ev"] - t["ev"]).abs().max().item() < 1e-5
+    assert rel(f["scalars"], t["scalars"]) < 1e-6
+    # b_dec.grad = bf16(column sums of g_recon): at most one bf16 rounding apart
+    db = (f["b_dec"].float() - t["b_dec"].float()).abs()
+    assert bool((db <= t["b_dec"].float().abs() * 2 ** -7 + 1e-30).all())
+    assert rel(f["clip"], t["clip"]) < 1e-2
+
+
+@pytest.mark.parametrize("B", [1024, 1000])
+def test_sliced_loss_and_dacts_match_whole_batch(gpu, B):
+    """The sharded step's per-slice loss rows + d_acts (run as each slice's all-reduce lands)
+    reproduce the whole-batch launches bit for bit (same per-row math, same slab layout)."""
+    n, d, h = 2, 256, 1024
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16", seed=3,
+               device=str(gpu))
+    cc = ca.CrossCoder(cfg, n_models=n)
+    g = torch.Generator().manual_seed(9)
+    raw = (torch.randn(B, n, d, generator=g) * 3).to(gpu)
+    factor = torch.tensor([0.7, 1.3]).to(torch.bfloat16).to(gpu)
+    ws = cc._workspace(B)
+    a = cc.arena()
+    outs = []
+    for sliced in (False, True):
+        G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+        if sliced:
+            engine.forward(ws, a, raw, factor, loss=False)
+            chunks = engine.row_chunks(B, 4)
+            assert len(chunks) == 4 and chunks[-1][1] == B
+            for r0, r1 in chunks:
+                engine.loss_rows(ws, a, r0, r1)
+                engine.dacts_rows(ws, a, 2.0, r0, r1)
+            engine.loss_finalize(ws)
+            engine.backward(ws, a, G, 2.0, dacts_done=True)
+        else:  # the whole batch through the same two-pass decode + loss kernels
+            engine.forward(ws, a, raw, factor, loss=False)
+            engine.loss_rows(ws, a, 0, B)
+            engine.loss_finalize(ws)
+            engine.backward(ws, a, G, 2.0)
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in (ws.g_recon, ws.g_pre, ws.row_part, ws.loss_colpart, ws.scalars[:6],
+                                         G.data, ws.sq)])
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("B", [1024, 1000])
+def test_transposed_wgrad_step_matches_batch_major(gpu, B):
+    """The step with batch-contiguous copies (x^T, acts^T, g_recon^T, g_pre^T; G4/G5 KC/KC) gives the
+    same gradients, partial sums and losses bit for bit as the batch-major MN/MN form."""
+    n, d, h = 2, 256, 1024
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16", seed=4,
+               device=str(gpu))
+    cc = ca.CrossCoder(cfg, n_models=n)
+    g = torch.Generator().manual_seed(10)
+    raw = (torch.randn(B, n, d, generator=g) * 3).to(gpu)
+    factor = torch.tensor([0.7, 1.3]).to(torch.bfloat16).to(gpu)
+    a = cc.arena()
+    outs = []
+    for tr in (True, False):
+        ws = engine.StepWorkspace(B, n, d, h, torch.bfloat16, gpu, transposed=tr)
+        assert ws.tr == tr
+        ws.fused_ncb = 0  # both through the two-pass decode + loss (the fused form has its own test)
+        G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+        engine.forward(ws, a, raw, factor)
+        engine.backward(ws, a, G, 2.0)
+        torch.cuda.synchronize()
+        if ws.tr:  # the transposed copies are exact transposes
+            assert torch.equal(ws.x_t, ws.x.t()) and torch.equal(ws.acts_t, ws.acts.t())
+            assert torch.equal(ws.g_recon_t, ws.g_recon.t())
+        outs.append([t.clone() for t in (ws.acts, ws.g_recon, ws.g_pre, ws.scalars[:6], G.data, ws.sq)])
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("rows,cols,r0,c0", [(4096, 4608, 0, 0), (72, 136, 0, 0), (200, 64, 8, 16), (8, 8, 0, 0)])
+def test_transpose_b16(gpu, rows, cols, r0, c0):
+    """cc_transpose_b16 over a (possibly offset) sub-matrix into a column slice of a wider output."""
+    g = torch.Generator().manual_seed(rows * 7 + cols)
+    src = torch.randn(rows + r0, cols + c0 + 8, generator=g).to(torch.bfloat16).to(gpu)
+    view = src[r0:, c0:c0 + cols]
+    out = torch.full((cols, rows + 16), 7.0, dtype=torch.bfloat16, device=gpu)
+    ops.transpose(view, out=out[:, 8:8 + rows])
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, 8:8 + rows], view.t())
+    assert bool((out[:, :8] == 7).all()) and bool((out[:, 8 + rows:] == 7).all())  # nothing outside the slice
+
+
+@pytest.mark.parametrize("h,n,d", [(16384, 2, 2304), (200, 2, 64), (72, 3, 192)])
+def test_transpose_dec_norms_matches_dec_norms(gpu, h, n, d):
+    """The fused W_dec^T + decoder-norms pass gives cc_dec_norms' bits and the exact transpose;
+    both match fp64 norms."""
+    g = torch.Generator().manual_seed(h + d)
+    W = (torch.randn(h, n * d, generator=g) * 0.05).to(torch.bfloat16).to(gpu)
+    W[3] = 0  # zero rows: inverse norm 0
+    E = lambda *s_: torch.empty(*s_, device=gpu)  # noqa: E731
+    nm1, tn1, inv1 = E(h, n), E(h), E(h, n)
+    ops.dec_norms(W, h, n, d, norms=nm1, total=tn1, inv_norms=inv1)
+    Wt = torch.empty(n * d, h, dtype=torch.bfloat16, device=gpu)
+    nm2, tn2, inv2 = E(h, n), E(h), E(h, n)
+    ops.transpose_dec_norms(W, n, d, Wt, E(ops.dec_norms_part_floats(h, n, d)), nm2, tn2, inv2)
+    torch.cuda.synchronize()
+    assert torch.equal(Wt, W.t())
+    assert torch.equal(nm1, nm2) and torch.equal(tn1, tn2) and torch.equal(inv1, inv2)
+    ref = W.double().view(h, n, d).norm(dim=-1).cpu()
+    assert rel(nm1, ref) < 1e-6 and float(inv1[3].abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("B,n,d", [(4096, 2, 2304), (1000, 2, 40), (72, 3, 520)])
+def test_prep_and_loss_transposed_outputs(gpu, B, n, d):
+    """cc_prep_input_t / cc_loss_fwd_bwd_rows_t: the same x / g_recon / partial slabs as the plain
+    kernels, plus exact transposes (loss over two row ranges written into one g_recon_t)."""
+    K = n * d
+    g = torch.Generator().manual_seed(B + K)
+    bf = torch.bfloat16
+    x_in = (torch.randn(B, n, d, generator=g) * 3).to(gpu)
+    factor = (torch.rand(n, generator=g) + 0.5).to(bf).to(gpu)
+    E = lambda *s_, dt=torch.float32: torch.empty(*s_, dtype=dt, device=gpu)  # noqa: E731
+    x1, x2, xt = E(B, K, dt=bf), E(B, K, dt=bf), E(K, B, dt=bf)
+    cp1, cp2 = E(ops.prep_part_rows(B), K), E(ops.prep_part_rows(B), K)
+    ops.prep_input(x_in, factor, bf, out=x1, colsum_part=cp1)
+    ops.prep_input(x_in, factor, bf, out=x2, colsum_part=cp2, out_t=xt)
+    recon = torch.randn(B, K, generator=g).to(gpu)
+    b_dec = (torch.randn(K, generator=g) * 0.1).to(bf).to(gpu)
+    mu = torch.randn(K, generator=g).to(gpu)
+    ncb = ops.loss_col_blocks(d)
+    outs = []
+    for tr in (False, True):
+        gr, gt = E(B, K, dt=bf), torch.zeros(K, B, dtype=bf, device=gpu)
+        rp, lc = E(2, n * ncb, B), E(ops.loss_part_rows(B), K)
+        cut = 32 * (B // 64)
+        for r0, r1 in ((0, cut), (cut, B)) if cut else ((0, B),):
+            ops.loss_fwd_bwd(recon, b_dec, x1, mu, gr, rp, lc, 2.0 / B, B, n, d, row0=r0, rows=r1 - r0,
+                             g_recon_t=gt if tr else None)
+        outs.append((gr, rp, lc, gt))
+    torch.cuda.synchronize()
+    assert torch.equal(x1, x2) and torch.equal(cp1, cp2) and torch.equal(xt, x1.t())
+    for a, b in zip(outs[0][:3], outs[1][:3]):
+        assert torch.equal(a, b)
+    assert torch.equal(outs[1][3], outs[1][0].t())
+
+
+@pytest.mark.parametrize("B,K,h", [(512, 768, 768), (1000, 80, 200), (4096, 4608, 2048)])
+def test_transposed_epilogue_outputs(gpu, B, K, h):
+    """cc_encode_fwd_t's acts_t and cc_dacts_bwd_t's g_pre_t (whole batch and a batch slice written
+    into its columns) are the exact transposes of cc_encode_fwd / cc_dacts_bwd's outputs."""
+    g = torch.Generator().manual_seed(B + K + h)
+    bf = torch.bfloat16
+    mk = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).to(bf).to(gpu)  # noqa: E731
+    x, W, b, Wd = mk(B, K), mk(h, K, sc=0.05), mk(h, sc=0.1), mk(h, K, sc=0.05)
+    g_recon = mk(B, K, sc=1e-2)
+    tn = torch.rand(h, generator=g).to(gpu) + 0.5
+    acts = torch.empty(B, h, dtype=bf, device=gpu)
+    acts2, acts_t = torch.empty_like(acts), torch.empty(h, B, dtype=bf, device=gpu)
+    bits = torch.zeros(ops.mask_bits_words(B, h), dtype=torch.int32, device=gpu)
+    ops.encode_fwd(x, W, b, acts, True)
+    ops.encode_fwd_t(x, W, b, acts2, acts_t, True, mask_bits=bits)
+    g_pre = torch.empty(B, h, dtype=bf, device=gpu)
+    ops.dacts_bwd(g_recon, Wd, acts, tn, 3e-4, g_pre)
+    r0 = 256 if B > 256 else 0
+    outs = []
+    for mb in (None, bits):  # the acts-tile mask, or G1's mask bits (whole-tile shapes): same bits
+        g_pre_t = torch.zeros(h, B, dtype=bf, device=gpu)
+        ops.dacts_bwd_t(g_recon, Wd, acts, tn, 3e-4, g_pre_t, mask_bits=mb)
+        g_pre_t2 = torch.zeros(h, B, dtype=bf, device=gpu)
+        ops.dacts_bwd_t(g_recon[r0:], Wd, acts[r0:], tn, 3e-4, g_pre_t2[:, r0:],
+                        mask_bits=None if mb is None else ops.mask_bits_rows(mb, h, r0, B))
+        outs.append((g_pre_t, g_pre_t2))
+    torch.cuda.synchronize()
+    assert torch.equal(acts, acts2) and torch.equal(acts_t, acts.t())
+    # the bits: acts > 0 in accumulator order (tile, wave 2 x 4, lane, fragment i, j, element e)
+    nbm, nbn = -(-B // 256), -(-h // 256)
+    bt = bits.view(nbm, nbn, 2, 4, 64, 4).cpu()
+    ti, tj, wr, wc, ln = 0, nbn - 1, 1, 2, 37
+    for i in range(8):
+        for j in range(4):
+            for e in range(4):
+                r = ti * 256 + wr * 128 + 16 * i + (ln & 15)
+                c = tj * 256 + wc * 64 + 16 * j + 4 * (ln >> 4) + e
+                b = 4 * (4 * i + j) + e
+                bit = (int(bt[ti, tj, wr, wc, ln, b >> 5]) >> (b & 31)) & 1
+                want = bool(acts[r, c] > 0) if r < B and c < h else False
+                assert bit == want, (i, j, e)
+    for g_pre_t, g_pre_t2 in outs:
+        assert torch.equal(g_pre_t, g_pre.t())
+        assert torch.equal(g_pre_t2[:, r0:], g_pre[r0:].t()) and not bool(g_pre_t2[:, :r0].any())
+
+
+@pytest.mark.parametrize("h", [2048, 200])
+@pytest.mark.parametrize("max_blocks", [0, 256])
+def test_tiled_decoder_adam_matches_flat(gpu, h, max_blocks):
+    """cc_adam_dec_transposed (decoder-half Adam in 64x64 tiles that also writes W_dec^T and the decoder
+    norm partials) == the flat cc_adam_step over the same half, bit for bit; its W_dec^T is the exact
+    transpose of the updated W_dec and cc_dec_norms_finalize gives cc_dec_norms' bits."""
+    n, d = 2, 256
+    K = n * d
+    g = torch.Generator().manual_seed(h + max_blocks)
+    bf = torch.bfloat16
+    mk = lambda sc: (torch.randn(h, K, generator=g) * sc).to(bf).to(gpu)  # noqa: E731
+    p0, gr, m0, v0 = mk(0.05), mk(1e-3), mk(1e-4), (torch.rand(h, K, generator=g) * 1e-6).to(bf).to(gpu)
+    coef = torch.tensor([0.7], device=gpu)
+    args = (coef, 5e-5, 0.9, 0.999, 1e-8, 3)
+    pf, mf, vf = p0.clone(), m0.clone(), v0.clone()
+    ops.adam_step(pf, gr.clone(), mf, vf, *args)
+    pt, mt, vt = p0.clone(), m0.clone(), v0.clone()
+    Wt = torch.empty(K, h, dtype=bf, device=gpu)
+    part = torch.empty(ops.dec_norms_part_floats(h, n, d), device=gpu)
+    ops.adam_dec_transposed(pt, gr.clone(), mt, vt, *args, Wt, part, max_blocks=max_blocks)
+    E = lambda *s_: torch.empty(*s_, device=gpu)  # noqa: E731
+    nm1, tn1, inv1 = E(h, n), E(h), E(h, n)
+    ops.dec_norms_finalize(part, h, n, d, nm1, tn1, inv1)
+    nm2, tn2, inv2 = E(h, n), E(h), E(h, n)
+    ops.dec_norms(pf, h, n, d, norms=nm2, total=tn2, inv_norms=inv2)
+    torch.cuda.synchronize()
+    assert torch.equal(pt, pf) and torch.equal(mt, mf) and torch.equal(vt, vf)
+    assert torch.equal(Wt, pf.t())
+    assert torch.equal(nm1, nm2) and torch.equal(tn1, tn2) and torch.equal(inv1, inv2)
+
+
+@pytest.mark.parametrize("h", [2048, 200])
+@pytest.mark.parametrize("max_blocks", [0, 256])
+@pytest.mark.parametrize("clip", ["coef", "sums"])
+def test_decoder_adam_norms_matches_flat(gpu, h, max_blocks, clip):
+    """cc_adam_dec_norms (the decoder-half Adam that also writes the decoder-norm partials of the updated
+    W_dec) == cc_adam_step / cc_adam_step_clip over the same half [W_dec | b_dec] bit for bit, and
+    cc_dec_norms_finalize of its partials gives cc_dec_norms' bits on the updated W_dec."""
+    n, d = 2, 256
+    K = n * d
+    numel = h * K + K
+    g = torch.Generator().manual_seed(h + max_blocks + len(clip))
+    bf = torch.bfloat16
+    mk = lambda sc: (torch.randn(numel, generator=g) * sc).to(bf).to(gpu)  # noqa: E731
+    p0, gr, m0, v0 = mk(0.05), mk(1e-3), mk(1e-4), (torch.rand(numel, generator=g) * 1e-6).to(bf).to(gpu)
+    coef = torch.tensor([0.7], device=gpu)
+    sums = torch.tensor([40.0, 3.0, 0.5, 0.25], device=gpu)
+    hyper = (5e-5, 0.9, 0.999, 1e-8, 3)
+    pf, mf, vf = p0.clone(), m0.clone(), v0.clone()
+    if clip == "coef":
+        ops.adam_step(pf, gr.clone(), mf, vf, coef, *hyper)
+    else:
+        ops.adam_step_clip(pf, gr.clone(), mf, vf, sums, 1.0, True, *hyper)
+    pt, mt, vt = p0.clone(), m0.clone(), v0.clone()
+    part = torch.full((ops.dec_norms_part_floats(h, n, d),), float("nan"), device=gpu)
+    ops.adam_dec_norms(pt, gr.clone(), mt, vt, h, K, *hyper, part, coef=coef if clip == "coef" else None,
+                       clip_sums=(sums, 1.0) if clip == "sums" else None, max_blocks=max_blocks)
+    E = lambda *s_: torch.empty(*s_, device=gpu)  # noqa: E731
+    nm1, tn1, inv1 = E(h, n), E(h), E(h, n)
+    ops.dec_norms_finalize(part, h, n, d, nm1, tn1, inv1)
+    nm2, tn2, inv2 = E(h, n), E(h), E(h, n)
+    ops.dec_norms(pf[:h * K].view(h, K), h, n, d, norms=nm2, total=tn2, inv_norms=inv2)
+    torch.cuda.synchronize()
+    assert torch.equal(pt, pf) and torch.equal(mt, mf) and torch.equal(vt, vf)
+    assert not bool(torch.isnan(part).any())
+    assert torch.equal(nm1, nm2) and torch.equal(tn1, tn2) and torch.equal(inv1, inv2)
+
+
+@pytest.mark.parametrize("B, n, d, h", [(4096, 2, 2304, 2048), (1024, 2, 256, 1024), (1000, 4, 128, 512),
+                                        (512, 2, 64, 200)])
+def test_decode_loss_on_wdec_matches_transposed(gpu, B, n, d, h):
+    """The fused G2 + loss reading W_dec [h][K] itself (cc_decode_loss, transposed LDS reads of the B operand)
+    == the same pass over W_dec^T (cc_decode_loss_t), bit for bit in every output: both loops accumulate each
+    output in the same k order."""
+    K = n * d
+    g = torch.Generator().manual_seed(B + h)
+    bf = torch.bfloat16
+    acts = torch.relu(torch.randn(B, h, generator=g)).to(bf).to(gpu)
+    W = (torch.randn(h, K, generator=g) * 0.05).to(bf).to(gpu)
+    b_dec = (torch.randn(K, generator=g) * 0.1).to(bf).to(gpu)
+    x = torch.randn(B, K, generator=g).to(bf).to(gpu)
+    x_mean = x.float().mean(0)
+    ncb = ops.decode_loss_ncb(B, h, n, d, bf)
+    assert ncb == d // 64
+    nws = max(ops.decode_ws_floats(B, h, K, bf), 1)
+    outs = []
+    for direct in (False, True, "no_t"):
+        g_recon = torch.full((B, K), float("nan"), dtype=bf, device=gpu)
+        g_t = torch.full((K, B), float("nan"), dtype=bf, device=gpu)
+        rp = torch.full((2, n * ncb, B), float("nan"), device=gpu)
+        cp = torch.full((ops.col_part_rows(B), K), float("nan"), device=gpu)
+        dws = torch.empty(nws, device=gpu)
+        if direct == "no_t":  # g_recon^T not wanted: everything else the same, g_t untouched
+            ops.decode_loss(acts, W, b_dec, x, x_mean, 2.0 / B, g_recon, None, rp, cp, dws, n, d)
+        elif direct:
+            ops.decode_loss(acts, W, b_dec, x, x_mean, 2.0 / B, g_recon, g_t, rp, cp, dws, n, d)
+        else:
+            ops.decode_loss_t(acts, W.t().contiguous(), b_dec, x, x_mean, 2.0 / B, g_recon, g_t, rp, cp, dws, n, d)
+        outs.append((g_recon, g_t, rp, cp))
+    torch.cuda.synchronize()
+    for a, b in zip(outs[0], outs[1]):
+        assert not bool(torch.isnan(a.float()).any())
+        assert torch.equal(a, b)
+    g_recon, g_t, rp, cp = outs[2]
+    assert torch.equal(g_recon, outs[0][0]) and torch.equal(rp, outs[0][2]) and torch.equal(cp, outs[0][3])
+    assert bool(torch.isnan(g_t.float()).all())
+    # the decoder norms' finaliser carried by the launch (the split-K leftover's, or before the GEMM where the
+    # shape has none): cc_dec_norms_finalize's bits, the GEMM outputs unchanged
+    part = torch.rand(ops.dec_norms_part_floats(h, n, d), generator=g).to(gpu)
+    ref = [torch.full(sh, float("nan"), device=gpu) for sh in ((h, n), (h,), (h, n))]
+    ops.dec_norms_finalize(part, h, n, d, *ref)
+    got = [torch.full_like(r, float("nan")) for r in ref]
+    g_recon = torch.full((B, K), float("nan"), dtype=bf, device=gpu)
+    g_t = torch.full((K, B), float("nan"), dtype=bf, device=gpu)
+    rp = torch.full((2, n * ncb, B), float("nan"), device=gpu)
+    cp = torch.full((ops.col_part_rows(B), K), float("nan"), device=gpu)
+    ops.decode_loss(acts, W, b_dec, x, x_mean, 2.0 / B, g_recon, g_t, rp, cp, torch.empty(nws, device=gpu), n, d,
+                    norm_fin=(part, *got))
+    torch.cuda.synchronize()
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+    for a, b in zip((g_recon, g_t, rp, cp), outs[1]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("comm", ["all_reduce", "reduce_scatter"])
+@pytest.mark.parametrize("chunks", [1, 2])
+def test_sharded_trainer_world1_matches_trainer(gpu, comm, chunks):
+    """ShardedTrainer over a 1-rank RCCL group takes the same steps as the single-GPU Trainer, in the shipped
+    exchange forms: the all-reduce as one synchronous collective (1 slice, the world-1 default) or in the 2
+    batch slices of the world > 1 default (slice 2's exchange in flight during slice 1's loss rows + d_acts), and
+    the reduce-scatter + all-gather exchange."""
+    import os
+
+    import torch.distributed as dist
+    from crosscoder_amd import sharded
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(29600 + os.getpid() % 1000 + 2 * (comm == "reduce_scatter") + chunks)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
+    try:
+        B, n, d, h = 1024, 2, 256, 2048
+        cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+                   num_tokens=B * 20, device=str(gpu))
+        dicts = []
+        for which in ("single", "sharded"):
+            buf = ca.SyntheticBuffer(cfg, rows=B * 3, seed=1)
+            if which == "single":
+                tr = ca.Trainer(cfg, buffer=buf, crosscoder=ca.CrossCoder(cfg))
+            else:
+                tr = sharded.ShardedTrainer(cfg, buffer=buf, recon_chunks=chunks, comm=comm)
+            dicts.append([tr.step() for _ in range(3)])
+            torch.cuda.synchronize()
+            if which == "single":
+                p_single = tr.crosscoder.arena().data.float().cpu()
+            else:
+                p_sharded = tr.crosscoder.arena().data.float().cpu()
+        for a, b in zip(*dicts):
+            for k in ("l2_loss", "l1_loss", "l0_loss", "explained_variance"):
+                assert math.isclose(a[k], b[k], rel_tol=2e-4, abs_tol=1e-4), (k, a[k], b[k])
+            assert a["lr"] == b["lr"] and a["l1_coeff"] == b["l1_coeff"]
+        # the reconstruction (fp32 partial + b_dec, vs the fused G2 + loss) and the clip sums are combined in a
+        # different order: a bf16 rounding may flip, the bounds of test_gpu_sharded.py
+        d = (p_single - p_sharded).abs()
+        assert d.max().item() <= 4 * cfg["lr"] + 2 ** -7 * p_single.abs().max().item(), d.max().item()
+        assert (d == 0).float().mean().item() > 0.9
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shape", [(4096, 16384, 4608), (4096, 2048, 4608), (4000, 1024, 4600), (1024, 1024, 2304),
+                                   (300, 512, 200)])
+def test_decode_split_schedule(gpu, dbg_lib, shape):
+    """cc_decode_fwd_ws (whole 256-tile waves + split-K leftover tiles) vs the single-launch decode:
+    the whole-wave columns bit for bit, the split columns to fp32 summation order, both vs fp64
+    (ragged batch / column tails included)."""
+    B, h, K = shape
+    g = torch.Generator().manual_seed(B + h + K)
+    acts = torch.relu(torch.randn(B, h, generator=g)).to(torch.bfloat16).to(gpu)
+    W = (torch.randn(h, K, generator=g) * 0.05).to(torch.bfloat16).to(gpu)
+    nws = ops.decode_ws_floats(B, h, K, torch.bfloat16)
+    nbm, nbn = -(-B // 256), -(-K // 256)
+    waves = nbm * nbn // 256
+    split = waves > 0 and (nbm * nbn) % 256 and (256 * waves) % nbm == 0
+    assert bool(nws) == bool(split)
+    ws = torch.full((nws,), float("nan"), device=gpu) if nws else None
+    r_split = torch.empty(B, K, device=gpu)
+    r_one = torch.empty(B, K, device=gpu)
+    ops.decode_partial(acts, W, r_split, ws)
+    ops.decode_fwd(acts, W, None, recon_f32=r_one)
+    r_t = torch.empty(B, K, device=gpu)
+    ops.decode_partial_t(acts, W.t().contiguous(), r_t, ws)  # W_dec^T operand: same schedule, same bits
+    # main tiles + split units as two launches instead of one: same bits
+    lib = ops.lib()
+    r_two, r_two_t = torch.empty(B, K, device=gpu), torch.empty(B, K, device=gpu)
+    lib.cc_debug_set_dec_one_launch(0)
+    try:
+        ops.decode_partial(acts, W, r_two, ws)
+        ops.decode_partial_t(acts, W.t().contiguous(), r_two_t, ws)
+    finally:
+        lib.cc_debug_set_dec_one_launch(1)
+    torch.cuda.synchronize()
+    assert torch.equal(r_t, r_split)
+    assert torch.equal(r_two, r_split) and torch.equal(r_two_t, r_split)
+    if (B, h, K) == (4096, 16384, 4608):
+        assert nws == 8 * 4096 * 512  # 32 leftover tiles of 288 -> 8-way split
+    ref = acts.double().cpu() @ W.double().cpu()
+    assert rel(r_split, ref) < 1e-5
+    assert rel(r_split, r_one) < 1e-6
+    if nws:
+        col0 = 256 * (256 * waves // nbm)
+        assert torch.equal(r_split[:, :col0], r_one[:, :col0])
+
+
+@pytest.mark.parametrize("B,h,K", [(512, 512, 256), (4096, 16384, 4608)])
+def test_whole_tile_epilogue_matches_general_form(gpu, dbg_lib, B, h, K):
+    """G1 / G3 on whole 256 x 256 tiles with the ReLU on take the epilogue's fast kernel form (no range
+    selects, one bf16 conversion, integer l0 count): every output and partial slab bit-identical to the
+    general form (cc_debug_set_pp_fast(0)), which partial tiles use."""
+    g = torch.Generator().manual_seed(11)
+    bf = torch.bfloat16
+    x = torch.randn(B, K, generator=g).to(bf).to(gpu)
+    W = (torch.randn(h, K, generator=g) * 0.05).to(bf).to(gpu)
+    b_enc = (torch.randn(h, generator=g) * 0.1).to(bf).to(gpu)
+    tn = torch.rand(h, generator=g).to(gpu)
+    g_recon = (torch.randn(B, K, generator=g) * 1e-3).to(bf).to(gpu)
+    lib = ops.lib()
+
+    def run():
+        acts, acts_t = torch.empty(B, h, device=gpu, dtype=bf), torch.empty(h, B, device=gpu, dtype=bf)
+        colp = torch.zeros(ops.col_part_rows(B), h, device=gpu)
+        l0p = torch.zeros(1 << 16, device=gpu)
+        bits = torch.zeros(ops.mask_bits_words(B, h), dtype=torch.int32, device=gpu)
+        ops.encode_fwd_t(x, W, b_enc, acts, acts_t, True, colsum_part=colp, l0_part=l0p, mask_bits=bits)
+        gp_t = torch.empty(h, B, device=gpu, dtype=bf)
+        colp3 = torch.zeros(ops.col_part_rows(B), h, device=gpu)
+        # (the fast d_acts form reads the mask bits, the general one the acts tile)
+        ops.dacts_bwd_t(g_recon, W, acts, tn, 1e-4, gp_t, colsum_part=colp3, mask_bits=bits)
+        torch.cuda.synchronize()
+        return acts, acts_t, colp, l0p, gp_t, colp3
+
+    fast = run()
+    lib.cc_debug_set_pp_fast(0)
+    try:
+        general = run()
+    finally:
+        lib.cc_debug_set_pp_fast(1)
+    for a, b in zip(fast, general):
+        assert torch.equal(a.view(torch.int16) if a.dtype == bf else a, b.view(torch.int16) if b.dtype == bf else b)
+    assert fast[0].float().max() > 0 and (fast[4] != 0).any()
+
+
+# ----------------------------------------------------------------------------- around the step (§8f)
+def test_buffer_matches_reference_with_fake_lms(gpu):
+    """Buffer (buffer.py:12-125) with deterministic fake LMs: normalisation factors and every next()
+    batch bit-identical to the reference's, across refreshes (the shuffle is cc_gather_rows)."""
+    import json
+    import os
+
+    from tests.test_cpu_host import FakeLM
+
+    r = torch.load(os.path.join("tests", "golden", "buffer_fake_lm.pt"), weights_only=True)
+    cfg = dict(json.loads(r["cfg"]), device=str(gpu))
+    torch.manual_seed(49)
+    buf = ca.Buffer(cfg, FakeLM(r["A_table"], r["A_pos"]), FakeLM(r["B_table"], r["B_pos"]), r["tokens"])
+    assert torch.equal(buf.normalisation_factor.cpu(), r["normalisation_factor"])
+    assert buf.buffer.shape[0] == r["buffer_size"] and buf.buffer.is_cuda
+    for want in r["next"]:
+        assert torch.equal(buf.next().cpu(), want)
+
+
+@pytest.mark.parametrize("rows,row_elems,dtype", [(523776 // 64, 2 * 2304, torch.bfloat16), (1000, 24, torch.float32),
+                                                  (7, 8, torch.bfloat16), (0, 8, torch.float32)])
+def test_gather_rows_matches_torch_indexing(gpu, rows, row_elems, dtype):
+    g = torch.Generator().manual_seed(rows + row_elems)
+    src = torch.randn(max(rows, 1), row_elems, generator=g).to(dtype).to(gpu)
+    perm = torch.randperm(rows, generator=g).to(gpu)
+    out = ops.gather_rows(src[:rows] if rows else src[:0], perm)
+    torch.cuda.synchronize()
+    assert torch.equal(out, src[:rows][perm])
+    # an out-of-range index gives a zero row, never a fault
+    if rows:
+        bad = perm.clone()
+        bad[0] = rows + 5
+        out2 = ops.gather_rows(src[:rows], bad)
+        torch.cuda.synchronize()
+        assert torch.equal(out2[0], torch.zeros_like(out2[0])) and torch.equal(out2[1:], src[:rows][perm[1:]])
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("fold_decoder", [True, False])
+def test_fold_activation_scaling_factor_matches_reference(gpu, dtype, fold_decoder):
+    """Crosscoder_model_diff.ipynb:35368-35378 (and the encoder-only variant :35752-35763) restated in
+    torch on the CPU vs cc_fold_scaling: bit-identical parameters."""
+    r = load(f"step_b64_n2_d32_h256_{dtype}")
+    cfg = dict(r["cfg"], device=str(gpu))
+    P = {k: v.clone() for k, v in r["init"].items()}
+    P["b_dec"] = (torch.randn(P["b_dec"].shape, generator=torch.Generator().manual_seed(1)) * 0.1).to(P["b_dec"].dtype)
+    cc = make_cc(cfg, P, gpu, 2)
+    base, chat = 0.2758961493232058, 0.24422852496546169
+    ca.fold_activation_scaling_factor(cc, base, chat, fold_decoder=fold_decoder)
+    ref = {k: v.clone() for k, v in P.items()}
+    ref["W_enc"][0] = ref["W_enc"][0] * base
+    ref["W_enc"][1] = ref["W_enc"][1] * chat
+    if fold_decoder:
+        ref["W_dec"][:, 0, :] = ref["W_dec"][:, 0, :] / base
+        ref["W_dec"][:, 1, :] = ref["W_dec"][:, 1, :] / chat
+        ref["b_dec"][0, :] = ref["b_dec"][0, :] / base
+        ref["b_dec"][1, :] = ref["b_dec"][1, :] / chat
+    sd = cc.state_dict()
+    for k in O.PARAM_ORDER:
+        assert torch.equal(sd[k].cpu(), ref[k]), k
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_decoder_stats_match_reference_analysis(gpu, dtype):
+    """analysis.py:9-40 (norms, relative norms, shared mask, cosine sims) vs an fp64 evaluation of the
+    same weights (fp32 results: rel <= 1e-5) and vs the reference's own dtype arithmetic."""
+    r = load(f"step_b64_n2_d32_h256_{dtype}")
+    cfg = dict(r["cfg"], device=str(gpu))
+    P = {k: v.clone() for k, v in r["init"].items()}
+    g = torch.Generator().manual_seed(2)
+    P["W_dec"] = (P["W_dec"].float() * (0.2 + torch.rand(P["W_dec"].shape[0], 2, 1, generator=g) * 2)).to(
+        P["W_dec"].dtype)
+    cc = make_cc(cfg, P, gpu, 2)
+    st = ca.decoder_stats(cc)
+    W = P["W_dec"].double()
+    norms = W.norm(dim=-1)
+    rel = norms[:, 1] / norms.sum(dim=-1)
+    cos = (W[:, 0, :] * W[:, 1, :]).sum(-1) / (W[:, 0, :].norm(dim=-1) * W[:, 1, :].norm(dim=-1))
+    assert rel_(st["norms"], norms) < 1e-5 and rel_(st["relative_norms"], rel) < 1e-5
+    assert rel_(st["cosine_sims"], cos) < 1e-5
+    assert torch.equal(st["shared_latent_mask"].cpu(), ((rel.float() < 0.7) & (rel.float() > 0.3)))
+    # the reference's own arithmetic in the parameter dtype (what analysis.py prints)
+    Wd = P["W_dec"]
+    ref_norms = Wd.norm(dim=-1)
+    tol = 1e-6 if dtype == "fp32" else 2 ** -7
+    assert ((st["norms"].cpu() - ref_norms.float()).abs() <= tol * ref_norms.float().abs() + 1e-7).all()
+
+
+def rel_(a, b):
+    return rel(a, b)
+
+
+def test_segment_sums(gpu):
+    g = torch.Generator().manual_seed(4)
+    sq = torch.rand(5000, generator=g).to(gpu)
+    off = [0, 1000, 4100, 4200, 5000]
+    out = torch.empty(4, device=gpu)
+    ops.segment_sums(sq, off, out, zero_mask=1 << 3)
+    torch.cuda.synchronize()
+    ref = [sq[a:b].double().sum().item() for a, b in zip(off, off[1:])]
+    assert all(math.isclose(out[i].item(), ref[i], rel_tol=1e-6) for i in range(3)) and out[3].item() == 0.0
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("zero_mask", [0, 1 << 3])
+def test_grad_tail_sums_match_separate_launches(gpu, dtype, zero_mask):
+    """cc_grad_tail_sums (bias-gradient column sums + squared-sum partials + per-parameter sums, one
+    launch: the latent-sharded step's backward tail) == 2 x reduce_rows + segment_sums, bit for bit."""
+    h, K, R1, R2, nw = 1000, 4608, 16, 128, 3000
+    g = torch.Generator().manual_seed(7)
+    gpc = torch.randn(R1, h, generator=g).to(gpu)
+    lpc = torch.randn(R2, K, generator=g).to(gpu)
+    nr1, nr2 = ops.reduce_parts(h), ops.reduce_parts(K)
+    off = [0, nw, 2 * nw, 2 * nw + nr1, 2 * nw + nr1 + nr2]
+    res = []
+    for fused in (True, False):
+        sq = torch.rand(off[-1], generator=torch.Generator().manual_seed(8)).to(gpu)
+        gb_enc, gb_dec = torch.empty(h, dtype=dtype, device=gpu), torch.empty(K, dtype=dtype, device=gpu)
+        out = torch.full((4,), float("nan"), device=gpu)
+        if fused:
+            ctr = torch.zeros(1, dtype=torch.int32, device=gpu)
+            for _ in range(2):  # the counter is left at zero: a second launch works the same
+                ops.grad_tail_sums(gpc, gb_enc, sq[off[2]:off[3]], lpc, gb_dec, sq[off[3]:off[4]], sq, off, out, ctr,
+                                   zero_mask=zero_mask)
+            torch.cuda.synchronize()
+            assert int(ctr.item()) == 0
+        else:
+            ops.reduce_rows(gpc, R1, h, out_t=gb_enc, sq_part=sq[off[2]:off[3]])
+            ops.reduce_rows(lpc, R2, K, out_t=gb_dec, sq_part=sq[off[3]:off[4]])
+            ops.segment_sums(sq, off, out, zero_mask=zero_mask)
+        torch.cuda.synchronize()
+        res.append((gb_enc, gb_dec, sq, out))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    assert (res[0][3][3].item() == 0.0) == bool(zero_mask)
+
+
+# ----------------------------------------------------------------------------- BASELINE configs 4 / 5 shapes
+@pytest.mark.parametrize("B,n,d,h", [(8192, 2, 3584, 8192),     # config 4 per-GPU shard (2x3584->65536 / 8)
+                                     (4096, 4, 2304, 32768)])   # config 5: 4x2304->32768 on one GPU
+def test_baseline_config_shapes_spot_check(gpu, B, n, d, h):
+    """One fused fwd+bwd at the BASELINE config shapes (bf16): sampled rows / latents of every
+    GEMM output checked against the oracle formulas evaluated in fp64 on the GPU's own bf16
+    inputs of that GEMM (size-independent: no error compounding across kernels)."""
+    cfg = {"seed": 7, "dict_size": h, "d_in": d, "enc_dtype": "bf16", "dec_init_norm": 0.08, "device": str(gpu),
+           "batch_size": B}
+    cc = ca.CrossCoder(cfg, n_models=n)
+    g = torch.Generator(device=gpu).manual_seed(3)
+    raw = (torch.randn(B, n, d, generator=g, device=gpu) * 3).to(torch.bfloat16)
+    factor = torch.full((n,), 0.35, device=gpu).to(torch.bfloat16)
+    ws = cc._workspace(B)
+    a = cc.arena()
+    G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+    engine.forward(ws, a, raw, factor)
+    engine.backward(ws, a, G, l1_coeff=2.0)
+    torch.cuda.synchronize()
+    K = n * d
+    gi = torch.Generator().manual_seed(B + h)
+    rows = torch.randint(0, B, (24,), generator=gi)
+    lat = torch.randint(0, h, (12,), generator=gi)
+    D = lambda t: t.double().cpu()  # noqa: E731
+    x, We, Wd, be = D(ws.x), D(a.W_enc_hk), D(a.W_dec_hk), D(a.b_enc)
+    acts, grec, gpre = D(ws.acts), D(ws.g_recon), D(ws.g_pre)
+    tn = Wd.view(h, n, d).norm(dim=-1).sum(-1)
+    # G1: acts rows
+    pre = x[rows] @ We.t() + be
+    assert rel(acts[rows], pre.clamp_min(0)) < 1e-2
+    # G2 + loss (one pass): g_recon rows = bf16(2 (acts W_dec + b_dec - x) / B), split-K leftover columns
+    # included (crosscoder.py:82-89, 104-106)
+    recon = acts[rows] @ Wd + D(a.b_dec_flat)
+    assert rel(grec[rows], 2.0 * (recon - x[rows]) / B) < 8e-3
+    # G3: g_pre rows = (g_recon W_dec^T + l1c tn / B) * [acts > 0]
+    ref3 = (grec[rows] @ Wd.t() + 2.0 * tn / B) * (acts[rows] > 0)
+    assert rel(gpre[rows], ref3) < 1e-2
+    # G4: dW_dec latents = acts^T g_recon + l1c/B * colsum(acts) * W_dec / ||W_dec||
+    inv = 1.0 / Wd.view(h, n, d).norm(dim=-1)
+    l1t = (2.0 / B) * acts.sum(0)[lat, None, None] * Wd.view(h, n, d)[lat] * inv[lat, :, None]
+    ref4 = acts[:, lat].t() @ grec + l1t.reshape(len(lat), K)
+    assert rel(D(G.W_dec_hk)[lat], ref4) < 1e-2
+    # G5: dW_enc latents = g_pre^T x
+    assert rel(D(G.W_enc_hk)[lat], gpre[:, lat].t() @ x) < 1e-2
+    # bias gradients
+    assert rel(D(G.b_enc), gpre.sum(0)) < 1e-2
+    assert rel(D(G.b_dec_flat), grec.sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("enc_dtype,B,n,d,h", [("bf16", 1024, 2, 256, 2048), ("fp32", 96, 2, 40, 200),
+                                               ("bf16", 512, 4, 64, 384), ("fp32", 256, 2, 64, 1000)])
+def test_fused_tails_match_separate_launches(gpu, enc_dtype, B, n, d, h):
+    """The one-launch loss tail (l1 partials from the activation column sums + EV + loss scalars,
+    cc_loss_tail) and grad tail (bias-gradient sums + clip coefficient, cc_grad_tail) the step runs equal
+    the separate reduce_rows / loss_finalize / clip_finalize launches bit for bit, and leave their arrival
+    counters at zero; the mapped-host forms of both loss finalisers deliver the same scalars + sequence word."""
+    from crosscoder_amd import _hip
+
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype=enc_dtype,
+               device=str(gpu))
+    cc = ca.CrossCoder(cfg, n_models=n)
+    g = torch.Generator().manual_seed(B + h)
+    raw = (torch.randn(B, n, d, generator=g) * 3).to(gpu)
+    factor = torch.tensor([0.7, 1.3, 0.9, 1.1][:n]).to(cc.dtype).to(gpu)
+    ws = cc._workspace(B)
+    a = cc.arena()
+    G = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+    engine.forward(ws, a, raw, factor)          # loss tail
+    engine.backward(ws, a, G, 2.0, clip=1.0)    # grad tail
+    torch.cuda.synchronize()
+    assert not bool(ws.tail_ctr.any())
+    f32 = lambda t: torch.empty_like(t)  # noqa: E731
+    # loss side, separately
+    colsum, l1p = f32(ws.colsum_acts), f32(ws.l1_part)
+    ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=colsum, dot_w=ws.tn, dot_part=l1p)
+    # (x.mean(0) and sum_b acts: where the step carries them in the G1 / G2 prologues, reduce_rows' bits)
+    xm = f32(ws.x_mean)
+    ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], n * d, scale=1.0 / B, out_f32=xm)
+    ev, ev_a, ev_b, sc = f32(ws.ev), f32(ws.ev_a), f32(ws.ev_b), f32(ws.scalars)
+    rp = engine._row_part(ws)  # (the layout of the pass that wrote the row terms)
+    ops.loss_finalize(rp, l1p, ws.n_l1, ws.l0_part, ws.n_wave, ev, ev_a, ev_b, sc, B, n, d, ncb=ws.row_ncb)
+    host = _hip.MappedHostBuffer(16)
+    sc2 = f32(ws.scalars)
+    ops.loss_finalize(rp, l1p, ws.n_l1, ws.l0_part, ws.n_wave, f32(ev), f32(ev), f32(ev), sc2, B, n, d,
+                      host=host, seq=7, ncb=ws.row_ncb)
+    # the fused tail again, into mapped host memory (the Trainer's path)
+    host2 = _hip.MappedHostBuffer(16)
+    l1p2, sc3 = f32(l1p), f32(ws.scalars)
+    ops.loss_tail(ws.colsum_acts, ws.tn, l1p2, rp, ws.l0_part, ws.n_wave, f32(ev), f32(ev), f32(ev), sc3, B, n, d,
+                  ws.tail_ctr[0:1], host=host2, seq=9, ncb=ws.row_ncb)
+    # grad side, separately
+    sq = ws.sq.clone()
+    gbe, gbd = torch.empty_like(G.b_enc), torch.empty_like(G.b_dec_flat)
+    o = ws.sq_off
+    ops.reduce_rows(ws.gpre_colpart, ws.gpre_colpart.shape[0], h, out_t=gbe, sq_part=sq[o[2]:o[3]])
+    ops.reduce_rows(engine.loss_colpart(ws), ws.loss_col_rows, n * d, out_t=gbd, sq_part=sq[o[3]:o[4]])
+    clip = torch.empty(8, device=gpu)
+    ops.clip_finalize(sq, o, 1.0, cc.dtype == torch.bfloat16, clip)
+    torch.cuda.synchronize()
+    host.wait(8, 7)
+    host2.wait(8, 9)
+    assert not bool(ws.tail_ctr.any())
+    for x, y in ((colsum, ws.colsum_acts), (xm, ws.x_mean), (l1p, ws.l1_part), (ev, ws.ev), (ev_a, ws.ev_a),
+                 (ev_b, ws.ev_b),
+                 (sc[:6], ws.scalars[:6]), (sq, ws.sq), (gbe, G.b_enc), (gbd, G.b_dec_flat), (l1p2, l1p),
+                 (sc3[:6], sc[:6])):
+        assert torch.equal(x, y)
+    for hb in (host, host2):
+        assert torch.equal(torch.from_numpy(hb.f32[:6].copy()), sc[:6].cpu())
+    # where the step ran G4 + G5 + the grad tail as one launch (cc_wgrad_both_clip_t), its finaliser
+    # accumulates the same fp64 squared sums with 512 instead of 1024 threads
+    if ws.tr:
+        assert torch.allclose(clip[:6], ws.clip_out[:6], rtol=2 ** -8, atol=0)
+        # ... and its weight gradients / sq partials are the stand-alone dual GEMM's
+        G2 = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+        sq2 = torch.zeros_like(ws.sq)
+        o = ws.sq_off
+        ops.wgrad_both_t(ws.acts_t, ws.g_recon_t, a.W_dec_hk, ws.inv_norms, ws.colsum_acts, 2.0 / B, G2.W_dec_hk,
+                         sq2[o[1]:o[2]], ws.g_pre_t, ws.x_t, G2.W_enc_hk, sq2[o[0]:o[1]], n, d)
+        torch.cuda.synchronize()
+        assert torch.equal(G2.W_dec_hk, G.W_dec_hk) and torch.equal(G2.W_enc_hk, G.W_enc_hk)
+        assert torch.equal(sq2[o[0]:o[2]], ws.sq[o[0]:o[2]])
+        # the latent-sharded form (cc_wgrad_both_sums_t): the per-parameter squared sums of the segment
+        # finaliser, b_dec masked out as on ranks != 0
+        sums, ref_sums = torch.empty(8, device=gpu), torch.empty(8, device=gpu)
+        G3 = engine.Arena(a.h, a.n, a.d, a.data.dtype, gpu)
+        sq3 = torch.zeros_like(ws.sq)
+        ops.wgrad_both_sums_t(ws.acts_t, ws.g_recon_t, a.W_dec_hk, ws.inv_norms, ws.colsum_acts, 2.0 / B, G3.W_dec_hk,
+                              sq3[o[1]:o[2]], ws.g_pre_t, ws.x_t, G3.W_enc_hk, sq3[o[0]:o[1]], n, d, ws.gpre_colpart,
+                              G3.b_enc, sq3[o[2]:o[3]], engine.loss_colpart(ws), G3.b_dec_flat, sq3[o[3]:o[4]], sq3, o,
+                              sums, ws.tail_ctr[1:2], ws.tile_sum, zero_mask=0b1000)
+        ops.segment_sums(ws.sq, o, ref_sums, zero_mask=0b1000)
+        torch.cuda.synchronize()
+        assert torch.equal(sq3, ws.sq) and torch.equal(G3.b_enc, G.b_enc) and torch.equal(G3.b_dec_flat, G.b_dec_flat)
+        assert sums[3].item() == 0.0
+        assert torch.allclose(sums[:4], ref_sums[:4], rtol=1e-6, atol=0)
+        assert not bool(ws.tail_ctr.any())
+    else:
+        assert torch.equal(clip[:6], ws.clip_out[:6])
+    assert torch.equal(torch.from_numpy(host.f32[:6].copy()), sc2[:6].cpu())
+    assert torch.equal(sc2[:6], sc[:6])
+
+
+def test_two_get_losses_before_one_backward(gpu):
+    """Two get_losses() graphs alive at once (gradient accumulation, `get_losses(a).l2 +
+    get_losses(b).l2`): the second forward must not overwrite the activations the first graph's
+    backward needs.  Gradients = the sum of the oracle's gradients of both batches (fp32)."""
+    r = load("step_b64_n2_d32_h256_fp32")
+    cfg = dict(r["cfg"], device=str(gpu))
+    cc = make_cc(cfg, r["init"], gpu, 2)
+    g = torch.Generator().manual_seed(11)
+    xa, xb = (torch.randn(64, 2, 32, generator=g) * 2 for _ in range(2))
+    la, lb = cc.get_losses(xa.to(gpu)), cc.get_losses(xb.to(gpu))
+    (la.l2_loss + 2.0 * la.l1_loss + lb.l2_loss).backward()
+    P = {k: v.detach().clone().requires_grad_(True) for k, v in r["init"].items()}
+    oa, ob = O.get_losses(xa, P, torch.float32), O.get_losses(xb, P, torch.float32)
+    (oa["l2_loss"] + 2.0 * oa["l1_loss"] + ob["l2_loss"]).backward()
+    assert math.isclose(la.l2_loss.item(), oa["l2_loss"].item(), rel_tol=1e-5)
+    assert math.isclose(lb.l2_loss.item(), ob["l2_loss"].item(), rel_tol=1e-5)
+    for k in O.PARAM_ORDER:
+        assert rel(getattr(cc, k).grad.cpu(), P[k].grad) < 2e-5, k
+
+
+def test_param_access_orders_after_side_stream_adam(gpu):
+    """After Trainer.step() the decoder half of Adam may still run on the side stream, and its last rows are
+    deferred to the next reader (engine.DEC_SIDE_ROWS): reading the params through any public path
+    (attribute, parameters(), state_dict(), optimizer.state) first launches those rows on torch's current
+    stream and orders it after the side stream (the arena's pending work is consumed)."""
+    B, n, d, h = 512, 2, 128, 1024
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+               num_tokens=B * 20, device=str(gpu))
+    tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=2), crosscoder=ca.CrossCoder(cfg))
+    cc = tr.crosscoder
+    for access in (lambda: cc.W_dec, lambda: list(cc.parameters()), lambda: cc.state_dict(),
+                   lambda: tr.optimizer.state, lambda: cc.b_dec):
+        tr.step()
+        a = cc._arena
+        assert a.pending is not None or a.pending_rest is not None  # the decoder-half Adam of this step
+        access()
+        assert a.pending is None and a.pending_rest is None
+    # and what such a read sees is the finished update: the same bits after a full device sync
+    tr.step()
+    w = cc.W_dec.detach().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(w, cc.W_dec.detach())
+
+
+def test_sae_vis_export_matches_notebook_fold(gpu):
+    """Crosscoder_model_diff.ipynb:35752-35801: the encoder-only fold of the scaling factors into a copy,
+    exported as the state_dict the sae_vis fork loads: same keys / shapes / strides as the reference,
+    W_enc[m] scaled bit-identically to the notebook's torch ops, W_dec / biases unchanged, and the live
+    crosscoder untouched."""
+    r = load("step_b64_n2_d32_h256_bf16")
+    cfg = dict(r["cfg"], device=str(gpu))
+    cc = make_cc(cfg, r["init"], gpu, 2)
+    base, chat = 0.2758961493232058, 0.24422852496546169
+    sd, vcfg = ca.sae_vis_export(cc, base, chat)
+    assert vcfg == {"d_in": 32, "d_hidden": 256, "apply_b_dec_to_input": False}
+    ref = {k: v.clone() for k, v in r["init"].items()}
+    ref["W_enc"][0] = ref["W_enc"][0] * base
+    ref["W_enc"][1] = ref["W_enc"][1] * chat
+    assert list(sd) == list(ref)
+    for k in ref:
+        assert sd[k].dtype == torch.bfloat16 and sd[k].shape == ref[k].shape and sd[k].stride() == ref[k].stride()
+        assert torch.equal(sd[k], ref[k]), k
+    for k, v in r["init"].items():  # the source crosscoder is unchanged
+        assert torch.equal(cc.state_dict()[k].cpu(), v), k
+
+
+# ----------------------------------------------------------------------------- shapes off the 8-grid
+@pytest.mark.parametrize("enc_dtype,B,n,d,h", [("fp32", 64, 2, 37, 203), ("fp32", 48, 3, 20, 100),
+                                               ("bf16", 96, 2, 37, 203)])
+def test_odd_shapes_match_oracle(gpu, enc_dtype, B, n, d, h):
+    """dict_size / d_in that are not multiples of 8 (the reference takes any shape; the kernels move
+    16-byte rows): the crosscoder runs on zero-padded kernel dims and its reference-shaped parameters,
+    encode / decode, get_losses + autograd and three Trainer steps match the oracle (fp32: the
+    fixtures' tolerances; bf16: the reference's own bf16 envelope), and the padding stays zero."""
+    cfg = {"seed": 13, "batch_size": B, "buffer_mult": 128, "lr": 5e-5, "num_tokens": B * 4, "l1_coeff": 2,
+           "beta1": 0.9, "beta2": 0.999, "dict_size": h, "seq_len": 1024, "enc_dtype": enc_dtype,
+           "device": str(gpu), "dec_init_norm": 0.08, "d_in": d, "log_every": 100, "save_every": 30000}
+    dt = O.DTYPES[enc_dtype]
+    cc = ca.CrossCoder(cfg, n_models=n)
+    P = O.init_params(cfg, n_models=n)
+    for k in O.PARAM_ORDER:
+        assert torch.equal(getattr(cc, k).detach().cpu(), P[k]), k
+    g = torch.Generator().manual_seed(B + d)
+    x = (torch.randn(B, n, d, generator=g) * 2).to(dt)
+    fp32 = dt == torch.float32
+    # encode / decode / forward
+    acts = cc.encode(x.to(gpu)).cpu()
+    recon = cc.decode(acts.to(gpu)).cpu()
+    assert acts.shape == (B, h) and recon.shape == (B, n, d)
+    with torch.no_grad():
+        acts_ref = O.encode(x.double(), {k: v.double() for k, v in P.items()})
+        recon_ref = O.decode(acts.double(), {k: v.double() for k, v in P.items()})
+    assert rel(acts, acts_ref) < (2e-5 if fp32 else 8e-3)
+    assert rel(recon, recon_ref) < (2e-5 if fp32 else 8e-3)
+    # get_losses + backward vs the oracle (fp64 truth on the same inputs)
+    lo = cc.get_losses(x.to(gpu))
+    (lo.l2_loss + 2.0 * lo.l1_loss).backward()
+    torch.cuda.synchronize()
+    P_ref = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    lo_ref = O.get_losses(x, P_ref, dt)
+    (lo_ref["l2_loss"] + 2.0 * lo_ref["l1_loss"]).backward()
+    lo64, g64, _ = truth_fp64(x, P, 2.0)
+    for f in ("l2_loss", "l1_loss"):
+        ours, truth = getattr(lo, f).double().cpu(), lo64[f].detach()
+        if fp32:
+            assert rel(ours, truth) < 2e-5, f
+        else:
+            ok, e = envelope_ok(ours, lo_ref[f].detach(), truth)
+            assert ok, (f, e)
+    for k in O.PARAM_ORDER:
+        gk = getattr(cc, k).grad
+        assert gk is not None and gk.shape == P[k].shape, k
+        if fp32:
+            assert rel(gk, g64[k]) < 2e-5, k
+        else:
+            ok, e = envelope_ok(gk, P_ref[k].grad, g64[k], floor=2e-2 if k == "W_enc" else 2e-3)
+            assert ok, (k, e)
+    # three Trainer steps vs the oracle trainer on the same normalised batches
+    cc2 = ca.CrossCoder(cfg, n_models=n)
+    bufs = [(torch.randn(B, n, d, generator=g) * 3).to(dt) for _ in range(3)]
+    factors = [torch.tensor([0.7, 1.3, 0.9][:n]).to(dt) for _ in range(3)]
+    tr = ca.Trainer(cfg, buffer=_Replay(bufs, factors, gpu), crosscoder=cc2)
+    ref_tr = O.OracleTrainer(dict(cfg, device="cpu"), P, n_models=n)
+    for s in range(3):
+        dd = tr.step()
+        dr = ref_tr.step(O.buffer_next(bufs[s], factors[s]))
+        assert list(dd) == list(dr)
+        tol = 1e-5 if fp32 else 2e-3
+        for k in ("l2_loss", "l1_loss", "explained_variance"):
+            assert abs(dd[k] - dr[k]) <= tol * max(1.0, abs(dr[k])), (s, k, dd[k], dr[k])
+    tr.synchronize()
+    lr = cfg["lr"]
+    for k in O.PARAM_ORDER:
+        p, pr = getattr(cc2, k).detach().cpu().float(), ref_tr.P[k].detach().float()
+        diff = (p - pr).abs()
+        if fp32:  # (m / sqrt(v) of near-zero gradients amplifies fp32 summation-order differences; a
+            # Trainer whose Adam does not run is ~3 lr off)
+            assert diff.max().item() <= 0.05 * lr, (k, diff.max().item() / lr)
+        else:
+            assert (diff <= 2 * _bf16_ulp(pr) + 3 * lr).all(), (k, (diff / lr).max().item())
+    a = cc2.arena()
+    assert a.padded
+    Wenc = a.W_enc_hk.view(a.h, n, a.d)
+    assert float(Wenc[h:].abs().sum()) == 0.0 and float(Wenc[:, :, d:].abs().sum()) == 0.0
+    Wdec = a.W_dec_hk.view(a.h, n, a.d)
+    assert float(Wdec[h:].abs().sum()) == 0.0 and float(Wdec[:, :, d:].abs().sum()) == 0.0
+    assert float(a.b_enc[h:].abs().sum()) == 0.0 and float(a.b_dec_flat.view(n, a.d)[:, d:].abs().sum()) == 0.0
