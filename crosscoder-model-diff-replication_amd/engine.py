@@ -15,18 +15,22 @@ every GEMM streams 128-byte rows.
 
 Step (reference trainer.py:41-63 -> crosscoder.py:96-130 -> autograd -> clip -> Adam), single GPU:
   prep      x = dtype(buf * factor), x^T, column sums for x.mean(0)          buffer.py:124, crosscoder.py:99
-  G1        acts = relu(x W_enc + b_enc), acts^T, mask bits, colsum/l0 slabs crosscoder.py:69-80,128
-  reduce    x.mean(0), sum_b acts                                           crosscoder.py:112,126
-  (rest)    the decoder-half Adam's last rows of the previous step, then the side stream's norm
-            finaliser ||W_dec[h,m]||, sum over m                            crosscoder.py:123-125
-  G2+loss   acts W_dec + b_dec - x -> l2/tv row terms, g_recon = 2(r-x)/B,
-            g_recon^T, db_dec slab (no fp32 reconstruction)                 crosscoder.py:82-89,104-121
-  [side]    loss tail: l1 partials, EV, the loss scalars (+ host copy)      crosscoder.py:106-128
-  G3        g_pre = (g_recon W_dec^T + l1c tn/B) * (acts>0), stored as g_pre^T  autograd
+  G1        (prologue: x.mean(0)) acts = relu(x W_enc + b_enc), acts^T, mask bits, colsum/l0 slabs
+                                                                            crosscoder.py:69-80,112,128
+  (rest)    the decoder-half Adam's last rows of the previous step (+ their norm partials), then a wait
+            for the side stream's rows
+  G2+loss   (prologue: sum_b acts) acts W_dec + b_dec - x -> l2/tv row terms, g_recon = 2(r-x)/B,
+            g_recon^T, db_dec slab (no fp32 reconstruction); its split-K leftover launch also finalises
+            ||W_dec[h,m]||, their sum over m and inverses from the Adam's partials
+                                                                            crosscoder.py:82-89,104-126
+  G3        (prologue of its first workgroups: the loss tail -- l1 partials, EV, the loss scalars into
+            mapped host memory) g_pre = (g_recon W_dec^T + l1c tn/B) * (acts>0), stored as g_pre^T
+                                                                            crosscoder.py:106-128, autograd
   G4G5      dW_dec = acts^T g_recon + l1c/B colsum(acts) W_dec/||W_dec||,
             dW_enc = g_pre^T x, db_enc / db_dec, the clip coefficient        autograd, trainer.py:46
   adam      encoder half on this stream; the decoder half's first rows on the side stream beside the
             next step's G1 (with the next step's norm partials)              trainer.py:47
+G1, G3 and G4G5 are persistent launches that hand out their tiles per XCD from counters (DYNAMIC_TILES).
 """
 import contextlib
 
@@ -293,7 +297,7 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     """Forward + reconstruction-loss gradient.  P: params Arena.  x_in [B, n, d] any of
     fp32/bf16, factor [n] or None.  Leaves losses in ws.scalars / ws.ev*, g_recon ready
     (loss=False: stops at the fp32 reconstruction, for loss_rows / loss_finalize by slices;
-    finalize=False: stops after the loss rows, for loss_finalize_beside).  Where the fused entry
+    finalize=False: stops after the loss rows, for loss_finalize_with_g3 / loss_finalize_beside).  Where the fused entry
     serves the shape, G2 and the loss rows are one pass (decode_loss_t; no fp32 reconstruction)."""
     B, n, d, h, K = ws.B, ws.n, ws.d, ws.h, ws.K
     ws.next_slot()
