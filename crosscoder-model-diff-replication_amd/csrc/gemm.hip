@@ -69,6 +69,7 @@ struct GemmArgs {
   uint32_t* mask_bits;  // ping-pong EPI_ENC (out) / EPI_DACTS FAST (in): the activation mask, 1 bit per output
                         // in accumulator order: [tile tm*nbn + tn][thread][4] u32, bit 4(4i+j)+e of fragment (i,j)
   uint32_t* tile_ctr;   // persistent ping-pong launches: 8 per-XCD tile counters (dynamic order), NULL: static
+  uint32_t* wave_sync;  // probe only: 8 zeroed per-XCD arrival words (TileLoop::wave_wait), NULL: off
   RedSeg pre;           // a column reduction the launch runs before its tiles (cc_colsum_job), pre_blocks > 0
   int pre_blocks;
   LossTailArgs tail;    // the forward's loss tail the launch runs before its tiles (cc_loss_tail_job), tail_items > 0
@@ -595,7 +596,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmAr
   const int nb0 = a0.nbm * a0.nbn;
   float* wsum_lds = (float*)(smem + PP_SLOT + 64);  // (beside the claim word: free until the next prologue barrier)
   const int wave = threadIdx.x >> 6;
-  for (TileLoop L(2 * nb0, a0.tile_ctr); L.more();) {
+  for (TileLoop L(2 * nb0, a0.tile_ctr, a0.wave_sync); L.more();) {
     const int t = L.begin();
     const int tid = pp_opaque_tid();
     float w;
@@ -652,6 +653,18 @@ static int g_pp_mask = 7, g_pp_fast = 1, g_dec_one_launch = 1;
 CC_DEBUG_API void cc_debug_set_pp_mask(int mask) { g_pp_mask = mask; }
 CC_DEBUG_API void cc_debug_set_pp_fast(int on) { g_pp_fast = on; }
 CC_DEBUG_API void cc_debug_set_dec_one_launch(int on) { g_dec_one_launch = on; }
+// G4G5 (cc_wgrad_both_t / the _clip_t, _sums_t forms) in the static order with each XCD's waves of tiles
+// started together (TileLoop::wave_wait): the L2 panel-reuse probe of VERDICT r03 item 4
+static int g_wave_sync = 0;
+CC_DEBUG_API void cc_debug_set_wave_sync(int on) { g_wave_sync = on; }
+static void debug_wave_sync(GemmArgs& a, hipStream_t st) {
+  static uint32_t* words = nullptr;
+  if (!g_wave_sync) return;
+  if (!words && hipMalloc((void**)&words, 64) != hipSuccess) return;
+  if (hipMemsetAsync(words, 0, 32, st) != hipSuccess) return;
+  a.wave_sync = words;
+  a.tile_ctr = nullptr;
+}
 // Test / probe kernel: `blocks` workgroups of 512 threads that each hold `lds_bytes` of LDS and spin for `ns`
 // nanoseconds of the 100 MHz wall clock (s_sleep between reads) -- a stand-in for another stream's kernel that
 // holds CUs (a delayed producer, or RCCL's collective kernel beside a GEMM).  Every wave exits on the clock.
@@ -1340,6 +1353,9 @@ int cc_wgrad_both_t(const void* actsT, const void* g_reconT, const void* W_dec, 
   }
   a0.nbm = a1.nbm = (a0.M + BM - 1) / BM;
   a0.nbn = a1.nbn = (a0.N + 255) / 256;
+#ifdef CC_DEBUG_HOOKS
+  debug_wave_sync(a0, st);
+#endif
   hipLaunchKernelGGL((gemm_pp_dual_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(pp_grid(2 * a0.nbm * a0.nbn)), dim3(NTHR),
                      0, st, a0, a1);
   CC_LAUNCH_CHECK();
@@ -1394,6 +1410,9 @@ static int wgrad_both_tail(const void* actsT, const void* g_reconT, const void* 
   tl.counter = counter;
   tl.tile_sum = tile_sum;
   a0.tile_ctr = tile_ctr;
+#ifdef CC_DEBUG_HOOKS
+  debug_wave_sync(a0, (hipStream_t)stream);
+#endif
   const int grid = pp_grid(2 * a0.nbm * a0.nbn);
   hipLaunchKernelGGL((gemm_pp_dual_tail_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(grid), dim3(NTHR), 0,
                      (hipStream_t)stream, a0, a1, tl);

@@ -454,9 +454,10 @@ CC_DEV int pp_opaque_tid() {
 constexpr int PP_SLOT = 2 * 256 * 128;  // LDS byte offset of the tile-claim broadcast word (see above)
 struct TileLoop {
   unsigned* ctr;
+  unsigned* wsync;  // probe only (cc_debug_set_wave_sync): static order, the XCD's waves of tiles start together
   int x, nwx, ntx, i;
   unsigned nxt;
-  CC_DEV TileLoop(int nt, unsigned* c) : ctr(c), nxt(0) {
+  CC_DEV TileLoop(int nt, unsigned* c, unsigned* ws = nullptr) : ctr(c), wsync(ws), nxt(0) {
     const int G = gridDim.x;
     x = blockIdx.x & 7;
     nwx = (G >> 3) + ((G & 7) > x);
@@ -469,9 +470,25 @@ struct TileLoop {
     if (ctr && threadIdx.x == 0) nxt = atomicInc(ctr + x, (unsigned)(ntx - 1));
     return x + 8 * i;
   }
+  // Probe of L2 panel reuse: every workgroup of the XCD finishes its tile of wave k before
+  // any starts wave k + 1, so the XCD's concurrent tiles stream their shared A / B panels at the same K position.
+  // Arrivals on the XCD's word (zeroed before the launch); the wait is bounded (~2 ms) so every wave exits.
+  // The caller's barrier follows.
+  CC_DEV void wave_wait() {
+    if (threadIdx.x != 0) return;
+    const unsigned k = (unsigned)(i / nwx);
+    __hip_atomic_fetch_add(wsync + x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (i + nwx >= ntx) return;
+    const unsigned target = min((k + 1) * (unsigned)nwx, (unsigned)ntx);
+    for (int it = 0; it < (1 << 16); ++it) {
+      if (__hip_atomic_load(wsync + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
   // after the tile and pp_tile_boundary()
   CC_DEV void advance(char* smem) {
     if (!ctr) {
+      if (wsync) wave_wait();
       i += nwx;
       return;
     }
@@ -551,7 +568,7 @@ template <bool AKC, bool BKC, int EPI0, int EPI1>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_kernel(const GemmArgs a0, const GemmArgs a1) {
   __shared__ __attribute__((aligned(16))) char smem[EPI0 == EPI_WGDEC || EPI1 == EPI_WGDEC ? PP_LDS_W : PP_LDS];
   const int nb0 = a0.nbm * a0.nbn;
-  for (TileLoop L(2 * nb0, a0.tile_ctr); L.more();) {
+  for (TileLoop L(2 * nb0, a0.tile_ctr, a0.wave_sync); L.more();) {
     const int t = L.begin();
     const int tid = pp_opaque_tid();
     if (t < nb0) pp_tile<AKC, BKC, EPI0>(a0, smem, t, tid);
