@@ -30,6 +30,17 @@
 
 #include <type_traits>
 
+// experiment switch (default 0): bit 0 = s_setprio 1 around each MFMA cluster; bit 1 = static priority 1 for
+// the second wave group (waves 4-7) from kernel start
+#ifndef CC_PP_PRIO
+#define CC_PP_PRIO 0
+#endif
+CC_DEV void pp_static_prio() {
+#if CC_PP_PRIO & 2
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
+}
+
 CC_DEV int pp_h(int k) { return ((k >> 1) & 1) | ((k >> 2) & 2); }
 
 // Per-lane source offset (bytes, step k0 = 0) of DMA ci (0..31) of a 256 x 64 operand tile, or
@@ -211,6 +222,7 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
   constexpr int TILE = 256 * 128;  // one operand's K-step image
   constexpr int BUF = 2 * TILE;
 
+  pp_static_prio();
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -381,11 +393,17 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
+#if CC_PP_PRIO & 1
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
         for (int j = 0; j < WG::TN; ++j)
           acc[ib + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii], acc[ib + ii][j], 0, 0, 0);
+#if CC_PP_PRIO & 1
+      __builtin_amdgcn_s_setprio(0);
+#endif
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
     }
