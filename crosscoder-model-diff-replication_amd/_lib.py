@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libcrosscoder_hip.so")
 DEBUG_LIB_PATH = os.path.join(_HERE, "libcrosscoder_hip_dbg.so")
 DEFAULT_PP_MASK = 7  # the ping-pong layouts both libraries default to (csrc/gemm.hip: g_pp_mask)
 DEBUG_SETTERS = ("cc_debug_set_pp_mask", "cc_debug_set_pp_fast", "cc_debug_set_dec_one_launch",
-                 "cc_debug_set_wave_sync")
+                 "cc_debug_set_wave_sync", "cc_debug_set_epi_store")
 
 CC_BF16 = 1
 CC_F32 = 2
@@ -177,6 +177,7 @@ def debug_library():
         dbg.cc_debug_set_pp_fast(1)
         dbg.cc_debug_set_dec_one_launch(1)
         dbg.cc_debug_set_wave_sync(0)
+        dbg.cc_debug_set_epi_store(1)
         _lib = prev
 
 

@@ -656,6 +656,12 @@ CC_DEBUG_API void cc_debug_set_dec_one_launch(int on) { g_dec_one_launch = on; }
 // G4G5 (cc_wgrad_both_t / the _clip_t, _sums_t forms) in the static order with each XCD's waves of tiles
 // started together (TileLoop::wave_wait): the L2 panel-reuse probe of VERDICT r03 item 4
 static int g_wave_sync = 0;
+// ping-pong GEMMs without their output tiles' HBM stores (the epilogue still runs into LDS): the store-exposure probe
+static int g_epi_store = 1;
+CC_DEBUG_API void cc_debug_set_epi_store(int on) { g_epi_store = on; }
+static void debug_epi_store(GemmArgs& a) {
+  if (!g_epi_store) a.out = a.out_t = nullptr;
+}
 CC_DEBUG_API void cc_debug_set_wave_sync(int on) { g_wave_sync = on; }
 static void debug_wave_sync(GemmArgs& a, hipStream_t st) {
   static uint32_t* words = nullptr;
@@ -766,6 +772,9 @@ static int pp_grid(int64_t tiles) {
 
 template <bool AKC, bool BKC, int EPI>
 static int launch_pp(GemmArgs a, hipStream_t st) {
+#ifdef CC_DEBUG_HOOKS
+  debug_epi_store(a);
+#endif
   a.nbm = (a.M + BM - 1) / BM;
   a.nbn = (a.N + 255) / 256;
   if constexpr (EPI == EPI_ENC || EPI == EPI_DACTS) {
@@ -1355,6 +1364,8 @@ int cc_wgrad_both_t(const void* actsT, const void* g_reconT, const void* W_dec, 
   a0.nbn = a1.nbn = (a0.N + 255) / 256;
 #ifdef CC_DEBUG_HOOKS
   debug_wave_sync(a0, st);
+  debug_epi_store(a0);
+  debug_epi_store(a1);
 #endif
   hipLaunchKernelGGL((gemm_pp_dual_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(pp_grid(2 * a0.nbm * a0.nbn)), dim3(NTHR),
                      0, st, a0, a1);
@@ -1412,6 +1423,8 @@ static int wgrad_both_tail(const void* actsT, const void* g_reconT, const void* 
   a0.tile_ctr = tile_ctr;
 #ifdef CC_DEBUG_HOOKS
   debug_wave_sync(a0, (hipStream_t)stream);
+  debug_epi_store(a0);
+  debug_epi_store(a1);
 #endif
   const int grid = pp_grid(2 * a0.nbm * a0.nbn);
   hipLaunchKernelGGL((gemm_pp_dual_tail_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(grid), dim3(NTHR), 0,

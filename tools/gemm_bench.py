@@ -27,11 +27,14 @@ def load(path):
 
 
 def main():
-    # each argument: path/to/lib.so[@pp_mask]  (the mask selects the ping-pong loop per layout)
+    # each argument: path/to/lib.so[@pp_mask][#nostore]  (the mask selects the ping-pong loop per layout; #nostore:
+    # debug build, the ping-pong epilogues skip their output tiles' HBM stores)
     libs = []
     for arg in sys.argv[1:]:
-        path, _, mask = arg.partition("@")
-        libs.append((os.path.basename(path) + (f"@{mask}" if mask else ""), load(path), int(mask) if mask else None))
+        spec, _, flag = arg.partition("#")
+        path, _, mask = spec.partition("@")
+        libs.append((os.path.basename(path) + (f"@{mask}" if mask else "") + (f"#{flag}" if flag else ""), load(path),
+                     (int(mask) if mask else None, flag == "nostore")))
     dev = torch.device("cuda:0")
     bf = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
@@ -96,9 +99,11 @@ def main():
     flop = 2.0 * B * K * h
     res = {}
     for rnd in range(5):
-        for path, L, mask in libs:
+        for path, L, (mask, nostore) in libs:
             if mask is not None:
                 L.cc_debug_set_pp_mask(mask)
+            if hasattr(L, "cc_debug_set_epi_store"):
+                L.cc_debug_set_epi_store(0 if nostore else 1)
             only = os.environ.get("CC_GEMM_ONLY")
             for name, fn in calls(L).items():
                 if only and name not in only.split(","):
