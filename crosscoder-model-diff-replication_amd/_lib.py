@@ -156,6 +156,8 @@ def load_debug():
             fn.argtypes = [ctypes.c_int]
         lib.cc_debug_spin.restype = _i
         lib.cc_debug_spin.argtypes = [_i64, _i64, _i64, _p]
+        lib.cc_debug_set_stamps.restype = None
+        lib.cc_debug_set_stamps.argtypes = [_p]
         lib.cc_debug_spin_ev.restype = _i
         lib.cc_debug_spin_ev.argtypes = [_i64, _i64, _p, _p]
         _debug = lib

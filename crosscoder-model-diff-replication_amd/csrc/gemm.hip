@@ -70,6 +70,7 @@ struct GemmArgs {
                         // in accumulator order: [tile tm*nbn + tn][thread][4] u32, bit 4(4i+j)+e of fragment (i,j)
   uint32_t* tile_ctr;   // persistent ping-pong launches: 8 per-XCD tile counters (dynamic order), NULL: static
   uint32_t* wave_sync;  // probe only: 8 zeroed per-XCD arrival words (TileLoop::wave_wait), NULL: off
+  uint64_t* stamps;     // probe build only (-DCC_PP_STAMPS): [tile][8] clock stamps of a ping-pong tile (pp_tile)
   RedSeg pre;           // a column reduction the launch runs before its tiles (cc_colsum_job), pre_blocks > 0
   int pre_blocks;
   LossTailArgs tail;    // the forward's loss tail the launch runs before its tiles (cc_loss_tail_job), tail_items > 0
@@ -656,11 +657,15 @@ CC_DEBUG_API void cc_debug_set_dec_one_launch(int on) { g_dec_one_launch = on; }
 // G4G5 (cc_wgrad_both_t / the _clip_t, _sums_t forms) in the static order with each XCD's waves of tiles
 // started together (TileLoop::wave_wait): the L2 panel-reuse probe of VERDICT r03 item 4
 static int g_wave_sync = 0;
+// per-tile clock stamps of the ping-pong GEMMs (probe build -DCC_PP_STAMPS; NULL: off): pp_tile's anatomy probe
+static uint64_t* g_stamps = nullptr;
+CC_DEBUG_API void cc_debug_set_stamps(void* buf) { g_stamps = (uint64_t*)buf; }
 // ping-pong GEMMs without their output tiles' HBM stores (the epilogue still runs into LDS): the store-exposure probe
 static int g_epi_store = 1;
 CC_DEBUG_API void cc_debug_set_epi_store(int on) { g_epi_store = on; }
-static void debug_epi_store(GemmArgs& a) {
+static void debug_epi_store(GemmArgs& a, int64_t stamp_tile0 = 0) {
   if (!g_epi_store) a.out = a.out_t = nullptr;
+  if (g_stamps) a.stamps = g_stamps + stamp_tile0 * 8;
 }
 CC_DEBUG_API void cc_debug_set_wave_sync(int on) { g_wave_sync = on; }
 static void debug_wave_sync(GemmArgs& a, hipStream_t st) {
@@ -1365,7 +1370,7 @@ int cc_wgrad_both_t(const void* actsT, const void* g_reconT, const void* W_dec, 
 #ifdef CC_DEBUG_HOOKS
   debug_wave_sync(a0, st);
   debug_epi_store(a0);
-  debug_epi_store(a1);
+  debug_epi_store(a1, (int64_t)a0.nbm * a0.nbn);
 #endif
   hipLaunchKernelGGL((gemm_pp_dual_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(pp_grid(2 * a0.nbm * a0.nbn)), dim3(NTHR),
                      0, st, a0, a1);
@@ -1424,7 +1429,7 @@ static int wgrad_both_tail(const void* actsT, const void* g_reconT, const void* 
 #ifdef CC_DEBUG_HOOKS
   debug_wave_sync(a0, (hipStream_t)stream);
   debug_epi_store(a0);
-  debug_epi_store(a1);
+  debug_epi_store(a1, (int64_t)a0.nbm * a0.nbn);
 #endif
   const int grid = pp_grid(2 * a0.nbm * a0.nbn);
   hipLaunchKernelGGL((gemm_pp_dual_tail_kernel<true, true, EPI_WGDEC, EPI_WGENC>), dim3(grid), dim3(NTHR), 0,

@@ -35,6 +35,25 @@
 #ifndef CC_PP_PRIO
 #define CC_PP_PRIO 0
 #endif
+// Tile anatomy probe (build with -DCC_PP_STAMPS; GemmArgs::stamps set by the debug build's cc_debug_set_stamps):
+// thread 0 keeps s_memtime at tile entry (0), after the prologue's barrier (1), after the K loop (2), after the
+// drain before the epilogue (3) and after the epilogue's stores are issued (4), plus the 100 MHz wall clock at
+// entry (5) and end (6), and writes them with one store per value after the epilogue (no store inside the
+// K loop: it would sit in the loop's counted vmcnt waits).
+#ifdef CC_PP_STAMPS
+#define PP_STAMP_DECL uint64_t pp_st[7] = {(uint64_t)__builtin_amdgcn_s_memtime(), 0, 0, 0, 0, (uint64_t)wall_clock64(), 0}
+#define PP_STAMP(k) pp_st[k] = __builtin_amdgcn_s_memtime()
+#define PP_STAMP_WRITE(args, bid)                                                         \
+  do {                                                                                    \
+    pp_st[6] = wall_clock64();                                                            \
+    if ((args).stamps && threadIdx.x == 0)                                                \
+      for (int k_ = 0; k_ < 7; ++k_) (args).stamps[(int64_t)(bid) * 8 + k_] = pp_st[k_]; \
+  } while (0)
+#else
+#define PP_STAMP_DECL
+#define PP_STAMP(k)
+#define PP_STAMP_WRITE(args, bid)
+#endif
 CC_DEV void pp_static_prio() {
 #if CC_PP_PRIO & 2
   if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
@@ -222,6 +241,7 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
   constexpr int TILE = 256 * 128;  // one operand's K-step image
   constexpr int BUF = 2 * TILE;
 
+  PP_STAMP_DECL;
   pp_static_prio();
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -360,6 +380,7 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
   wait_vmcnt<6>();
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs half a phase behind
+  PP_STAMP(1);
 
   bf16x8 bfr[WG::TN][2];
   auto kstep = [&](auto tail, int t) {
@@ -416,6 +437,7 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
     for (; t < nk - 2; ++t) kstep(std::integral_constant<int, 0>{}, t);
   for (; t < nk; ++t) kstep(std::integral_constant<int, 1>{}, t);  // last two steps: DMAs past the end prefetch W_dec
   if (wr == 0) __builtin_amdgcn_s_barrier();
+  PP_STAMP(2);
   // the epilogue's column vectors fly while the last (zero-fill) DMAs drain
   const FragGeom<256> fg(args, m0, n0, wr, wc, lane);
   EpiCols<CC_BF16, 256> evec;
@@ -433,8 +455,12 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
     gemm_epilogue<CC_BF16, EPI, 256>(args, acc, tm, m0, n0, wr, wc, lane, bid * 8 + wave);
   } else {  // (the host routes N % 8 != 0 to gemm_kernel)
     __builtin_amdgcn_s_barrier();  // every wave's zero-fill DMAs landed: the LDS is free
-    return pp_epilogue_lds<EPI, FAST>(args, acc, smem, qb, pf, tm, m0, n0, wr, wc, lane, wave, bid * 8 + wave, fg,
-                                      evec);
+    PP_STAMP(3);
+    const float wsum = pp_epilogue_lds<EPI, FAST>(args, acc, smem, qb, pf, tm, m0, n0, wr, wc, lane, wave,
+                                                  bid * 8 + wave, fg, evec);
+    PP_STAMP(4);
+    PP_STAMP_WRITE(args, bid);
+    return wsum;
   }
   return 0.f;
 }
