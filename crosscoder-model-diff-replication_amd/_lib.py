@@ -93,8 +93,8 @@ SIGNATURES = {
                                  _i64, _p]),
     "cc_decode_loss_ncb": (_i64, [_i64, _i64, _i64, _i64, _i]),
     "cc_decode_loss_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i, _p]),
-    "cc_decode_loss": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64,
-                            _i, _p]),
+    "cc_decode_loss": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _p,
+                            _i64, _i64, _i64, _i64, _i, _p]),
     "cc_transposed_ok": (_i, [_i64, _i64, _i64, _i]),
     "cc_encode_fwd_t": (_i, [_p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_mask_bits_words": (_i64, [_i64, _i64]),
@@ -111,7 +111,8 @@ SIGNATURES = {
     "cc_adam_step": (_i, [_p, _p, _p, _p, _i64, _p, _d, _d, _d, _d, _i64, _i64, _i, _p]),
     "cc_adam_step_clip": (_i, [_p, _p, _p, _p, _i64, _p, _i, _f, _i, _p, _d, _d, _d, _d, _i64, _i64, _i, _p]),
     "cc_adam_dec_norms": (_i, [_p, _p, _p, _p, _i64, _p, _p, _i, _f, _i, _d, _d, _d, _d, _i64, _i64, _p, _i64, _i64, _i,
-                               _p]),
+                               _p, _p]),
+    "cc_adam_capped_blocks": (_i64, [_i64, _i64]),
 }
 
 _lib = None

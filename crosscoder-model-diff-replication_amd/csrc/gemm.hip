@@ -71,6 +71,12 @@ struct GemmArgs {
   uint32_t* tile_ctr;   // persistent ping-pong launches: 8 per-XCD tile counters (dynamic order), NULL: static
   uint32_t* wave_sync;  // probe only: 8 zeroed per-XCD arrival words (TileLoop::wave_wait), NULL: off
   uint64_t* stamps;     // probe build only (-DCC_PP_STAMPS): [tile][8] clock stamps of a ping-pong tile (pp_tile)
+  // wait in the kernel for a producer on another stream (cc_decode_loss: the side-stream Adam's done counter,
+  // AdamArgs::done_ctr) before the first operand load: until *wait_ctr - wait_target >= 0 (mod 2^32); a wait
+  // past ~1 s gives up, sets *wait_err (host-visible) and runs on (NULL wait_ctr: none)
+  const uint32_t* wait_ctr;
+  uint32_t wait_target;
+  uint32_t* wait_err;
   RedSeg pre;           // a column reduction the launch runs before its tiles (cc_colsum_job), pre_blocks > 0
   int pre_blocks;
   LossTailArgs tail;    // the forward's loss tail the launch runs before its tiles (cc_loss_tail_job), tail_items > 0
@@ -1178,7 +1184,8 @@ template <bool BKC>
 static int decode_loss(const void* acts, const void* W_dec, const void* b_dec, const void* x, const float* x_mean,
                        float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
                        int64_t ws_floats, const float* norm_part, float* norms, float* tn, float* inv_norms,
-                       const cc_colsum_job* pre, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, hipStream_t st) {
+                       const cc_colsum_job* pre, const uint32_t* wait_ctr, uint32_t wait_target, uint32_t* wait_err,
+                       int64_t B, int64_t h, int64_t n, int64_t d, int dtype, hipStream_t st) {
   if (!acts || !W_dec || !b_dec || !x || !x_mean || !g_recon || !row_part || !col_part) return CC_ERR_NULL;
   if (BKC && !g_recon_t) return CC_ERR_NULL;
   if (!cc_decode_loss_ncb(B, h, n, d, dtype) || !use_pp(n * d, true, BKC, dtype)) return CC_ERR_SHAPE;
@@ -1188,10 +1195,6 @@ static int decode_loss(const void* acts, const void* W_dec, const void* b_dec, c
   const int64_t ldb = BKC ? h : K;
   DecPlan p;
   const bool split = dec_plan(B, h, K, dtype, p);
-  if (norm_part && !split) {  // (no leftover launch to carry it: the stand-alone finaliser first)
-    const int rc = cc_dec_norms_finalize(norm_part, h, n, d, norms, tn, inv_norms, st);
-    if (rc) return rc;
-  }
   GemmArgs a = {};
   a.A = acts; a.lda = h; a.B = W_dec; a.ldb = ldb;
   a.M = (int)B; a.N = split ? p.nbn_main * 256 : (int)K; a.K = (int)h;
@@ -1201,6 +1204,7 @@ static int decode_loss(const void* acts, const void* W_dec, const void* b_dec, c
   int rc = check_gemm(a, dtype, true, BKC);
   if (rc) return rc;
   if ((rc = set_pre(a, pre))) return rc;
+  a.wait_ctr = wait_ctr; a.wait_target = wait_target; a.wait_err = wait_err;
   a.nbm = (a.M + BM - 1) / BM;
   a.nbn = (a.N + 255) / 256;
   const bool fast = B % BM == 0 && a.N % 256 == 0;
@@ -1209,7 +1213,9 @@ static int decode_loss(const void* acts, const void* W_dec, const void* b_dec, c
     if (fast) hipLaunchKernelGGL((gemm_pp_kernel<true, BKC, EPI_DLOSS, true>), grid, dim3(NTHR), 0, st, a);
     else hipLaunchKernelGGL((gemm_pp_kernel<true, BKC, EPI_DLOSS>), grid, dim3(NTHR), 0, st, a);
     CC_LAUNCH_CHECK();
-    return CC_OK;
+    // (no leftover launch to carry it: the stand-alone finaliser after the GEMM, which reads no norms -- and,
+    // with wait_ctr, after the GEMM's wait for the partials' producer)
+    return norm_part ? cc_dec_norms_finalize(norm_part, h, n, d, norms, tn, inv_norms, st) : CC_OK;
   }
   if (!ws) return CC_ERR_NULL;
   const int64_t split_stride = split_stride_of(B, p);
@@ -1219,6 +1225,7 @@ static int decode_loss(const void* acts, const void* W_dec, const void* b_dec, c
   t.A = acts; t.lda = h; t.B = (const bf16_t*)W_dec + (int64_t)p.nbn_main * 256 * (BKC ? h : 1); t.ldb = ldb;
   t.M = (int)B; t.N = p.tail_cols; t.K = (int)h;
   t.out = ws; t.ldo = p.tail_cols;
+  t.wait_ctr = wait_ctr; t.wait_target = wait_target; t.wait_err = wait_err;
   t.nbm = (t.M + BM - 1) / BM;
   t.nbn = (t.N + 255) / 256;
   const dim3 grid(a.nbm * a.nbn + p.nsplit * t.nbm * t.nbn);
@@ -1255,16 +1262,18 @@ int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, c
                      float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
                      int64_t ws_floats, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
   return decode_loss<true>(acts, W_dec_t, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t, row_part, col_part, ws,
-                           ws_floats, nullptr, nullptr, nullptr, nullptr, nullptr, B, h, n, d, dtype,
-                           (hipStream_t)stream);
+                           ws_floats, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, B, h, n, d,
+                           dtype, (hipStream_t)stream);
 }
 
 int cc_decode_loss(const void* acts, const void* W_dec, const void* b_dec, const void* x, const float* x_mean,
                    float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
                    int64_t ws_floats, const float* norm_part, float* norms, float* tn, float* inv_norms,
-                   const cc_colsum_job* pre, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
+                   const cc_colsum_job* pre, const uint32_t* wait_ctr, uint32_t wait_target, uint32_t* wait_err,
+                   int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
   return decode_loss<false>(acts, W_dec, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t, row_part, col_part, ws,
-                            ws_floats, norm_part, norms, tn, inv_norms, pre, B, h, n, d, dtype, (hipStream_t)stream);
+                            ws_floats, norm_part, norms, tn, inv_norms, pre, wait_ctr, wait_target, wait_err, B, h, n,
+                            d, dtype, (hipStream_t)stream);
 }
 
 int cc_dacts_bwd(const void* g_recon, const void* W_dec, const void* acts, const float* tn, float l1_scale,

@@ -543,6 +543,24 @@ struct TileLoop {
   }
 };
 
+// GemmArgs::wait_ctr: thread 0 polls the producer's counter (s_sleep between reads), then one agent-scope acquire
+// (drops this XCD's stale L2 lines of the producer's output) and the barrier.  Bounded: every wave exits.
+CC_DEV void pp_wait_ready(const GemmArgs& a) {
+  if (!a.wait_ctr) return;
+  if (threadIdx.x == 0) {
+    int it = 0;
+    while ((int)(__hip_atomic_load(a.wait_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.wait_target) < 0) {
+      if (++it > (1 << 22)) {  // (~1 s)
+        if (a.wait_err) __hip_atomic_store(a.wait_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
 // The launch's prologue reduction (GemmArgs::pre: reduce_rows' two phases, the same bits as cc_reduce_rows):
 // 256-thread group g of workgroup b reduces column blocks 2b + g, 2b + g + 2 * grid, ... before b's first tile.
 // A few workgroups start their tiles ~2 us late (the dynamic tile order evens that out); the step saves a launch.
@@ -598,6 +616,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(16))) char smem[EPI == EPI_WGDEC ? PP_LDS_W : PP_LDS];
   pp_prologue_reduce(args, smem, gridDim.x);
   pp_prologue_loss_tail(args, smem);
+  pp_wait_ready(args);
   for (TileLoop L(args.nbm * args.nbn, args.tile_ctr); L.more();) {
     pp_tile<AKC, BKC, EPI, FAST>(args, smem, L.begin(), pp_opaque_tid());
     pp_tile_boundary();
@@ -634,9 +653,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_main_splitk_kernel(const Gemm
   const int nb0 = a0.nbm * a0.nbn;
   if ((int)blockIdx.x < nb0) {
     pp_prologue_reduce(a0, smem, nb0);
+    pp_wait_ready(a0);
     pp_tile<AKC, BKC, EPI, FAST>(a0, smem, blockIdx.x);
     return;
   }
+  pp_wait_ready(t);
   const int b = blockIdx.x - nb0;
   const int s = b / (t.nbm * t.nbn);
   const int tb = b - s * t.nbm * t.nbn;
@@ -659,6 +680,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_splitk_kernel(const GemmArgs 
   // config 2, vs 80-134 us with each split pinned to one XCD: s = b % 8)
   const int s = blockIdx.x / (args.nbm * args.nbn);
   const int tb = blockIdx.x - s * args.nbm * args.nbn;
+  pp_wait_ready(args);
   GemmArgs a = args;
   a.k_step0 = s * steps_per;
   a.k_steps = nk_total - a.k_step0 < steps_per ? nk_total - a.k_step0 : steps_per;

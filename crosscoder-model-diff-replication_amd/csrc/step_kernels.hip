@@ -371,7 +371,21 @@ struct AdamArgs {
   // (adam_kernel only; nullptr: none)
   float* norm_part;
   int norm_rows, norm_ld;
+  // the capped grid-stride forms: each workgroup, when its stores are done, releases them (agent scope) and adds
+  // 1 here -- a reader launched on another stream (G2, cc_decode_loss's wait_ctr) waits for the count in its
+  // kernel instead of for an event (nullptr: none)
+  unsigned* done_ctr;
 };
+// Every thread of the workgroup: its stores drained, the barrier, one agent-scope release (writes the XCD's L2
+// back), then the arrival count.
+CC_DEV void adam_signal_done(unsigned* ctr) {
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 // The step's clip coefficient: read (coef), formed from squared sums (clip_sums), or 1
 CC_DEV float adam_coef(const AdamArgs& a) {
   if (a.clip_sums) {
@@ -519,6 +533,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
       }
     }
   }
+  if (a.done_ctr) adam_signal_done(a.done_ctr);
 }
 
 // The capped-grid (side-stream) bf16 Adam with the next chunk's loads in flight during this chunk's math.
@@ -536,9 +551,8 @@ __global__ __launch_bounds__(256) void adam_pipe_kernel(const AdamArgs a) {
   const float coef = adam_coef(a);
   const int64_t stride = (int64_t)gridDim.x * 256 * 8;
   int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
-  if (i >= a.numel) return;
   bf16x8 p, g, m, v;
-  adam_pipe_load(a, i, p, g, m, v);
+  if (i < a.numel) adam_pipe_load(a, i, p, g, m, v);
   for (; i < a.numel; i += stride) {
     const int64_t nx = i + stride;
     bf16x8 p2 = p, g2 = g, m2 = m, v2 = v;
@@ -565,6 +579,7 @@ __global__ __launch_bounds__(256) void adam_pipe_kernel(const AdamArgs a) {
     __builtin_nontemporal_store(v, (bf16x8*)((bf16_t*)a.v + i));
     p = p2; g = g2; m = m2; v = v2;
   }
+  if (a.done_ctr) adam_signal_done(a.done_ctr);
 }
 
 // Decoder-half Adam over W_dec [h][K] (bf16) in 64 x 64 tiles that also emits what the next
@@ -870,6 +885,7 @@ static AdamArgs adam_args(void* p, const void* g, void* m, void* v, int64_t nume
   return a;
 }
 static int adam_launch(const AdamArgs& a, int64_t max_blocks, int dtype, hipStream_t st);
+static int64_t adam_capped_blocks(int64_t numel, int64_t max_blocks);
 
 extern "C" {
 
@@ -913,11 +929,16 @@ int cc_adam_step_clip(void* p, const void* g, void* m, void* v, int64_t numel, c
   return adam_launch(a, max_blocks, dtype, (hipStream_t)stream);
 }
 
+int64_t cc_adam_capped_blocks(int64_t numel, int64_t max_blocks) {
+  return numel > 0 && max_blocks > 0 ? adam_capped_blocks(numel, max_blocks) : 0;
+}
+
 int cc_adam_dec_norms(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, const float* sums,
                       int nparams, float max_norm, int emulate_bf16, double lr, double beta1, double beta2,
                       double eps, int64_t step, int64_t max_blocks, float* norm_part, int64_t h, int64_t K, int dtype,
-                      void* stream) {
+                      uint32_t* done_ctr, void* stream) {
   if (!p || !g || !m || !v || !norm_part || (!coef && !sums)) return CC_ERR_NULL;
+  if (done_ctr && max_blocks <= 0) return CC_ERR_SHAPE;  // (the signal is the capped grid-stride forms')
   if (numel <= 0 || step <= 0 || h <= 0 || K <= 0 || K % 64 || h * K > numel || h * K >= ((int64_t)1 << 31))
     return CC_ERR_SHAPE;
   if (sums && (nparams <= 0 || nparams > 6)) return CC_ERR_SHAPE;
@@ -932,18 +953,22 @@ int cc_adam_dec_norms(void* p, const void* g, void* m, void* v, int64_t numel, c
   a.norm_part = norm_part;
   a.norm_rows = (int)h;
   a.norm_ld = (int)K;
+  a.done_ctr = done_ctr;
   // (the grid-stride form: the bulk kernel does not form the partials)
   return adam_launch(a, max_blocks > 0 ? max_blocks : 1024, dtype, (hipStream_t)stream);
 }
 
 }  // extern "C"
 
+// workgroups of adam_launch's capped grid-stride form
+static int64_t adam_capped_blocks(int64_t numel, int64_t max_blocks) {
+  const int64_t blocks = ((numel + 7) / 8 + 255) / 256;
+  return blocks > max_blocks ? max_blocks : blocks;
+}
 static int adam_launch(const AdamArgs& a, int64_t max_blocks, int dtype, hipStream_t st) {
   const int64_t numel = a.numel;
   if (max_blocks > 0) {  // capped grid-stride form: leaves most CUs to a concurrent GEMM
-    int64_t work = (numel + 7) / 8;
-    int64_t blocks = (work + 255) / 256;
-    if (blocks > max_blocks) blocks = max_blocks;
+    const int64_t blocks = adam_capped_blocks(numel, max_blocks);
     if (dtype == CC_BF16 && numel % 8 == 0) {
       hipLaunchKernelGGL(adam_pipe_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
       CC_LAUNCH_CHECK();

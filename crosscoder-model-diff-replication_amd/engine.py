@@ -59,6 +59,13 @@ DYNAMIC_TILES = True
 LOSS_TAIL_IN_G3 = True
 
 
+# G2 (the step's first reader of the decoder half) waits for the side-stream decoder-half Adam inside its kernel
+# (a done counter the Adam's workgroups increment; cc_decode_loss' wait_ctr) instead of the compute stream
+# waiting for the Adam's event: the ~10 us a cross-stream dependency takes to release the next kernel go away.
+# Other readers still wait for the event.  The same bits either way.
+G2_WAITS_IN_KERNEL = True
+
+
 def _tile_ctr(ws, k):
     return ws.tile_ctr[k] if DYNAMIC_TILES else None
 
@@ -98,6 +105,8 @@ class Arena:
         self.pending = None  # event the decoder half's Adam (side stream) records; see clip_and_adam
         # the decoder half's last rows, launched by the first reader on its own stream (engine.adam)
         self.pending_rest = None
+        # a stream already ordered after `pending` by a launch that waited for the Adam in its kernel
+        self.pending_ordered = None
 
     def enc_part(self):
         return self.data[:self.split]
@@ -105,15 +114,24 @@ class Arena:
     def dec_part(self):
         return self.data[self.split:]
 
-    def wait_pending(self):
+    def wait_pending(self, kernel_wait=False):
         """Order torch's current stream after the decoder half's Adam if it ran on a side stream (launching
-        its deferred last rows first, if any)."""
+        its deferred last rows first, if any).  kernel_wait (the caller is a cc_decode_loss launch that can wait
+        in its kernel): returns that wait's (counter, target) instead of ordering the stream, where the Adam
+        signals one; the stream then counts as ordered once that launch is enqueued (pending_ordered)."""
+        tok = None
         if self.pending_rest is not None:
             rest, self.pending_rest = self.pending_rest, None
-            rest()
+            tok = rest(kernel_wait)
+        if tok is not None:
+            return tok
         if self.pending is not None:
-            self.pending.wait(torch.cuda.current_stream(self.data.device))
+            cur = torch.cuda.current_stream(self.data.device)
+            if cur != self.pending_ordered:
+                self.pending.wait(cur)
             self.pending = None
+            self.pending_ordered = None
+        return None
 
     def like(self, dtype=None, device=None):
         """A zeroed arena of the same dims (grads / Adam moments)."""
@@ -232,6 +250,12 @@ class StepWorkspace:
         self.acts_pending = False  # forward deferred the activation column sums to loss_finalize
         # arrival counters of the fused tail launches (loss tail, grad tail); each launch leaves 0
         self.tail_ctr = torch.zeros(2, dtype=torch.int32, device=device)
+        # the side-stream decoder-half Adam's done counter (each workgroup adds 1; never reset) and the count
+        # G2 waits for in its kernel (G2_WAITS_IN_KERNEL); wait_err: a mapped host word G2 sets if that wait
+        # ever times out (checked by the next forward)
+        self.adam_done = torch.zeros(8, dtype=torch.int32, device=device)
+        self.adam_done_target = 0
+        self.wait_err = None
         self.norms_token = None
         self.busy = None  # weakref to the token of an autograd graph whose backward still needs this workspace
 
@@ -319,12 +343,17 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     if not fused:
         ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
         ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts)
-    P.wait_pending()
+    fused_g2 = bool(loss and ws.fused_ncb)
+    # (only while the decoder norms are the Adam's own: otherwise decoder_norms below reads W_dec on this stream)
+    wait = P.wait_pending(kernel_wait=fused_g2 and G2_WAITS_IN_KERNEL and ws.norms_token == _norms_token(P))
+    if wait is not None:
+        wait = (*wait, _wait_err(ws))
     decoder_norms(ws, P)  # (+ W_dec^T), unless launched already after the last Adam
-    if loss and ws.fused_ncb:
-        # (carries a pending norm finaliser and, fused, the activation column sums)
+    if fused_g2:
+        # (carries a pending norm finaliser and, fused, the activation column sums; waits in its kernel for the
+        # side-stream Adam where `wait`)
         decode_loss(ws, P, grad_scale, pre=ops.colsum_job(ws.acts_colpart, ws.acts_colpart.shape[0], h, 1.0,
-                                                          ws.colsum_acts) if fused else None)
+                                                          ws.colsum_acts) if fused else None, wait=wait)
         ws.acts_pending = True
         if finalize:
             loss_finalize(ws)
@@ -346,15 +375,28 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
             loss_finalize(ws)
 
 
-def decode_loss(ws, P, grad_scale=None, pre=None):
+def _wait_err(ws):
+    """The mapped host word a G2 launch sets if its in-kernel wait times out (raised here, by the next forward)."""
+    if ws.wait_err is None:
+        ws.wait_err = _hip.MappedHostBuffer(4)
+    if ws.wait_err.u32[0]:
+        raise RuntimeError("crosscoder_hip: G2's in-kernel wait for the decoder-half Adam timed out (a step's results "
+                           "are invalid)")
+    return ws.wait_err.device_ptr
+
+
+def decode_loss(ws, P, grad_scale=None, pre=None, wait=None):
     """G2 + loss rows + g_recon (and g_recon^T) in one pass over the whole batch (decode_loss: W_dec read
-    directly).  pre: an ops.colsum_job the launch runs first."""
+    directly).  pre: an ops.colsum_job the launch runs first; wait: (counter, target, err) of the side-stream
+    Adam it waits for in the kernel."""
     gs = 2.0 / ws.B if grad_scale is None else grad_scale
     nf = (ws.norm_part, ws.norms, ws.tn, ws.inv_norms) if ws.norms_fin_pending else None
     ws.norms_fin_pending = False
     with _span("G2_decode"):
         ops.decode_loss(ws.acts, P.W_dec_hk, P.b_dec_flat, ws.x, ws.x_mean, gs, ws.g_recon, ws.g_recon_t,
-                        ws.row_part_fused, ws.loss_colpart, ws.dec_ws, ws.n, ws.d, norm_fin=nf, pre=pre)
+                        ws.row_part_fused, ws.loss_colpart, ws.dec_ws, ws.n, ws.d, norm_fin=nf, pre=pre, wait=wait)
+    if wait is not None:
+        P.pending_ordered = torch.cuda.current_stream(ws.x.device)
     ws.row_ncb = ws.fused_ncb
     ws.loss_col_rows = ops.col_part_rows(ws.B)
 
@@ -601,16 +643,21 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
             dec = [A.dec_part() for A in (P, G, M, V)]
             kw = dict(coef=coef if clip_sums is None else None, clip_sums=clip_sums, emulate=emulate)
             hp = (lr, beta1, beta2, eps, step)
+            target = None
             if hs > 0:
                 with _span("adam_dec"):
-                    ops.adam_dec_norms(*(t[:hs * K] for t in dec), hs, K, *hp, ws.norm_part[:hs * nblk],
-                                       max_blocks=DEC_ADAM_BLOCKS, **kw)
+                    nb = ops.adam_dec_norms(*(t[:hs * K] for t in dec), hs, K, *hp, ws.norm_part[:hs * nblk],
+                                            max_blocks=DEC_ADAM_BLOCKS, done_ctr=ws.adam_done, **kw)
+                ws.adam_done_target = (ws.adam_done_target + nb) & 0xFFFFFFFF
+                target = ws.adam_done_target
             done = _hip.DeviceEvent().record(side_stream)
 
-            def rest():
+            def rest(kernel_wait=False):
                 # the rows on the reader's stream, then it waits for the side stream's rows; the norm partials are
                 # then complete, and the finaliser rides in the next G2 launch (decode_loss: G3 and the loss tail,
-                # its first readers, run after G2) or runs before the first other reader (flush_norms)
+                # its first readers, run after G2) or runs before the first other reader (flush_norms).
+                # kernel_wait (the reader is that G2 launch): G2 waits for the side stream's rows in its kernel
+                # (returns the done counter and its target; P.pending keeps the event for other streams' readers)
                 cur = torch.cuda.current_stream(dev)
                 with _span("adam_dec_rest"):
                     if ws.h > hs:
@@ -618,8 +665,12 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
                                            **kw)
                     else:  # (every row on the side stream: b_dec only)
                         step_(*(t[hs * K:] for t in dec))
-                done.wait(cur)
                 ws.norms_fin_pending = True
+                if kernel_wait and target is not None:
+                    P.pending = done
+                    return ws.adam_done, target
+                done.wait(cur)
+                return None
 
             ws.norms_token = _norms_token(P)
             P.pending_rest = rest

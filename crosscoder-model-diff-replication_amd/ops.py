@@ -220,16 +220,20 @@ def decode_loss_t(acts, W_dec_t, b_dec, x, x_mean, grad_scale, g_recon, g_recon_
 
 
 def decode_loss(acts, W_dec_hk, b_dec, x, x_mean, grad_scale, g_recon, g_recon_t, row_part, col_part, ws, n, d,
-                norm_fin=None, pre=None):
+                norm_fin=None, pre=None, wait=None):
     """decode_loss_t reading W_dec [h, K] itself (cc_decode_loss, transposed LDS reads of the B operand): the same
     bits without the W_dec^T copy.  g_recon_t may be None.  norm_fin = (part, norms, total, inv_norms): the decoder
-    norms' finaliser (dec_norms_finalize) rides in the launch."""
+    norms' finaliser (dec_norms_finalize) rides in the launch.  wait = (ctr, target, err_addr): the launch waits in
+    the kernel for a done counter of adam_dec_norms on another stream (err_addr: host-visible word set on a
+    timeout)."""
     B, h = acts.shape
     part, norms, total, inv = norm_fin if norm_fin is not None else (None, None, None, None)
+    wctr, wtarget, werr = wait if wait is not None else (None, 0, None)
     check(lib().cc_decode_loss(_ptr(acts), _ptr(W_dec_hk), _ptr(b_dec), _ptr(x), _ptr(x_mean), grad_scale,
                                _ptr(g_recon), _ptr(g_recon_t), _ptr(row_part), _ptr(col_part), _ptr(ws),
-                               0 if ws is None else ws.numel(), _ptr(part), _ptr(norms), _ptr(total), _ptr(inv), pre, B,
-                               h, n, d, dtype_code(acts.dtype), _stream(acts)))
+                               0 if ws is None else ws.numel(), _ptr(part), _ptr(norms), _ptr(total), _ptr(inv), pre,
+                               _ptr(wctr), int(wtarget) & 0xFFFFFFFF, werr, B, h, n, d, dtype_code(acts.dtype),
+                               _stream(acts)))
 
 
 def loss_fwd_bwd(recon_f32, b_dec, x, x_mean, g_recon, row_part, col_part, grad_scale, B, n, d, row0=0, rows=None,
@@ -376,14 +380,23 @@ def dec_norms_finalize(part, h, n, d, norms, total, inv_norms=None):
 
 
 def adam_dec_norms(p, g, m, v, h, K, lr, beta1, beta2, eps, step, part, coef=None, clip_sums=None, emulate=True,
-                   max_blocks=0):
+                   max_blocks=0, done_ctr=None):
     """Adam over the decoder half p/g/m/v (flat views, W_dec [h, K] first) that also writes the decoder-norm
     partials of the updated W_dec into `part` (cc_adam_dec_norms; dec_norms_finalize completes them).
-    coef: the clip coefficient tensor; or clip_sums = (sums, max_norm): formed in the kernel."""
+    coef: the clip coefficient tensor; or clip_sums = (sums, max_norm): formed in the kernel.  done_ctr (int32
+    device word, max_blocks > 0): each workgroup adds 1 when its results are released; returns the number of
+    workgroups (adam_capped_blocks) then, else None."""
     sums, max_norm = clip_sums if clip_sums is not None else (None, 0.0)
     check(lib().cc_adam_dec_norms(_ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(coef), _ptr(sums),
                                   0 if sums is None else sums.numel(), float(max_norm), int(emulate), lr, beta1, beta2,
-                                  eps, int(step), int(max_blocks), _ptr(part), h, K, dtype_code(p.dtype), _stream(p)))
+                                  eps, int(step), int(max_blocks), _ptr(part), h, K, dtype_code(p.dtype),
+                                  _ptr(done_ctr), _stream(p)))
+    return adam_capped_blocks(p.numel(), max_blocks) if done_ctr is not None else None
+
+
+def adam_capped_blocks(numel, max_blocks):
+    """Workgroups of the capped-grid Adam launch (cc_adam_capped_blocks)."""
+    return int(lib().cc_adam_capped_blocks(int(numel), int(max_blocks)))
 
 
 def adam_dec_transposed(p, g, m, v, coef, lr, beta1, beta2, eps, step, W_dec_t, part, max_blocks=0):

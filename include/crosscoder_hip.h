@@ -193,15 +193,20 @@ int cc_decode_loss_t(const void* acts, const void* W_dec_t, const void* b_dec, c
 /* cc_decode_loss_t reading W_dec [h][K] itself (the parameter, no transposed copy; same bits): the GEMM's B
  * operand goes through transposed LDS reads.  g_recon_t may be NULL here (not written then).
  * norm_part (optional, with norms / tn / inv_norms as in cc_dec_norms_finalize): the decoder norms'
- * finaliser rides in the launch of the split-K leftover (or runs just before the GEMM where the shape has
+ * finaliser rides in the launch of the split-K leftover (or runs right after the GEMM where the shape has
  * none) -- the same bits as cc_dec_norms_finalize(norm_part, h, n, d, norms, tn, inv_norms), ordered before
  * whatever the stream runs next (crosscoder.py:123-125 for the backward and the loss tail).
  * pre (optional): a column reduction the launch runs before its tiles (the step: sum_b acts from the
- * encoder's column partials, which G4 and the l1 loss read, crosscoder.py:126). */
+ * encoder's column partials, which G4 and the l1 loss read, crosscoder.py:126).
+ * wait_ctr (optional): W_dec / b_dec / norm_part come from a producer on another stream (the decoder-half Adam,
+ * cc_adam_dec_norms' done_ctr): every workgroup waits in the kernel, after `pre`, until
+ * (int32_t)(*wait_ctr - wait_target) >= 0 instead of the stream waiting for an event.  A wait past ~1 s gives
+ * up and sets *wait_err (host-visible memory, e.g. mapped pinned) -- the results are then invalid. */
 int cc_decode_loss(const void* acts, const void* W_dec, const void* b_dec, const void* x, const float* x_mean,
                    float grad_scale, void* g_recon, void* g_recon_t, float* row_part, float* col_part, float* ws,
                    int64_t ws_floats, const float* norm_part, float* norms, float* tn, float* inv_norms,
-                   const cc_colsum_job* pre, int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream);
+                   const cc_colsum_job* pre, const uint32_t* wait_ctr, uint32_t wait_target, uint32_t* wait_err,
+                   int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream);
 
 /* Loss reduction (crosscoder.py:106-128, trainer.py:51-61): per-row explained variances
  * ev/ev_a/ev_b [B] (fp32) and scalars[0:8] = {l2, l1, l0, mean ev, mean ev_a, mean ev_b, 0, 0};
@@ -408,11 +413,16 @@ int cc_dec_norms_finalize(const float* part, int64_t h, int64_t n, int64_t d, fl
  * `part` (cc_dec_norms_part_floats(h, n, d) floats) from the updated W_dec for cc_dec_norms_finalize: the next
  * step's decoder norms (crosscoder.py:123-125, same bits as cc_dec_norms) without another pass over W_dec.
  * The clip coefficient comes from `coef`, or (sums != NULL) is formed from the per-parameter squared sums as
- * in cc_adam_step_clip.  K % 64 == 0; max_blocks caps the grid (0: 1024). */
+ * in cc_adam_step_clip.  K % 64 == 0; max_blocks caps the grid (0: 1024).
+ * done_ctr (optional, max_blocks > 0): each of the launch's cc_adam_capped_blocks(numel, max_blocks)
+ * workgroups adds 1 to *done_ctr once its stores are released (agent scope): the count a cc_decode_loss
+ * launch on another stream waits for (wait_ctr / wait_target). */
 int cc_adam_dec_norms(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, const float* sums,
                       int nparams, float max_norm, int emulate_bf16, double lr, double beta1, double beta2,
                       double eps, int64_t step, int64_t max_blocks, float* part, int64_t h, int64_t K, int dtype,
-                      void* stream);
+                      uint32_t* done_ctr, void* stream);
+/* Workgroups of the capped-grid Adam launch (max_blocks > 0) over numel elements. */
+int64_t cc_adam_capped_blocks(int64_t numel, int64_t max_blocks);
 
 int cc_adam_dec_transposed(void* p, const void* g, void* m, void* v, int64_t h, int64_t K, const float* coef,
                            double lr, double beta1, double beta2, double eps, int64_t step, int64_t max_blocks,

@@ -534,7 +534,7 @@ def test_delayed_side_stream_adam_still_orders_the_norm_readers(gpu, dbg_lib, mo
         def adam_dec_norms(*a, _ns=delay_ns, **k):
             if _ns and k.get("max_blocks", 0) > 0:  # (the side-stream launch)
                 ops.check(dbg_lib.cc_debug_spin(1, 0, _ns, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
-            orig(*a, **k)
+            return orig(*a, **k)
 
         monkeypatch.setattr(ops, "adam_dec_norms", adam_dec_norms)
         cc = ca.CrossCoder(cfg)
@@ -545,6 +545,36 @@ def test_delayed_side_stream_adam_still_orders_the_norm_readers(gpu, dbg_lib, mo
         m = torch.cat([st[p]["exp_avg"].detach().flatten().float() for p in cc.parameters()])
         v = torch.cat([st[p]["exp_avg_sq"].detach().flatten().float() for p in cc.parameters()])
         torch.cuda.synchronize()
+        outs.append((dicts, cc.arena().data.clone(), m, v))
+    (d0, p0, m0, v0), (d1, p1, m1, v1) = outs
+    assert d0 == d1
+    assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+
+
+@pytest.mark.parametrize("B,n,d,h", [(1024, 2, 256, 2048), (512, 4, 128, 1024)])
+def test_g2_kernel_wait_matches_stream_wait(gpu, B, n, d, h, monkeypatch):
+    """G2 waiting for the side-stream decoder-half Adam inside its kernel (engine.G2_WAITS_IN_KERNEL: the Adam's
+    workgroups count into a done counter, cc_decode_loss' wait_ctr) == the compute stream waiting for the Adam's
+    event: the same loss dicts, params and moments bit for bit; the counter ends at the host's target, and no
+    wait timed out."""
+    from crosscoder_amd import engine
+    cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+               num_tokens=B * 20, device=str(gpu))
+    outs = []
+    for in_kernel in (False, True):
+        monkeypatch.setattr(engine, "G2_WAITS_IN_KERNEL", in_kernel)
+        cc = ca.CrossCoder(cfg, n_models=n)
+        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 4, seed=9), crosscoder=cc)
+        dicts = [tr.step() for _ in range(4)]
+        st = tr.optimizer.state
+        m = torch.cat([st[p]["exp_avg"].detach().flatten().float() for p in cc.parameters()])
+        v = torch.cat([st[p]["exp_avg_sq"].detach().flatten().float() for p in cc.parameters()])
+        torch.cuda.synchronize()
+        ws = cc._workspace(B, step=True)
+        assert ws.adam_done_target > 0
+        assert int(ws.adam_done[0]) & 0xFFFFFFFF == ws.adam_done_target
+        if in_kernel:
+            assert ws.wait_err is not None and int(ws.wait_err.u32[0]) == 0  # (the in-kernel path ran, no timeout)
         outs.append((dicts, cc.arena().data.clone(), m, v))
     (d0, p0, m0, v0), (d1, p1, m1, v1) = outs
     assert d0 == d1
