@@ -550,11 +550,13 @@ CC_DEV void pp_wait_ready(const GemmArgs& a) {
   if (threadIdx.x == 0) {
     int it = 0;
     while ((int)(__hip_atomic_load(a.wait_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.wait_target) < 0) {
-      if (++it > (1 << 22)) {  // (~1 s)
+      if (++it > (1 << 21)) {  // (~1 s)
         if (a.wait_err) __hip_atomic_store(a.wait_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
-      __builtin_amdgcn_s_sleep(8);
+      // ~0.6 us between reads: every workgroup of the launch polls the one word (at 0.25 us they would put
+      // ~1 G atomic reads/s on it while the producer finishes)
+      __builtin_amdgcn_s_sleep(20);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
