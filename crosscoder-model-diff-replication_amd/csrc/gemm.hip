@@ -70,7 +70,7 @@ struct GemmArgs {
                         // in accumulator order: [tile tm*nbn + tn][thread][4] u32, bit 4(4i+j)+e of fragment (i,j)
   uint32_t* tile_ctr;   // persistent ping-pong launches: 8 per-XCD tile counters (dynamic order), NULL: static
   uint32_t* wave_sync;  // probe only: 8 zeroed per-XCD arrival words (TileLoop::wave_wait), NULL: off
-  uint64_t* stamps;     // probe build only (-DCC_PP_STAMPS): [tile][8] clock stamps of a ping-pong tile (pp_tile)
+  uint64_t* stamps;     // probe build only (-DCC_PP_STAMPS): [tile][12] clock stamps of a ping-pong tile (pp_tile)
   // wait in the kernel for a producer on another stream (cc_decode_loss: the side-stream Adam's done counter,
   // AdamArgs::done_ctr) before the first operand load: until *wait_ctr - wait_target >= 0 (mod 2^32); a wait
   // past ~1 s gives up, sets *wait_err (host-visible) and runs on (NULL wait_ctr: none)
@@ -671,7 +671,7 @@ static int g_epi_store = 1;
 CC_DEBUG_API void cc_debug_set_epi_store(int on) { g_epi_store = on; }
 static void debug_epi_store(GemmArgs& a, int64_t stamp_tile0 = 0) {
   if (!g_epi_store) a.out = a.out_t = nullptr;
-  if (g_stamps) a.stamps = g_stamps + stamp_tile0 * 8;
+  if (g_stamps) a.stamps = g_stamps + stamp_tile0 * 12;
 }
 CC_DEBUG_API void cc_debug_set_wave_sync(int on) { g_wave_sync = on; }
 static void debug_wave_sync(GemmArgs& a, hipStream_t st) {

@@ -39,7 +39,8 @@
 // thread 0 keeps s_memtime at tile entry (0), after the prologue's barrier (1), after the K loop (2), after the
 // drain before the epilogue (3) and after the epilogue's stores are issued (4), plus the 100 MHz wall clock at
 // entry (5) and end (6), and writes them with one store per value after the epilogue (no store inside the
-// K loop: it would sit in the loop's counted vmcnt waits).
+// K loop: it would sit in the loop's counted vmcnt waits); the LDS epilogue adds s_memtime after its element
+// work (7), after the direct stores (8) and after the transposed stores (9).  12 slots per tile.
 #ifdef CC_PP_STAMPS
 #define PP_STAMP_DECL uint64_t pp_st[7] = {(uint64_t)__builtin_amdgcn_s_memtime(), 0, 0, 0, 0, (uint64_t)wall_clock64(), 0}
 #define PP_STAMP(k) pp_st[k] = __builtin_amdgcn_s_memtime()
@@ -47,12 +48,22 @@
   do {                                                                                    \
     pp_st[6] = wall_clock64();                                                            \
     if ((args).stamps && threadIdx.x == 0)                                                \
-      for (int k_ = 0; k_ < 7; ++k_) (args).stamps[(int64_t)(bid) * 8 + k_] = pp_st[k_]; \
+      for (int k_ = 0; k_ < 7; ++k_) (args).stamps[(int64_t)(bid) * 12 + k_] = pp_st[k_]; \
   } while (0)
 #else
 #define PP_STAMP_DECL
 #define PP_STAMP(k)
 #define PP_STAMP_WRITE(args, bid)
+#endif
+// (inside the epilogue: slots 7.. of the tile, stored at once -- after the K loop, outside its counted waits)
+#ifdef CC_PP_STAMPS
+#define PP_EPI_STAMP(args, wave_slot, k)                                                       \
+  do {                                                                                        \
+    if ((args).stamps && threadIdx.x == 0)                                                    \
+      (args).stamps[(int64_t)((wave_slot) >> 3) * 12 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define PP_EPI_STAMP(args, wave_slot, k)
 #endif
 CC_DEV void pp_static_prio() {
 #if CC_PP_PRIO & 2
@@ -213,6 +224,7 @@ CC_DEV float pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], cha
   const float wsum = epilogue_core<CC_BF16, EPI, 256, FAST>(args, acc, fg, io, tm, m0, n0, wr, lane, wave_slot, ecols,
                                                             cw);
   __syncthreads();
+  PP_EPI_STAMP(args, wave_slot, 7);
   if (args.out) {
     const __amdgpu_buffer_rsrc_t rout = tile_rsrc(args.out, args.ldo, m0, n0, args.M, args.N, 2);
 #pragma unroll
@@ -223,7 +235,9 @@ CC_DEV float pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], cha
                                              (int)piece_off(ci, lane, rows, cols, ldo), 0, 0);
     }
   }
+  PP_EPI_STAMP(args, wave_slot, 8);
   if (args.out_t) pp_store_transposed(args, smem, qb, m0, n0, rows, cols, lane, wave);
+  PP_EPI_STAMP(args, wave_slot, 9);
   return wsum;
 }
 

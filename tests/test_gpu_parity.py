@@ -564,7 +564,7 @@ def test_g2_kernel_wait_matches_stream_wait(gpu, B, n, d, h, monkeypatch):
     for in_kernel in (False, True):
         monkeypatch.setattr(engine, "G2_WAITS_IN_KERNEL", in_kernel)
         cc = ca.CrossCoder(cfg, n_models=n)
-        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 4, seed=9), crosscoder=cc)
+        tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 4, n_models=n, seed=9), crosscoder=cc)
         dicts = [tr.step() for _ in range(4)]
         st = tr.optimizer.state
         m = torch.cat([st[p]["exp_avg"].detach().flatten().float() for p in cc.parameters()])

@@ -67,20 +67,23 @@ def main():
     }
     for name in which:
         fn, ntiles = calls[name]
-        stamps = torch.zeros(ntiles * 8, device=dev, dtype=torch.int64)
+        stamps = torch.zeros(ntiles * 12, device=dev, dtype=torch.int64)
         for _ in range(20):
             assert fn() == 0
         L.cc_debug_set_stamps(P(stamps))
         assert fn() == 0
         L.cc_debug_set_stamps(None)
         torch.cuda.synchronize()
-        s = stamps.view(ntiles, 8).cpu().numpy().astype(np.int64)
+        s = stamps.view(ntiles, 12).cpu().numpy().astype(np.int64)
         cyc = s[:, 4] - s[:, 0]
         wall_us = (s[:, 6] - s[:, 5]) * 0.01
         ghz = np.median(cyc / (wall_us * 1e3))
         us = lambda c: c / (ghz * 1e3)  # noqa: E731
         seg = {"prologue": us(s[:, 1] - s[:, 0]), "k_loop": us(s[:, 2] - s[:, 1]), "drain": us(s[:, 3] - s[:, 2]),
                "epilogue": us(s[:, 4] - s[:, 3]), "tile": us(s[:, 4] - s[:, 0])}
+        if (s[:, 7] > 0).all():  # the LDS epilogue's own points: element work, direct stores, transposed stores
+            seg.update({"epi_core": us(s[:, 7] - s[:, 3]), "epi_store": us(s[:, 8] - s[:, 7]),
+                        "epi_store_t": us(s[:, 9] - s[:, 8]), "epi_return": us(s[:, 4] - s[:, 9])})
         # static order: XCD x = t % 8 runs i = t // 8 on workgroup w = i % nwx, wave of tiles k = i // nwx
         nwx = 32
         t = np.arange(ntiles)
