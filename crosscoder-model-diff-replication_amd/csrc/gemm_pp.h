@@ -197,26 +197,24 @@ CC_DEV void pp_store_transposed(const GemmArgs& args, const char* smem, const in
 template <int EPI, bool FAST>
 CC_DEV float pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], char* smem, const int (&qb)[4],
                             bool input_staged, int tm, int m0, int n0, int wr, int wc, int lane, int wave,
-                            int wave_slot, const FragGeom<256>& fg, const EpiCols<CC_BF16, 256>& ecols) {
+                            int wave_slot, const FragGeom<256>& fg, const EpiCols<CC_BF16, 256>& ecols,
+                            const float (&cw)[8][4]) {
   const int rows = args.M - m0, cols = args.N - n0, ldo = (int)args.ldo;
   // the epilogue's input tile: d_acts' activation mask (the general form; FAST reads G1's mask bits instead),
   // the fused loss's x tile, dW_dec's W_dec tile (prefetched by the K loop)
   const void* in = (EPI == EPI_DACTS && !FAST) || EPI == EPI_DLOSS
                        ? args.mask_src
                        : (EPI == EPI_WGDEC && args.scale0 != 0.f ? args.w_src : nullptr);
-  float cw[8][4];  // dW_dec L1-term factors (EPI_WGDEC only)
-  if (in) {
-    if (!input_staged) {
-      const __amdgpu_buffer_rsrc_t rin = tile_rsrc(in, args.ldo, m0, n0, args.M, args.N, 2);
+  // (cw: dW_dec's L1-term factors, loaded by pp_tile under the K loop's drain; EPI_WGDEC's W_dec tile is
+  // staged by the K loop too, so only the other epilogues' input tiles move here)
+  if (in && !input_staged) {
+    const __amdgpu_buffer_rsrc_t rin = tile_rsrc(in, args.ldo, m0, n0, args.M, args.N, 2);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int ci = q * 8 + wave;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_void*)(smem + qb[q >> 2] + (ci & 31) * 1024), 16,
-                                                 (int)piece_off(ci, lane, rows, cols, ldo), 0, 0, 0);
-      }
+    for (int q = 0; q < 16; ++q) {
+      const int ci = q * 8 + wave;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_void*)(smem + qb[q >> 2] + (ci & 31) * 1024), 16,
+                                               (int)piece_off(ci, lane, rows, cols, ldo), 0, 0, 0);
     }
-    // the L1-term factors' loads fly with the tile DMA (one latency for both)
-    if constexpr (EPI == EPI_WGDEC) wgdec_factors<256>(args, fg, m0, n0, cw);
     wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
   }
@@ -456,6 +454,12 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
   const FragGeom<256> fg(args, m0, n0, wr, wc, lane);
   EpiCols<CC_BF16, 256> evec;
   if constexpr (EPI != EPI_F32 && EPI != EPI_DEC) load_epi_cols<CC_BF16, EPI, 256, FAST>(evec, args, fg, n0, tm, tn, tid);
+  // dW_dec's L1-term factors: their loads fly with the drain too (after it they would cost the epilogue a
+  // memory latency of their own)
+  float cw[8][4];
+  if constexpr (EPI == EPI_WGDEC) {
+    if (pf) wgdec_factors<256>(args, fg, m0, n0, cw);
+  }
   wait_vmcnt<0>();
 
   if constexpr (EPI == EPI_SPLIT) {  // split-K partial: accumulator fragments stored as they are (1 KB each)
@@ -471,7 +475,7 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
     __builtin_amdgcn_s_barrier();  // every wave's zero-fill DMAs landed: the LDS is free
     PP_STAMP(3);
     const float wsum = pp_epilogue_lds<EPI, FAST>(args, acc, smem, qb, pf, tm, m0, n0, wr, wc, lane, wave,
-                                                  bid * 8 + wave, fg, evec);
+                                                  bid * 8 + wave, fg, evec, cw);
     PP_STAMP(4);
     PP_STAMP_WRITE(args, bid);
     return wsum;
