@@ -151,10 +151,72 @@ CC_DEV void load_epi_cols(EpiCols<DT, BNT>& c, const GemmArgs& args, const FragG
   if constexpr (EPI == EPI_DLOSS) c.load(args, fg, n0, true);  // b_dec, x_mean
 }
 
+// Activation-mask bit of output (i, j, e) of a lane's 32 fragments (EPI_ENC writes them, EPI_DACTS FAST reads
+// them; 4 words per thread): word i / 2, bit k = 8 (i % 2) + 2j + e / 2 for the first element of the bf16 pair
+// e / 2 and k + 16 for the second -- a pair's two bits are one pk_min_u16(pair, 1) shifted left by k.
+CC_DEV constexpr int mask_bit_pos(int i, int j, int e) { return 8 * (i & 1) + 2 * j + (e >> 1) + 16 * (e & 1); }
+
+// EPI_ENC, FAST, bf16 (the step's G1): per bf16 pair -- the ReLU on the rounded pair (v_pk_max_i16 against 0:
+// a negative bf16 is a negative int16; max(round(t), 0) == round(max(t, 0)) bit for bit), the mask bits by one
+// pk_min_u16(pair, 1) or-ed into the pair's word, the l0 count as the popcount of the bits, the column sums of
+// the stored values in pairs.  The same outputs as enc_dacts_core's general arithmetic with half its VALU
+// instructions (a NaN pre-activation is the exception: it stays NaN here -- as torch.relu keeps it -- where
+// fmaxf made it 0).
+template <int BNT, class IO>
+CC_DEV void enc_fast_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN],
+                          const FragGeom<BNT>& fg, const IO& io, int tm, int n0, int wr, int lane, int wave_slot,
+                          const EpiCols<CC_BF16, BNT>& cols) {
+  using WG = WaveGeom<BNT>;
+  static_assert(WG::TM == 8 && WG::TN == 4, "mask bits: 32 fragments");
+  uint32_t bw[4] = {0u, 0u, 0u, 0u};
+  const uint32_t ones = 0x00010001u;
+#pragma unroll
+  for (int j = 0; j < WG::TN; ++j) {
+    typedef __attribute__((ext_vector_type(2))) float f32x2;
+    const f32x2 bb[2] = {{V4<CC_BF16>::get(cols.bias[j], 0), V4<CC_BF16>::get(cols.bias[j], 1)},
+                         {V4<CC_BF16>::get(cols.bias[j], 2), V4<CC_BF16>::get(cols.bias[j], 3)}};
+    f32x2 cs[2] = {{0.f, 0.f}, {0.f, 0.f}};  // (e 0, 1 | e 2, 3: packed adds, the per-element order unchanged)
+#pragma unroll
+    for (int i = 0; i < WG::TM; ++i) {
+      uint32_t w[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x2 t = (f32x2){acc[i][j][2 * h], acc[i][j][2 * h + 1]} + bb[h];  // (packed fp32 adds)
+        const float t0 = t[0], t1 = t[1];
+        // (single instructions on purpose: the vector-typed forms lowered to compares and selects)
+        uint32_t pr, r, pos;
+        asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(pr) : "v"(t0), "v"(t1));  // RNE, as f2bf
+        asm("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(pr));
+        asm("v_pk_min_u16 %0, %1, %2" : "=v"(pos) : "v"(r), "s"(ones));
+        w[h] = r;
+        asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(bw[i >> 1]) : "v"(pos), "i"(mask_bit_pos(i, j, 2 * h)), "v"(bw[i >> 1]));
+        cs[h] += (f32x2){__uint_as_float(r << 16), __uint_as_float(r & 0xffff0000u)};
+      }
+      io.out4p(i, j, __builtin_bit_cast(bf16x4, (u32x2){w[0], w[1]}));
+    }
+    if (args.col_part) {  // reduce over the 16 lanes (rows) that share these 4 columns
+      float csum[4] = {cs[0][0], cs[0][1], cs[1][0], cs[1][1]};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) csum[e] = row16_sum(csum[e]);
+      if ((lane & 15) == 0 && fg.cv[j])
+        st4<CC_F32>(args.col_part, (int64_t)(tm * WG::WARPS_M + wr) * args.N + n0 + fg.c0 + 16 * j, csum);
+    }
+  }
+  if (args.mask_bits)
+    *(u32x4*)mask_bits_at(args, tm, n0 / BNT, wave_slot % 8 * 64 + lane) = u32x4{bw[0], bw[1], bw[2], bw[3]};
+  if (args.wave_part1) {
+    const int l0i = __builtin_popcount(bw[0]) + __builtin_popcount(bw[1]) + __builtin_popcount(bw[2]) +
+                    __builtin_popcount(bw[3]);
+    // (integer-valued floats below 2^24: the per-lane counts sum exactly either way)
+    float t = wave_sum((float)l0i);
+    if (lane == 0) args.wave_part1[wave_slot] = t;
+  }
+}
+
 // EPI_ENC / EPI_DACTS element-wise part (see epilogue_core).  FAST (bf16): every fragment in range, ReLU on.
 // Activation mask (EPI_DACTS): FAST reads G1's mask bits (cols.bits, no mask tile), the general form the
 // acts tile through io.in4.  EPI_ENC writes the bits (args.mask_bits, ping-pong path) for the d_acts GEMM
-// of the same tile grid and wave / lane map: bit 4(4i + j) + e <-> acc[i][j][e].
+// of the same tile grid and wave / lane map: bit mask_bit_pos(i, j, e) of word i / 2 <-> acc[i][j][e].
 template <int DT, int EPI, int BNT, bool FAST, class IO>
 CC_DEV void enc_dacts_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN],
                            const FragGeom<BNT>& fg, const IO& io, int tm, int n0, int wr, int lane, int wave_slot,
@@ -199,11 +261,11 @@ CC_DEV void enc_dacts_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT
         float t = acc[i][j][e] + add[e];
         if constexpr (EPI == EPI_ENC) {
           if (FAST || args.flag) t = fmaxf(t, 0.f);
-        } else if constexpr (FAST) {  // bit 4(4i + j) + e = word i / 2, bit 16 (i % 2) + 4j + e
+        } else if constexpr (FAST) {  // (mask_bit_pos)
           // (the bit sign-extended to an all-ones / zero mask, opaque so that it stays two VALU ops instead of
           // a compare + select per element)
           int m;
-          asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(cols.bits[i >> 1]), "i"(16 * (i & 1) + 4 * j + e));
+          asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(cols.bits[i >> 1]), "i"(mask_bit_pos(i, j, e)));
           t = __int_as_float(__float_as_int(t) & m);
         } else {
           t = V4<DT>::get(mraw[i][j % JB], e) > 0.f ? t : 0.f;
@@ -218,7 +280,7 @@ CC_DEV void enc_dacts_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT
       } else {
         io.out4(i, j, v);
       }
-      uint32_t nib = 0u;  // EPI_ENC: this fragment's 4 mask bits
+      uint32_t nib = 0u;  // EPI_ENC: this fragment's 4 mask bits (at bits 0, 16, 1, 17)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         csum[e] += v[e];
@@ -230,11 +292,10 @@ CC_DEV void enc_dacts_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT
           if constexpr (FAST) asm("v_med3_i32 %0, %1, 0, 1" : "=v"(pos) : "v"(__float_as_int(v[e])));
           else pos = v[e] > 0.f;  // (the general form: its range selects need the compares anyway)
           l0i += pos;
-          nib |= (uint32_t)pos << e;
+          nib |= (uint32_t)pos << ((e >> 1) + 16 * (e & 1));  // (mask_bit_pos within the fragment)
         }
       }
-      // bit 4(4i + j) + e = word i / 2, bit 16 (i % 2) + 4j + e
-      if constexpr (EPI == EPI_ENC) bw[i >> 1] |= nib << (16 * (i & 1) + 4 * j);
+      if constexpr (EPI == EPI_ENC) bw[i >> 1] |= nib << mask_bit_pos(i, j, 0);
     }
     if (args.col_part) {  // reduce over the 16 lanes (rows) that share these 4 columns
 #pragma unroll
@@ -347,7 +408,10 @@ CC_DEV float epilogue_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT
     // FAST (a kernel variant the host picks when every tile lies inside the matrix and the ReLU is on,
     // as in the step's G1 / G3): no range selects, one bf16 conversion per output, an integer l0
     // count.  Same bits as the general form.
-    enc_dacts_core<DT, EPI, BNT, FAST && DT == CC_BF16>(args, acc, fg, io, tm, n0, wr, lane, wave_slot, cols);
+    if constexpr (EPI == EPI_ENC && FAST && DT == CC_BF16 && BNT == 256)
+      enc_fast_core<BNT>(args, acc, fg, io, tm, n0, wr, lane, wave_slot, cols);
+    else
+      enc_dacts_core<DT, EPI, BNT, FAST && DT == CC_BF16>(args, acc, fg, io, tm, n0, wr, lane, wave_slot, cols);
   } else if constexpr (EPI == EPI_DLOSS) {
     static_assert(DT == CC_BF16, "the fused decode + loss epilogue is bf16 only");
     dloss_core<BNT, FAST>(args, acc, fg, io, tm, m0, n0, wr, lane, cols);
