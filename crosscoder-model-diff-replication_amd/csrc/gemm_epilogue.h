@@ -196,8 +196,7 @@ CC_DEV void enc_fast_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
     }
     if (args.col_part) {  // reduce over the 16 lanes (rows) that share these 4 columns
       float csum[4] = {cs[0][0], cs[0][1], cs[1][0], cs[1][1]};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) csum[e] = row16_sum(csum[e]);
+      row16_sum4(csum);
       if ((lane & 15) == 0 && fg.cv[j])
         st4<CC_F32>(args.col_part, (int64_t)(tm * WG::WARPS_M + wr) * args.N + n0 + fg.c0 + 16 * j, csum);
     }
