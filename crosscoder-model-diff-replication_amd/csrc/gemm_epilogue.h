@@ -151,6 +151,18 @@ CC_DEV void load_epi_cols(EpiCols<DT, BNT>& c, const GemmArgs& args, const FragG
   if constexpr (EPI == EPI_DLOSS) c.load(args, fg, n0, true);  // b_dec, x_mean
 }
 
+// Tile-anatomy probe points inside the epilogue (-DCC_PP_STAMPS builds, see gemm_pp.h): s_memtime into slot k
+// of the tile's 12, stored at once -- after the K loop, outside its counted waits.
+#ifdef CC_PP_STAMPS
+#define PP_EPI_STAMP(args, wave_slot, k)                                                       \
+  do {                                                                                        \
+    if ((args).stamps && threadIdx.x == 0)                                                    \
+      (args).stamps[(int64_t)((wave_slot) >> 3) * 12 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define PP_EPI_STAMP(args, wave_slot, k)
+#endif
+
 // Activation-mask bit of output (i, j, e) of a lane's 32 fragments (EPI_ENC writes them, EPI_DACTS FAST reads
 // them; 4 words per thread): word i / 2, bit k = 8 (i % 2) + 2j + e / 2 for the first element of the bf16 pair
 // e / 2 and k + 16 for the second -- a pair's two bits are one pk_min_u16(pair, 1) shifted left by k.
@@ -201,6 +213,7 @@ CC_DEV void enc_fast_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
         st4<CC_F32>(args.col_part, (int64_t)(tm * WG::WARPS_M + wr) * args.N + n0 + fg.c0 + 16 * j, csum);
     }
   }
+  PP_EPI_STAMP(args, wave_slot, 10);
   if (args.mask_bits)
     *(u32x4*)mask_bits_at(args, tm, n0 / BNT, wave_slot % 8 * 64 + lane) = u32x4{bw[0], bw[1], bw[2], bw[3]};
   if (args.wave_part1) {
@@ -210,6 +223,7 @@ CC_DEV void enc_fast_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>
     float t = wave_sum((float)l0i);
     if (lane == 0) args.wave_part1[wave_slot] = t;
   }
+  PP_EPI_STAMP(args, wave_slot, 11);
 }
 
 // EPI_ENC / EPI_DACTS element-wise part (see epilogue_core).  FAST (bf16): every fragment in range, ReLU on.

@@ -55,16 +55,7 @@
 #define PP_STAMP(k)
 #define PP_STAMP_WRITE(args, bid)
 #endif
-// (inside the epilogue: slots 7.. of the tile, stored at once -- after the K loop, outside its counted waits)
-#ifdef CC_PP_STAMPS
-#define PP_EPI_STAMP(args, wave_slot, k)                                                       \
-  do {                                                                                        \
-    if ((args).stamps && threadIdx.x == 0)                                                    \
-      (args).stamps[(int64_t)((wave_slot) >> 3) * 12 + (k)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define PP_EPI_STAMP(args, wave_slot, k)
-#endif
+// (PP_EPI_STAMP: gemm_epilogue.h)
 CC_DEV void pp_static_prio() {
 #if CC_PP_PRIO & 2
   if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);

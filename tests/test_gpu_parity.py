@@ -917,8 +917,8 @@ def test_transposed_epilogue_outputs(gpu, B, K, h):
             for e in range(4):
                 r = ti * 256 + wr * 128 + 16 * i + (ln & 15)
                 c = tj * 256 + wc * 64 + 16 * j + 4 * (ln >> 4) + e
-                b = 4 * (4 * i + j) + e
-                bit = (int(bt[ti, tj, wr, wc, ln, b >> 5]) >> (b & 31)) & 1
+                pos = 8 * (i & 1) + 2 * j + (e >> 1) + 16 * (e & 1)  # (mask_bit_pos, gemm_epilogue.h)
+                bit = (int(bt[ti, tj, wr, wc, ln, i >> 1]) >> pos) & 1
                 want = bool(acts[r, c] > 0) if r < B and c < h else False
                 assert bit == want, (i, j, e)
     for g_pre_t, g_pre_t2 in outs:

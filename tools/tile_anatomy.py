@@ -84,6 +84,9 @@ def main():
         if (s[:, 7] > 0).all():  # the LDS epilogue's own points: element work, direct stores, transposed stores
             seg.update({"epi_core": us(s[:, 7] - s[:, 3]), "epi_store": us(s[:, 8] - s[:, 7]),
                         "epi_store_t": us(s[:, 9] - s[:, 8]), "epi_return": us(s[:, 4] - s[:, 9])})
+        if (s[:, 10] > 0).all():  # G1's fast core: element loop, mask / l0 stores, the barrier after it
+            seg.update({"core_loop": us(s[:, 10] - s[:, 3]), "core_bits": us(s[:, 11] - s[:, 10]),
+                        "core_sync": us(s[:, 7] - s[:, 11])})
         # static order: XCD x = t % 8 runs i = t // 8 on workgroup w = i % nwx, wave of tiles k = i // nwx
         nwx = 32
         t = np.arange(ntiles)
