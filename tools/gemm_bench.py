@@ -72,8 +72,9 @@ def main():
         return {
             "G1_encode": lambda: L.cc_encode_fwd(P(x), P(W), P(b_enc), P(tn), P(acts), 1, P(parts), P(parts), P(parts),
                                                  B, K, h, 1, st),
+            # (as the step calls it: no l1 partials -- that selects the whole-tile FAST epilogue)
             "G1_encode_T": lambda: L.cc_encode_fwd_t(P(x), P(W), P(b_enc), P(tn), P(acts), P(actsT2), 1, P(parts),
-                                                     P(parts), P(parts), P(mbits), N0, N0, B, K, h, 1, st),
+                                                     N0, P(parts), P(mbits), N0, N0, B, K, h, 1, st),
             "G2_decode": lambda: L.cc_decode_fwd(P(acts), P(W2), N0, P(recon), N0, B, h, K, 1, st),
             "G2_decode_ws": lambda: L.cc_decode_fwd_ws(P(acts), P(W2), P(recon), P(dws), nws, B, h, K, 1, st),
             "G2_decode_ws_T": lambda: L.cc_decode_fwd_ws_t(P(acts), P(W2T), P(recon), P(dws), nws, B, h, K, 1, st),

@@ -58,7 +58,8 @@ def main():
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     N0 = ctypes.c_void_p(0)
     calls = {
-        "G1": (lambda: L.cc_encode_fwd_t(P(x), P(W), P(b_enc), P(tn), P(acts2), P(actsT2), 1, P(parts), P(parts),
+        # (as the step calls it: no l1 partials -- that selects the whole-tile FAST epilogue)
+        "G1": (lambda: L.cc_encode_fwd_t(P(x), P(W), P(b_enc), P(tn), P(acts2), P(actsT2), 1, P(parts), N0,
                                          P(parts), P(mbits), N0, N0, B, K, h, 1, st), (B // 256) * (h // 256)),
         "G3": (lambda: L.cc_dacts_bwd_t(P(g_recon), P(W2), P(acts), P(tn), 1e-4, P(mbits), P(gpT2), B, P(parts), N0,
                                         N0, B, K, h, 1, st), (B // 256) * (h // 256)),
