@@ -30,6 +30,14 @@
 
 #include <type_traits>
 
+// cache-policy bits (buffer-store aux) of the LDS epilogue's output-tile stores: direct and transposed (build
+// switches; 0 = default policy)
+#ifndef CC_EPI_STORE_AUX
+#define CC_EPI_STORE_AUX 0
+#endif
+#ifndef CC_EPI_STORE_T_AUX
+#define CC_EPI_STORE_T_AUX 0
+#endif
 // experiment switch (default 0): bit 0 = s_setprio 1 around each MFMA cluster; bit 1 = static priority 1 for
 // the second wave group (waves 4-7) from kernel start
 #ifndef CC_PP_PRIO
@@ -180,7 +188,7 @@ CC_DEV void pp_store_transposed(const GemmArgs& args, const char* smem, const in
           (lds_bf16x4*)(base + l1 * 512 + (((ca >> 3) ^ (l1 & 15)) << 4)));
       const bf16x8 v = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
       const uint32_t off = (c < cols && r < rows) ? (uint32_t)(((int64_t)c * ldt + r) * 2) : OOB;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rt, (int)off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rt, (int)off, 0, CC_EPI_STORE_T_AUX);
     }
   }
 }
@@ -221,7 +229,7 @@ CC_DEV float pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], cha
       const int ci = q * 8 + wave;
       const bf16x8 v = *(const bf16x8*)(smem + qb[q >> 2] + (ci & 31) * 1024 + lane * 16);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout,
-                                             (int)piece_off(ci, lane, rows, cols, ldo), 0, 0);
+                                             (int)piece_off(ci, lane, rows, cols, ldo), 0, CC_EPI_STORE_AUX);
     }
   }
   PP_EPI_STAMP(args, wave_slot, 8);
