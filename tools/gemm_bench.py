@@ -33,7 +33,7 @@ def main():
     for arg in sys.argv[1:]:
         spec, _, flag = arg.partition("#")
         path, _, mask = spec.partition("@")
-        label = os.path.join(os.path.basename(os.path.dirname(os.path.abspath(path))), os.path.basename(path))
+        label = os.path.relpath(path)
         libs.append((label + (f"@{mask}" if mask else "") + (f"#{flag}" if flag else ""), load(path),
                      (int(mask) if mask else None, flag == "nostore")))
     dev = torch.device("cuda:0")
