@@ -38,6 +38,9 @@
 #ifndef CC_EPI_STORE_T_AUX
 #define CC_EPI_STORE_T_AUX 0
 #endif
+#ifndef CC_EPI_STORE_WG_AUX  // (the weight-gradient epilogues' direct stores)
+#define CC_EPI_STORE_WG_AUX CC_EPI_STORE_AUX
+#endif
 // experiment switch (default 0): bit 0 = s_setprio 1 around each MFMA cluster; bit 1 = static priority 1 for
 // the second wave group (waves 4-7) from kernel start
 #ifndef CC_PP_PRIO
@@ -229,7 +232,8 @@ CC_DEV float pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], cha
       const int ci = q * 8 + wave;
       const bf16x8 v = *(const bf16x8*)(smem + qb[q >> 2] + (ci & 31) * 1024 + lane * 16);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout,
-                                             (int)piece_off(ci, lane, rows, cols, ldo), 0, CC_EPI_STORE_AUX);
+                                             (int)piece_off(ci, lane, rows, cols, ldo), 0,
+                                             EPI == EPI_WGDEC || EPI == EPI_WGENC ? CC_EPI_STORE_WG_AUX : CC_EPI_STORE_AUX);
     }
   }
   PP_EPI_STAMP(args, wave_slot, 8);
