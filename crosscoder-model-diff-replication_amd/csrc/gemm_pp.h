@@ -38,8 +38,11 @@
 #ifndef CC_EPI_STORE_T_AUX
 #define CC_EPI_STORE_T_AUX 0
 #endif
-#ifndef CC_EPI_STORE_WG_AUX  // (the weight-gradient epilogues' direct stores)
-#define CC_EPI_STORE_WG_AUX CC_EPI_STORE_AUX
+// The weight gradients go out non-temporal: the Adam launches read them once, and kept out of the Infinity Cache
+// they leave it to the parameters and activations the step reads next (step -8 / -21 us in two same-box A/Bs,
+// profiles/r04_ab_epilogue_store_policy.txt; the same policy on acts^T / g_pre^T / g_recon^T was slower)
+#ifndef CC_EPI_STORE_WG_AUX
+#define CC_EPI_STORE_WG_AUX 2
 #endif
 // experiment switch (default 0): bit 0 = s_setprio 1 around each MFMA cluster; bit 1 = static priority 1 for
 // the second wave group (waves 4-7) from kernel start
