@@ -38,6 +38,12 @@
 #ifndef CC_EPI_STORE_T_AUX
 #define CC_EPI_STORE_T_AUX 0
 #endif
+#ifndef CC_EPI_STORE_T_AUX_ENC  // (G1's acts^T)
+#define CC_EPI_STORE_T_AUX_ENC CC_EPI_STORE_T_AUX
+#endif
+#ifndef CC_EPI_STORE_T_AUX_DLOSS  // (G2's g_recon^T)
+#define CC_EPI_STORE_T_AUX_DLOSS CC_EPI_STORE_T_AUX
+#endif
 // The weight gradients go out non-temporal: the Adam launches read them once, and kept out of the Infinity Cache
 // they leave it to the parameters and activations the step reads next (step -8 / -21 us in two same-box A/Bs,
 // profiles/r04_ab_epilogue_store_policy.txt; the same policy on acts^T / g_pre^T / g_recon^T was slower)
@@ -172,6 +178,7 @@ CC_DEV uint32_t piece_off(int ci, int lane, int rows, int cols, int ldo) {
 // writes transposed rows (tile columns) 32w .. 32w+31, 16 at a time; per store a row gets 64
 // contiguous bytes (lane groups g = 0..3 take row chunks 8g.. of a 32-row band), and a wave's 8
 // bands complete its 16 rows of 512 B.
+template <int AUX>
 CC_DEV void pp_store_transposed(const GemmArgs& args, const char* smem, const int (&qb)[4], int m0, int n0, int rows,
                                 int cols, int lane, int wave) {
   const int64_t ldt = args.ldt;
@@ -194,7 +201,7 @@ CC_DEV void pp_store_transposed(const GemmArgs& args, const char* smem, const in
           (lds_bf16x4*)(base + l1 * 512 + (((ca >> 3) ^ (l1 & 15)) << 4)));
       const bf16x8 v = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
       const uint32_t off = (c < cols && r < rows) ? (uint32_t)(((int64_t)c * ldt + r) * 2) : OOB;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rt, (int)off, 0, CC_EPI_STORE_T_AUX);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rt, (int)off, 0, AUX);
     }
   }
 }
@@ -240,7 +247,10 @@ CC_DEV float pp_epilogue_lds(const GemmArgs& args, const f32x4 (&acc)[8][4], cha
     }
   }
   PP_EPI_STAMP(args, wave_slot, 8);
-  if (args.out_t) pp_store_transposed(args, smem, qb, m0, n0, rows, cols, lane, wave);
+  if (args.out_t)
+    pp_store_transposed<EPI == EPI_ENC     ? CC_EPI_STORE_T_AUX_ENC
+                        : EPI == EPI_DLOSS ? CC_EPI_STORE_T_AUX_DLOSS
+                                           : CC_EPI_STORE_T_AUX>(args, smem, qb, m0, n0, rows, cols, lane, wave);
   PP_EPI_STAMP(args, wave_slot, 9);
   return wsum;
 }
