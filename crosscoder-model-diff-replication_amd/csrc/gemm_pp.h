@@ -38,9 +38,10 @@
 #ifndef CC_EPI_STORE_T_AUX
 #define CC_EPI_STORE_T_AUX 0
 #endif
-#ifndef CC_WG_OPERAND_AUX
+#ifndef CC_WG_OPERAND_AUX  // cache policy of the weight-gradient GEMMs' operand DMAs (the activations' last reads)
 #define CC_WG_OPERAND_AUX 0
 #endif
+#define PP_OPERAND_AUX(E) ((E) == EPI_WGDEC || (E) == EPI_WGENC ? CC_WG_OPERAND_AUX : 0)
 #ifndef CC_EPI_STORE_T_AUX_ENC  // (G1's acts^T)
 #define CC_EPI_STORE_T_AUX_ENC CC_EPI_STORE_T_AUX
 #endif
@@ -335,9 +336,6 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
   // tail: 1 = the step may lie past the end (prologue and the last two K steps only: the steady-state
   // loop stays free of the branch); 0 = steady state; 2 = steady state of a K % 64 == 0 contraction:
   // every lane's step lies inside K, so the K advance rides in the scalar offset (no per-DMA VALU)
-  // cache policy of the operand DMAs: the weight-gradient GEMMs read the step's activations for the last time
-  // (build switch CC_WG_OPERAND_AUX, default policy)
-  constexpr int PP_OPERAND_AUX = EPI == EPI_WGDEC || EPI == EPI_WGENC ? CC_WG_OPERAND_AUX : 0;
   auto issue_t = [&](auto tail, int p, int T) {
     constexpr int TL = decltype(tail)::value;
     const bool isA = p < 2;
@@ -350,7 +348,7 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
 #pragma unroll
       for (int q = 0; q < 2; ++q)  // (vo[p][q] == OOB lanes stay past the record count)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? ra : rb, (lds_void*)(dst + pp_ci(p, q, wave) * 1024), 16,
-                                                 (int)vo[p][q], kadd, 0, PP_OPERAND_AUX);
+                                                 (int)vo[p][q], kadd, 0, PP_OPERAND_AUX(EPI));
       return;
     }
     if (TL == 1 && pf && T >= nk) {  // W_dec quarter 0 (B, T = nk), 1 (A, T = nk) or 2 (B, T = nk + 1)
@@ -372,7 +370,7 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
       const uint32_t v = vo[p][q];
       const uint32_t off = (kin && v != OOB) ? v + kadd : OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? ra : rb, (lds_void*)(dst + pp_ci(p, q, wave) * 1024), 16,
-                                               (int)off, 0, 0, PP_OPERAND_AUX);
+                                               (int)off, 0, 0, PP_OPERAND_AUX(EPI));
     }
   };
   auto issue = [&](int p, int T) { issue_t(std::integral_constant<int, 1>{}, p, T); };
