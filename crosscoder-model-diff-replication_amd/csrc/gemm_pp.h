@@ -586,9 +586,9 @@ struct TileLoop {
 CC_DEV void pp_wait_ready(const GemmArgs& a) {
   if (!a.wait_ctr) return;
   if (threadIdx.x == 0) {
-    int it = 0;
+    const uint64_t t0 = wall_clock64();  // (the 100 MHz constant clock: the bound does not depend on sclk)
     while ((int)(__hip_atomic_load(a.wait_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.wait_target) < 0) {
-      if (++it > (1 << 21)) {  // (~1 s)
+      if (wall_clock64() - t0 > 100000000ull) {  // (1 s)
         if (a.wait_err) __hip_atomic_store(a.wait_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }

@@ -552,7 +552,8 @@ def test_delayed_side_stream_adam_still_orders_the_norm_readers(gpu, dbg_lib, mo
 
 
 def test_g2_kernel_wait_timeout_is_loud(gpu, dbg_lib, monkeypatch):
-    """G2's in-kernel wait for the side-stream Adam is bounded (~1.3 s): with the side launch held back 3 s (three
+    """G2's in-kernel wait for the side-stream Adam is bounded (1 s of the constant 100 MHz clock): with the side
+    launch held back 3 s (three
     1 s spin kernels queued before it on its stream) G2 gives up, sets the workspace's mapped error word, and the
     next forward raises instead of training on a half-updated W_dec."""
     import ctypes
