@@ -25,7 +25,9 @@ CC_DEV void tile_put8(char* lds, int r, int chunk, const float v[8]) {
   for (int j = 0; j < 8; ++j) b[j] = (short)f2bf(v[j]);
   *(bf16x8*)(lds + r * 1024 + ((chunk ^ (r & 7)) << 4)) = b;
 }
-template <int R>
+// NT: non-temporal stores (prep's x^T: read once, by G5 at the step's end; kept out of the Infinity Cache it leaves
+// room for what the step reads before that -- step -7 us, profiles/r04_ab_epilogue_store_policy.txt)
+template <int R, bool NT = false>
 CC_DEV void tile_store_transposed(const char* lds, void* out_t, int64_t ldt, int64_t col0, int ncols, int64_t row0,
                                   int nrows) {
   constexpr int RQ = R / 32;  // 32-row bands
@@ -39,9 +41,12 @@ CC_DEV void tile_store_transposed(const char* lds, void* out_t, int64_t ldt, int
         (lds_bf16x4_s*)(lds + l0 * 1024 + (((ca >> 3) ^ (l0 & 7)) << 4) + (ca & 4) * 2));
     const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
         (lds_bf16x4_s*)(lds + l1 * 1024 + (((ca >> 3) ^ (l1 & 7)) << 4) + (ca & 4) * 2));
-    if (c < ncols && rb < nrows)
-      *(bf16x8*)((bf16_t*)out_t + (col0 + c) * ldt + row0 + rb) =
-          bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    if (c < ncols && rb < nrows) {
+      const bf16x8 v = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      bf16x8* dst = (bf16x8*)((bf16_t*)out_t + (col0 + c) * ldt + row0 + rb);
+      if constexpr (NT) __builtin_nontemporal_store(v, dst);
+      else *dst = v;
+    }
   }
 }
 
@@ -87,7 +92,7 @@ __global__ __launch_bounds__(256) void prep_kernel(const void* __restrict__ x_in
         }
       }
       __syncthreads();
-      tile_store_transposed<32>(lds, x_t, B, (int64_t)blockIdx.x * 512, K - blockIdx.x * 512, base,
+      tile_store_transposed<32, true>(lds, x_t, B, (int64_t)blockIdx.x * 512, K - blockIdx.x * 512, base,
                                 B - base < 32 ? B - base : 32);
       __syncthreads();
     }
