@@ -38,6 +38,13 @@
 #ifndef CC_EPI_STORE_T_AUX
 #define CC_EPI_STORE_T_AUX 0
 #endif
+// dW_dec's W_dec tile (the L1 term's input, prefetched into LDS) is read non-temporal: the next reader of W_dec is
+// the decoder-half Adam of the next step, which streams it non-temporal itself; not allocated in the Infinity
+// Cache it leaves room for the GEMM's operands (step -3.1 / -4.7 us in two same-box A/Bs, 10 of 12 rounds lower,
+// profiles/r04_ab_epilogue_store_policy.txt)
+#ifndef CC_WDEC_TILE_AUX
+#define CC_WDEC_TILE_AUX 2
+#endif
 #ifndef CC_WG_OPERAND_AUX  // cache policy of the weight-gradient GEMMs' operand DMAs (the activations' last reads)
 #define CC_WG_OPERAND_AUX 0
 #endif
@@ -357,7 +364,7 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
       for (int q = 0; q < 2; ++q) {
         const int ci = pp_ci(p, q, wave);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void*)(dst + ci * 1024), 16,
-                                                 (int)piece_off(32 * quarter + ci, lane, erows, ecols, eldo), 0, 0, 0);
+                                                 (int)piece_off(32 * quarter + ci, lane, erows, ecols, eldo), 0, 0, CC_WDEC_TILE_AUX);
       }
       return;
     }
@@ -400,7 +407,7 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
     for (int q = 0; q < 4; ++q) {
       const int ci = q * 8 + wave;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void*)(smem + qb[3] + ci * 1024), 16,
-                                               (int)piece_off(96 + ci, lane, erows, ecols, eldo), 0, 0, 0);
+                                               (int)piece_off(96 + ci, lane, erows, ecols, eldo), 0, 0, CC_WDEC_TILE_AUX);
     }
   }
   issue(2, 0);
