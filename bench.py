@@ -26,9 +26,14 @@ epilogue -- from an untimed attribution pass) and `cpu_baseline` (the oracle CPU
 rank 0, N = 1 only).
 """
 import argparse
+import datetime
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 # one HIP hardware queue per stream (HIP's default is 4 per process): the latent-sharded step uses the
@@ -44,8 +49,9 @@ import torch.distributed as dist  # noqa: E402
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import crosscoder_amd as ca  # noqa: E402
-from crosscoder_amd import engine  # noqa: E402
+# (crosscoder_amd -- the HIP library -- is imported by the rank processes only: the launcher parent of an
+# N > 1 run touches no GPU, see launch_ranks)
+ca = engine = None
 
 CONFIGS = {2: (4096, 2, 2304, 16384), 3: (4096, 2, 2304, 131072), 4: (8192, 2, 3584, 65536),
            5: (4096, 4, 2304, 32768)}  # (batch, n_models, d_model, dict_size)
@@ -153,6 +159,31 @@ def n1_same_workload(B, n, d, h):
     return None
 
 
+def clock_words(tr):
+    """The clock words of the fused G4G5 launch's tile-sum scratch (crosscoder_amd.ops.wgrad_clock) of the trainer's
+    step workspace, or None (shapes where the fused launch does not serve)."""
+    from crosscoder_amd import ops
+
+    ws = getattr(getattr(tr, "crosscoder", None), "_ws", None)  # (the step workspace; the sharded step's too)
+    ts = getattr(ws, "tile_sum", None)
+    if ts is not None:
+        return ops.wgrad_clock(ts)
+    return None
+
+
+def effective_clock(words):
+    """Shader clock the chip held over the roofline launches of the timed region: s_memtime ticks / s_memrealtime
+    (100 MHz) ticks, both from the last workgroup of each fused G4G5 launch over its lifetime."""
+    if words is None:
+        return None
+    w = words.tolist()
+    if w[1] <= 0 or w[2] <= 0:
+        return None
+    return {"effective_sclk_ghz": round(w[0] / (w[1] * 10.0), 4), "launches": int(w[2]),
+            "window_ms": round(w[1] * 1e-5, 3),
+            "source": "s_memtime / s_memrealtime of the last workgroup of each G4G5 launch (gemm.hip WgradTail::clock)"}
+
+
 def make_cfg(B, n, d, h):
     return {
         "seed": 49, "batch_size": B, "buffer_mult": 128, "lr": 5e-5, "num_tokens": 400_000_000, "l1_coeff": 2,
@@ -239,9 +270,100 @@ def hbm_rows(kern, B, n, d, h_local, es=2):
     return out
 
 
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv):
+    """`--gpus N` (N > 1) without a torchrun wrapper: start N rank processes under torch.distributed.run as
+    ONE child process group (subprocess: this parent never execs and touches no GPU -- it imports no HIP
+    library and only counts devices), relay rank 0's JSON line, and return non-zero if any rank fails or the
+    deadline passes (the whole group is then killed).  Returns the exit code."""
+    n = args.gpus
+    one_device = os.environ.get("CC_BENCH_ONE_DEVICE") == "1"  # rehearsal: every rank on cuda:0, gloo
+    if not one_device and not args.launcher_check:
+        have = torch.cuda.device_count()  # (does not initialise the GPU)
+        if have < n:
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}; no measurement made",
+                  file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + argv
+    env = dict(os.environ, CC_BENCH_LAUNCHED="1")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=None, text=True, env=env, start_new_session=True)
+    lines = []
+
+    def pump():  # rank output: the JSON line is kept, everything else goes to stderr
+        for line in p.stdout:
+            if line.startswith("{"):
+                lines.append(line.strip())
+            else:
+                sys.stderr.write(line)
+                sys.stderr.flush()
+
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    try:
+        rc = p.wait(timeout=args.deadline)
+    except subprocess.TimeoutExpired:
+        print(f"bench.py: the {n} ranks did not finish within --deadline {args.deadline} s; killing them",
+              file=sys.stderr, flush=True)
+        for sig in (signal.SIGTERM, signal.SIGKILL):
+            try:
+                os.killpg(p.pid, sig)
+            except ProcessLookupError:
+                break
+            try:
+                p.wait(timeout=10)
+                break
+            except subprocess.TimeoutExpired:
+                continue
+        return 124
+    th.join(timeout=10)
+    if rc != 0:
+        print(f"bench.py: rank launcher exited with {rc}", file=sys.stderr, flush=True)
+        return rc
+    if not lines:
+        print("bench.py: the ranks printed no result line", file=sys.stderr, flush=True)
+        return 3
+    try:
+        n_gpus = json.loads(lines[-1]).get("n_gpus")
+    except json.JSONDecodeError:
+        n_gpus = None
+    if n_gpus != n:
+        print(f"bench.py: the result line reports n_gpus {n_gpus}, asked for {n}", file=sys.stderr, flush=True)
+        return 3
+    print(lines[-1], flush=True)
+    return 0
+
+
+def launcher_check(args):
+    """--launcher-check (CPU test of the N-rank launch, no GPU and no HIP library): every rank joins a gloo group
+    and all-reduces its rank; rank 0 prints a line shaped like the bench's."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=args.pg_timeout))
+    t = torch.tensor([float(rank)])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"metric": "launcher-check", "n_gpus": world, "world_size_pg": dist.get_world_size(),
+                          "rank_sum": t.item()}), flush=True)
+    if args.launcher_check == "hang" and rank == world - 1:
+        time.sleep(3600)  # a rank that never returns: the parent's deadline must end the run
+    dist.destroy_process_group()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks) of this node; N > 1 without a torchrun wrapper starts the N ranks itself")
+    ap.add_argument("--deadline", type=float, default=1200.0,
+                    help="N > 1 launched by this script: seconds before every rank is killed (exit 124)")
+    ap.add_argument("--pg-timeout", type=float, default=300.0, help="torch.distributed collective timeout, s")
+    ap.add_argument("--launcher-check", nargs="?", const="ok", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, choices=sorted(CONFIGS), default=None,
@@ -258,6 +380,24 @@ def main():
     ap.add_argument("--force-sharded", action="store_true",
                     help="diagnostic: run the latent-sharded step even on one rank (1-rank RCCL group)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:  # no torchrun wrapper: this process becomes the launcher of the N ranks
+            return launch_ranks(args, sys.argv[1:])
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus and not args.force_sharded:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}", file=sys.stderr, flush=True)
+        return 2
+    if args.launcher_check:
+        return launcher_check(args)
+    return run_rank(args)
+
+
+def run_rank(args):
+    global ca, engine
+    import crosscoder_amd as ca
+    from crosscoder_amd import engine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -267,15 +407,27 @@ def main():
     one_device = os.environ.get("CC_BENCH_ONE_DEVICE") == "1"
     if one_device:
         local = 0
+    elif local >= torch.cuda.device_count():
+        print(f"bench.py: rank {rank} needs cuda:{local}, {torch.cuda.device_count()} GPUs visible", file=sys.stderr,
+              flush=True)
+        return 2
     torch.cuda.set_device(local)
     sharded_path = world > 1 or args.force_sharded
+    backend = None
     if sharded_path:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
+        pg_timeout = datetime.timedelta(seconds=args.pg_timeout)
         if one_device:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.init_process_group("gloo", rank=rank, world_size=world, timeout=pg_timeout)
         else:
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), rank=rank, world_size=world)
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), rank=rank, world_size=world,
+                                    timeout=pg_timeout)
+        backend = dist.get_backend()
+        if dist.get_world_size() != world:
+            print(f"bench.py: process group has {dist.get_world_size()} ranks, WORLD_SIZE {world}", file=sys.stderr,
+                  flush=True)
+            return 2
     config = args.config if args.config is not None else (2 if world == 1 else 3)
     B, n, d, h_total = CONFIGS[config]
     B = args.batch or B
@@ -313,6 +465,9 @@ def main():
     dom = max(gemms, key=gemms.get)
     engine.TIMER = timer
     timer.only = dom  # the roofline kernel, measured live inside the timed region
+    clk = clock_words(tr)
+    if clk is not None:
+        clk.zero_()
     if sharded_path:
         dist.barrier()
     torch.cuda.synchronize()
@@ -332,6 +487,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
+    clock = effective_clock(clk)
     step_s = elapsed / args.steps
     ms = step_s * 1e3
     rows_per_s = B / step_s  # activations (batch rows) trained per second by the whole job: `value`
@@ -360,6 +516,10 @@ def main():
         "value": round(rows_per_s, 1),
         "unit": "activations/s",
         "n_gpus": world,
+        # the ranks of the process group the collectives ran over (dist.get_world_size()) and its backend
+        # ("nccl" = RCCL); 1 / null for the single-GPU step, which has no collectives
+        "world_size_pg": dist.get_world_size() if sharded_path else 1,
+        "pg_backend": backend,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms, 4),
@@ -392,6 +552,10 @@ def main():
                      "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                      "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
                      "algorithmic_bytes": dom_alg_bytes},
+        # the shader clock over the timed region's roofline launches (DVFS under the package power cap: the same
+        # build runs faster on a box that holds a higher clock, so round-over-round comparisons need it)
+        "effective_sclk_ghz": clock["effective_sclk_ghz"] if clock else None,
+        "clock": clock,
         "hbm": hbm_rows(kern, B, n, d, h_local),
         "last_loss": {k: round(v, 6) for k, v in last.items()},
     }
@@ -401,7 +565,8 @@ def main():
         print(json.dumps(result), flush=True)
     if sharded_path:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

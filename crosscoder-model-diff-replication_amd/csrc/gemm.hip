@@ -574,19 +574,27 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 //   (3) the last workgroup to arrive (device-scope arrival counter, reset by it for the next launch) sums,
 //       per parameter, tile_sum over the tiles (G5 -> W_enc, G4 -> W_dec) and the bias blocks' partials in a
 //       fixed order -- whichever workgroups ran which tiles, the same bits -- into clip_grad_norm_'s
-//       coefficient.
+//       coefficient;
+//   (4) that workgroup also adds its own lifetime -- s_memtime (shader clock) and s_memrealtime (100 MHz) ticks
+//       from its start to the finaliser, which spans the launch: persistent workgroups all start in the first
+//       dispatch wave -- into clock[0] / clock[1] and counts the launch in clock[2], so the host reads the clock
+//       the chip held over the roofline launches (bench.py `effective_sclk_ghz`).
+constexpr int CC_WGRAD_CLOCK_WORDS = 8;  // (floats: the 4 uint64 clock words after the tile sums)
 struct WgradTail {
   RedSeg red[2];
   int red_blocks[2];
   ClipArgs clip;
   unsigned* counter;
   float* tile_sum;  // [2 * nb0]: the per-tile squared sums, dW_dec's tiles first
+  uint64_t* clock;  // [4] after tile_sum's tile sums: shader ticks, 100 MHz ticks, launches, (reserved)
 };
 
 template <bool AKC, bool BKC, int EPI0, int EPI1>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmArgs a0, const GemmArgs a1,
                                                                    const WgradTail tl) {
   __shared__ __attribute__((aligned(16))) char smem[EPI0 == EPI_WGDEC || EPI1 == EPI_WGDEC ? PP_LDS_W : PP_LDS];
+  // (scalar reads, uniform over the workgroup: they stay in SGPRs through the tile loop)
+  const uint64_t clk0 = __builtin_amdgcn_s_memtime(), wall0 = __builtin_amdgcn_s_memrealtime();
   {
     const int grp = threadIdx.x >> 8, t = threadIdx.x & 255;
     float(*red)[RED_COLS] = (float(*)[RED_COLS])(smem + grp * 4 * RED_COLS * sizeof(float));
@@ -644,7 +652,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmAr
     clip_finish<NTHR>(tl.clip, s, (double(*)[NTHR / 64])(smem + 64),
                       (float*)(smem + 64 + 8 * (NTHR / 64) * sizeof(double)));
   }
-  if (threadIdx.x == 0) atomicExch(tl.counter, 0u);
+  if (threadIdx.x == 0) {
+    atomicExch(tl.counter, 0u);
+    const uint64_t clk1 = __builtin_amdgcn_s_memtime(), wall1 = __builtin_amdgcn_s_memrealtime();
+    if (tl.clock) {  // (one writer per launch; launches sharing the words are ordered by their stream)
+      tl.clock[0] += clk1 - clk0;
+      tl.clock[1] += wall1 - wall0;
+      tl.clock[2] += 1;
+    }
+  }
 }
 
 // Launch-form switches.  The product library fixes them; the test-only debug build (-DCC_DEBUG_HOOKS,
@@ -848,7 +864,7 @@ int64_t cc_col_part_rows(int64_t M) { return 2 * ((M + BM - 1) / BM); }
 int64_t cc_wave_parts(int64_t M, int64_t N) { return 8 * n_blocks(M, N, 256); }
 // exactly the partials the weight-gradient GEMMs write (the clip sums all of them)
 int64_t cc_wgrad_parts(int64_t h, int64_t K, int dtype) { return 8 * n_blocks(h, K, pick_bn(K, false, false, dtype)); }
-int64_t cc_wgrad_tile_sums(int64_t h, int64_t K) { return 2 * n_blocks(h, K, 256); }
+int64_t cc_wgrad_tile_sums(int64_t h, int64_t K) { return 2 * n_blocks(h, K, 256) + CC_WGRAD_CLOCK_WORDS; }
 
 int cc_gemm_f32out(const void* A, int a_layout, int64_t lda, const void* Bm, int b_layout, int64_t ldb, float* C,
                    int64_t ldc, int64_t M, int64_t N, int64_t K, int dtype, void* stream) {
@@ -1397,7 +1413,7 @@ static int wgrad_both_tail(const void* actsT, const void* g_reconT, const void* 
                            int dtype, void* stream) {
   const int64_t K = n * d;
   if (!gpre_colpart || !g_b_enc || !sq_b_enc || !loss_colpart || !g_b_dec || !sq_b_dec || !sq || !off || !out ||
-      !counter || !tile_sum)
+      !counter || !tile_sum || !sq_dec || !sq_enc)  // (the clip's W_dec / W_enc sums come from sq_dec / sq_enc's tiles)
     return CC_ERR_NULL;
   if (R_enc <= 0 || R_dec <= 0) return CC_ERR_SHAPE;
   if (nparams != 4) return CC_ERR_SHAPE;  // W_enc, W_dec, b_enc, b_dec: the segments of sq
@@ -1434,6 +1450,7 @@ static int wgrad_both_tail(const void* actsT, const void* g_reconT, const void* 
   tl.clip.zero_mask = zero_mask;
   tl.counter = counter;
   tl.tile_sum = tile_sum;
+  tl.clock = (uint64_t*)(tile_sum + 2 * a0.nbm * a0.nbn);  // (2 * nb0 is even: 8-byte aligned)
   a0.tile_ctr = tile_ctr;
 #ifdef CC_DEBUG_HOOKS
   debug_wave_sync(a0, (hipStream_t)stream);

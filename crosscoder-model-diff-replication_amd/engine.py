@@ -243,6 +243,7 @@ class StepWorkspace:
         self.sq = E(self.sq_off[-1])
         self.clip_out = E(8)
         self.tile_sum = E(ops.wgrad_tile_sums(h, K))  # per-tile squared sums of the fused G4G5 + grad tail
+        ops.wgrad_clock(self.tile_sum).zero_()  # + the clock words the launch accumulates (bench: effective sclk)
         # per-XCD tile counters of the persistent G1 / G3 / G4G5 launches (dynamic tile order, DYNAMIC_TILES);
         # every launch leaves its counters at zero
         self.tile_ctr = torch.zeros(3, ops.TILE_CTR_WORDS, dtype=torch.int32, device=device)

@@ -440,8 +440,24 @@ def wgrad_both_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, grad_d
 
 
 def wgrad_tile_sums(h, K):
-    """floats of the per-tile squared-sum scratch of wgrad_both_clip_t / wgrad_both_sums_t"""
+    """floats of the per-tile squared-sum scratch of wgrad_both_clip_t / wgrad_both_sums_t (the tile sums, then the
+    launch clock words: see wgrad_clock)"""
     return int(lib().cc_wgrad_tile_sums(h, K))
+
+
+WGRAD_CLOCK_WORDS = 8  # floats at the end of the tile-sum scratch: 4 uint64 clock words (gemm.hip WgradTail::clock)
+
+
+def wgrad_clock(tile_sum):
+    """The clock words the fused G4G5 launches accumulate at the end of their tile-sum scratch, as a view
+    [shader-clock ticks, 100 MHz ticks, launches, reserved] (int64; zero them to start a window)."""
+    return tile_sum[-WGRAD_CLOCK_WORDS:].view(torch.int64)
+
+
+def _check_tile_sum(tile_sum, h, K):
+    if tile_sum.dtype != torch.float32 or not tile_sum.is_contiguous() or tile_sum.numel() < wgrad_tile_sums(h, K):
+        raise ValueError(f"tile_sum must be a contiguous fp32 buffer of >= {wgrad_tile_sums(h, K)} floats "
+                         f"(cc_wgrad_tile_sums({h}, {K})), got {tuple(tile_sum.shape)} {tile_sum.dtype}")
 
 
 def wgrad_both_clip_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, grad_dec, sq_dec, g_preT, xT, grad_enc,
@@ -450,6 +466,7 @@ def wgrad_both_clip_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, g
     """wgrad_both_t + grad_tail in one launch (the bias sums before the GEMM tiles, the clip coefficient
     in the last workgroup); same outputs."""
     h, B = actsT.shape
+    _check_tile_sum(tile_sum, h, n * d)
     arr = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
     check(lib().cc_wgrad_both_clip_t(
         _ptr(actsT), _ptr(g_reconT), _ptr(W_dec_hk), _ptr(norms), _ptr(colsum_acts), l1_scale, _ptr(grad_dec),
@@ -464,6 +481,7 @@ def wgrad_both_sums_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, g
                       counter, tile_sum, zero_mask=0, tile_ctr=None):
     """wgrad_both_t + grad_tail_sums in one launch (the latent-sharded step); same outputs."""
     h, B = actsT.shape
+    _check_tile_sum(tile_sum, h, n * d)
     arr = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
     check(lib().cc_wgrad_both_sums_t(
         _ptr(actsT), _ptr(g_reconT), _ptr(W_dec_hk), _ptr(norms), _ptr(colsum_acts), l1_scale, _ptr(grad_dec),

@@ -95,3 +95,23 @@ def test_sharded_world2_on_one_gpu_matches_trainer(gpu, comm, tmp_path):
     saved = torch.load(ck / "0.pt", weights_only=True)
     for k in ref_sd:
         assert torch.equal(saved[k], sd[k])
+
+
+def test_bench_gpus2_rehearsal_launches_its_own_ranks():
+    """`bench.py --gpus 2` without a torchrun wrapper starts 2 ranks itself (here both on
+    cuda:0 with gloo collectives, CC_BENCH_ONE_DEVICE=1) and prints ONE line with n_gpus 2 from a 2-rank group."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(CC_BENCH_ONE_DEVICE="1", PYTHONDONTWRITEBYTECODE="1")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--config", "2", "--steps", "2",
+                        "--warmup", "1", "--no-cpu-baseline", "--deadline", "200"], capture_output=True, text=True,
+                       env=env, timeout=260, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    (line,) = [json.loads(s) for s in p.stdout.splitlines() if s.startswith("{")]
+    assert line["n_gpus"] == 2 and line["world_size_pg"] == 2 and line["pg_backend"] == "gloo"
+    assert line["config"]["dict_size"] == 16384 and "8192 latents per GPU" in line["config"]["workload"]
+    assert math.isfinite(line["value"]) and line["value"] > 0
