@@ -78,7 +78,7 @@ SIGNATURES = {
     "cc_wgrad_both_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_wgrad_tile_sums": (_i64, [_i64, _i64]),
     "cc_wgrad_both_clip_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p,
-                                  _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_i64), _i, _f, _i, _p, _p, _p, _p, _i, _p]),
+                                  _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_i64), _i, _f, _i, _p, _p, _p, _p, _p, _i, _p]),
     "cc_wgrad_both_sums_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p,
                                   _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_i64), _i, _i, _p, _p, _p, _p, _i, _p]),
     "cc_wgrad_both": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),

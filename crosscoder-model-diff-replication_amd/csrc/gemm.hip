@@ -1403,6 +1403,13 @@ int cc_wgrad_both_t(const void* actsT, const void* g_reconT, const void* W_dec, 
   return CC_OK;
 }
 
+// (step_kernels.hip, library-internal: cc_grad_tail with the step's abort word)
+extern "C" int cc_grad_tail_abort(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,
+                                  const float* loss_colpart, int64_t R_dec, int64_t K, void* g_b_dec, float* sq_b_dec,
+                                  int dtype, const float* sq, const int64_t* off, int nparams, float max_norm,
+                                  int emulate_bf16, float* clip_out, uint32_t* counter, const uint32_t* abort,
+                                  void* stream);
+
 static int wgrad_both_tail(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
                            const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_preT,
                            const void* xT, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
@@ -1410,7 +1417,7 @@ static int wgrad_both_tail(const void* actsT, const void* g_reconT, const void* 
                            const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
                            const int64_t* off, int nparams, float max_norm, int emulate_bf16, int sums_only,
                            int zero_mask, float* out, uint32_t* counter, float* tile_sum, uint32_t* tile_ctr,
-                           int dtype, void* stream) {
+                           const uint32_t* abort, int dtype, void* stream) {
   const int64_t K = n * d;
   if (!gpre_colpart || !g_b_enc || !sq_b_enc || !loss_colpart || !g_b_dec || !sq_b_dec || !sq || !off || !out ||
       !counter || !tile_sum || !sq_dec || !sq_enc)  // (the clip's W_dec / W_enc sums come from sq_dec / sq_enc's tiles)
@@ -1430,8 +1437,8 @@ static int wgrad_both_tail(const void* actsT, const void* g_reconT, const void* 
     if (sums_only)
       return cc_grad_tail_sums(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec, sq_b_dec,
                                dtype, sq, off, nparams, zero_mask, out, counter, stream);
-    return cc_grad_tail(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec, sq_b_dec, dtype,
-                        sq, off, nparams, max_norm, emulate_bf16, out, counter, stream);
+    return cc_grad_tail_abort(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec, sq_b_dec,
+                              dtype, sq, off, nparams, max_norm, emulate_bf16, out, counter, abort, stream);
   }
   a0.nbm = a1.nbm = (a0.M + BM - 1) / BM;
   a0.nbn = a1.nbn = (a0.N + 255) / 256;
@@ -1448,6 +1455,7 @@ static int wgrad_both_tail(const void* actsT, const void* g_reconT, const void* 
   tl.clip.out = out;
   tl.clip.sums_only = sums_only;
   tl.clip.zero_mask = zero_mask;
+  tl.clip.abort = abort;
   tl.counter = counter;
   tl.tile_sum = tile_sum;
   tl.clock = (uint64_t*)(tile_sum + 2 * a0.nbm * a0.nbn);  // (2 * nb0 is even: 8-byte aligned)
@@ -1470,11 +1478,12 @@ int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_
                          const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
                          const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
                          const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
-                         uint32_t* counter, float* tile_sum, uint32_t* tile_ctr, int dtype, void* stream) {
+                         uint32_t* counter, float* tile_sum, uint32_t* tile_ctr, const uint32_t* abort_flag, int dtype,
+                         void* stream) {
   return wgrad_both_tail(actsT, g_reconT, W_dec, inv_norms, colsum_acts, l1_scale, grad_W_dec, sq_dec, g_preT, xT,
                          grad_W_enc, sq_enc, B, h, n, d, gpre_colpart, R_enc, g_b_enc, sq_b_enc, loss_colpart, R_dec,
                          g_b_dec, sq_b_dec, sq, off, nparams, max_norm, emulate_bf16, 0, 0, clip_out, counter, tile_sum,
-                         tile_ctr, dtype, stream);
+                         tile_ctr, abort_flag, dtype, stream);
 }
 
 int cc_wgrad_both_sums_t(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
@@ -1487,7 +1496,7 @@ int cc_wgrad_both_sums_t(const void* actsT, const void* g_reconT, const void* W_
   return wgrad_both_tail(actsT, g_reconT, W_dec, inv_norms, colsum_acts, l1_scale, grad_W_dec, sq_dec, g_preT, xT,
                          grad_W_enc, sq_enc, B, h, n, d, gpre_colpart, R_enc, g_b_enc, sq_b_enc, loss_colpart, R_dec,
                          g_b_dec, sq_b_dec, sq, off, nparams, 0.f, 0, 1, zero_mask, out, counter, tile_sum, tile_ctr,
-                         dtype, stream);
+                         nullptr, dtype, stream);
 }
 
 int cc_wgrad_both(const void* acts, const void* g_recon, const void* W_dec, const float* inv_norms,

@@ -172,8 +172,11 @@ CC_DEV constexpr int mask_bit_pos(int i, int j, int e) { return 8 * (i & 1) + 2 
 // a negative bf16 is a negative int16; max(round(t), 0) == round(max(t, 0)) bit for bit), the mask bits by one
 // pk_min_u16(pair, 1) or-ed into the pair's word, the l0 count as the popcount of the bits, the column sums of
 // the stored values in pairs.  The same outputs as enc_dacts_core's general arithmetic with half its VALU
-// instructions (a NaN pre-activation is the exception: it stays NaN here -- as torch.relu keeps it -- where
-// fmaxf made it 0).
+// instructions.  NaN pre-activations are the exception, and their sign decides: a NaN with the sign bit clear is a
+// positive int16, so it stays NaN (as torch.relu keeps every NaN) and sets its mask bit; a NaN with the sign bit set
+// is a negative int16 and becomes +0 (mask bit clear), as the general form's fmaxf turns every NaN into 0.  Neither
+// form matches torch for every NaN; a NaN pre-activation means the step's inputs or weights are already non-finite
+// (the reference then trains on NaN too), and no fixture pins it.
 template <int BNT, class IO>
 CC_DEV void enc_fast_core(const GemmArgs& args, const f32x4 (&acc)[WaveGeom<BNT>::TM][WaveGeom<BNT>::TN],
                           const FragGeom<BNT>& fg, const IO& io, int tm, int n0, int wr, int lane, int wave_slot,

@@ -589,14 +589,23 @@ struct TileLoop {
 };
 
 // GemmArgs::wait_ctr: thread 0 polls the producer's counter (s_sleep between reads), then one agent-scope acquire
-// (drops this XCD's stale L2 lines of the producer's output) and the barrier.  Bounded: every wave exits.
-CC_DEV void pp_wait_ready(const GemmArgs& a) {
-  if (!a.wait_ctr) return;
+// (drops this XCD's stale L2 lines of the producer's output) and the barrier.  Bounded: every wave exits.  Returns
+// false when the bound expired: the producer's output is not complete, so the caller runs NO tile of its own (it
+// must not compute on a half-updated operand) and the host-visible error word is set -- the same step's host read
+// raises, and the step's clip finaliser (ClipArgs::abort, the same word) keeps every Adam launch of the step from
+// applying an update.
+// (smem: the broadcast word is the tile-claim slot, PP_SLOT, which no DMA writes before the first tile's prologue
+// barrier)
+CC_DEV bool pp_wait_ready(const GemmArgs& a, char* smem) {
+  if (!a.wait_ctr) return true;
+  int& ok = *(int*)(smem + PP_SLOT);
   if (threadIdx.x == 0) {
     const uint64_t t0 = wall_clock64();  // (the 100 MHz constant clock: the bound does not depend on sclk)
+    int ready = 1;
     while ((int)(__hip_atomic_load(a.wait_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.wait_target) < 0) {
       if (wall_clock64() - t0 > 100000000ull) {  // (1 s)
         if (a.wait_err) __hip_atomic_store(a.wait_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ready = 0;
         break;
       }
       // ~0.6 us between reads: every workgroup of the launch polls the one word (at 0.25 us they would put
@@ -604,8 +613,10 @@ CC_DEV void pp_wait_ready(const GemmArgs& a) {
       __builtin_amdgcn_s_sleep(20);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    ok = ready;
   }
   __syncthreads();
+  return ok != 0;
 }
 
 // The launch's prologue reduction (GemmArgs::pre: reduce_rows' two phases, the same bits as cc_reduce_rows):
@@ -663,7 +674,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(16))) char smem[EPI == EPI_WGDEC ? PP_LDS_W : PP_LDS];
   pp_prologue_reduce(args, smem, gridDim.x);
   pp_prologue_loss_tail(args, smem);
-  pp_wait_ready(args);
+  if (!pp_wait_ready(args, smem)) {
+    // no tile runs, but the launch still makes its claims on the per-XCD counters (each launch leaves them at 0)
+    for (TileLoop L(args.nbm * args.nbn, args.tile_ctr); L.more();) {
+      L.begin();
+      L.advance(smem);
+      __syncthreads();
+    }
+    return;
+  }
   for (TileLoop L(args.nbm * args.nbn, args.tile_ctr); L.more();) {
     pp_tile<AKC, BKC, EPI, FAST>(args, smem, L.begin(), pp_opaque_tid());
     pp_tile_boundary();
@@ -700,11 +719,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_main_splitk_kernel(const Gemm
   const int nb0 = a0.nbm * a0.nbn;
   if ((int)blockIdx.x < nb0) {
     pp_prologue_reduce(a0, smem, nb0);
-    pp_wait_ready(a0);
-    pp_tile<AKC, BKC, EPI, FAST>(a0, smem, blockIdx.x);
+    if (pp_wait_ready(a0, smem)) pp_tile<AKC, BKC, EPI, FAST>(a0, smem, blockIdx.x);
     return;
   }
-  pp_wait_ready(t);
+  if (!pp_wait_ready(t, smem)) return;
   const int b = blockIdx.x - nb0;
   const int s = b / (t.nbm * t.nbn);
   const int tb = b - s * t.nbm * t.nbn;
@@ -727,7 +745,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_splitk_kernel(const GemmArgs 
   // config 2, vs 80-134 us with each split pinned to one XCD: s = b % 8)
   const int s = blockIdx.x / (args.nbm * args.nbn);
   const int tb = blockIdx.x - s * args.nbm * args.nbn;
-  pp_wait_ready(args);
+  if (!pp_wait_ready(args, smem)) return;
   GemmArgs a = args;
   a.k_step0 = s * steps_per;
   a.k_steps = nk_total - a.k_step0 < steps_per ? nk_total - a.k_step0 : steps_per;

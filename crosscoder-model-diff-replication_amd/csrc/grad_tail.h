@@ -94,7 +94,14 @@ struct ClipArgs {
   float* out;
   int sums_only;   // cc_segment_sums: out[p] = the raw per-parameter sum (0 where zero_mask has bit p)
   int zero_mask;
+  // the step's abort word (a host-mapped word an earlier launch of the step sets when it could not run, e.g. G2's
+  // in-kernel wait timing out): when set, the coefficient is written as CC_CLIP_ABORTED and every Adam launch
+  // that reads it leaves p / m / v untouched (nullptr: none)
+  const unsigned* abort;
 };
+// clip_out[0] of a step that must not update the parameters: clip_grad_norm_'s coefficient min(1, max_norm /
+// (total + 1e-6)) is never negative (NaN / inf norms give NaN / 0), so a negative value is free to mean it
+#define CC_CLIP_ABORTED (-1.0f)
 // One block of NT threads; red / norms: LDS scratch of the caller (the GEMM kernel that runs it as
 // its last workgroup's tail has no LDS to spare for static arrays of its own)
 template <int NT>
@@ -127,6 +134,9 @@ CC_DEV void clip_body(const ClipArgs& a, double (*red)[NT / 64], float* norms) {
 // the waves, per-parameter norms (bf16-rounded as torch's _foreach_norm on bf16), total, coefficient.
 template <int NT>
 CC_DEV void clip_finish(const ClipArgs& a, const double* s, double (*red)[NT / 64], float* norms) {
+  // (the abort word may live in host memory: its load is issued first, its latency hides under the reductions)
+  const unsigned aborted =
+      threadIdx.x == 0 && a.abort ? __hip_atomic_load(a.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
     double t = wave_sum_d(s[p]);
@@ -152,7 +162,7 @@ CC_DEV void clip_finish(const ClipArgs& a, const double* s, double (*red)[NT / 6
   if (threadIdx.x == 0) {
     float total;
     const float coef = clip_coef(norms, a.nparams, a.max_norm, a.emulate_bf16, total);
-    a.out[0] = coef;
+    a.out[0] = aborted ? CC_CLIP_ABORTED : coef;
     a.out[1] = total;
     for (int p = 0; p < a.nparams; ++p) a.out[2 + p] = norms[p];
   }

@@ -464,6 +464,7 @@ __global__ __launch_bounds__(256) void adam_bulk_kernel(const AdamArgs a, int64_
   // the coefficient after the element loads are in flight (its inputs' latency hides under theirs; formed
   // from the squared sums it also stores clip_out, which must not hold the loads back)
   const float coef = adam_coef_block(a);
+  if (coef < 0.f) return;  // CC_CLIP_ABORTED: the step's update is not applied
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t c = c0 + u * 256;
@@ -483,7 +484,10 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   // workgroup that holds a CU's whole LDS -- the decoder half runs beside G1)
   const float coef = adam_coef(a);
   const int64_t stride = (int64_t)gridDim.x * 256 * 8;
-  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8; i < a.numel; i += stride) {
+  // (CC_CLIP_ABORTED: the step's update is not applied -- p / m / v and the norm partials stay as they are --
+  // but the done count still arrives)
+  const int64_t numel = coef < 0.f ? 0 : a.numel;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8; i < numel; i += stride) {
     float p[8], g[8], m[8], v[8];
     const bool full = i + 8 <= a.numel;
     if (full) {
@@ -555,13 +559,14 @@ CC_DEV void adam_pipe_load(const AdamArgs& a, int64_t i, bf16x8& p, bf16x8& g, b
 __global__ __launch_bounds__(256) void adam_pipe_kernel(const AdamArgs a) {
   const float coef = adam_coef(a);
   const int64_t stride = (int64_t)gridDim.x * 256 * 8;
+  const int64_t numel = coef < 0.f ? 0 : a.numel;  // (CC_CLIP_ABORTED: as adam_kernel)
   int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
   bf16x8 p, g, m, v;
-  if (i < a.numel) adam_pipe_load(a, i, p, g, m, v);
-  for (; i < a.numel; i += stride) {
+  if (i < numel) adam_pipe_load(a, i, p, g, m, v);
+  for (; i < numel; i += stride) {
     const int64_t nx = i + stride;
     bf16x8 p2 = p, g2 = g, m2 = m, v2 = v;
-    if (nx < a.numel) adam_pipe_load(a, nx, p2, g2, m2, v2);
+    if (nx < numel) adam_pipe_load(a, nx, p2, g2, m2, v2);
     float q = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -599,6 +604,7 @@ __global__ __launch_bounds__(256) void adam_dec_tr_kernel(const AdamArgs a, int 
                                                           float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) char tile[64 * 128];
   const float coef = adam_coef(a);
+  if (coef < 0.f) return;  // CC_CLIP_ABORTED: the step's update is not applied
   const int nr = (h + 63) / 64, nblk = K / 64, ntiles = nr * nblk;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g4 = lane >> 4, i = lane & 15, q4 = i >> 2, p4 = i & 3;
@@ -1008,7 +1014,8 @@ extern "C" {
 static int grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,
                      const float* loss_colpart, int64_t R_dec, int64_t K, void* g_b_dec, float* sq_b_dec, int dtype,
                      const float* sq, const int64_t* off, int nparams, float max_norm, int emulate_bf16,
-                     int sums_only, int zero_mask, float* out, uint32_t* counter, void* stream) {
+                     int sums_only, int zero_mask, float* out, uint32_t* counter, void* stream,
+                     const uint32_t* abort = nullptr) {
   if (!gpre_colpart || !g_b_enc || !sq_b_enc || !loss_colpart || !g_b_dec || !sq_b_dec || !sq || !off || !out ||
       !counter)
     return CC_ERR_NULL;
@@ -1027,6 +1034,7 @@ static int grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* 
   a.clip.out = out;
   a.clip.sums_only = sums_only;
   a.clip.zero_mask = zero_mask;
+  a.clip.abort = abort;
   a.counter = counter;
   dim3 grid((unsigned)((a.red_blocks[0] + a.red_blocks[1] + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
@@ -1041,6 +1049,15 @@ int cc_grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_
                  uint32_t* counter, void* stream) {
   return grad_tail(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec, sq_b_dec, dtype, sq,
                    off, nparams, max_norm, emulate_bf16, 0, 0, clip_out, counter, stream);
+}
+
+// cc_grad_tail with the step's abort word (ClipArgs::abort): the fused G4G5 entry's fallback (library-internal)
+int cc_grad_tail_abort(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,
+                       const float* loss_colpart, int64_t R_dec, int64_t K, void* g_b_dec, float* sq_b_dec, int dtype,
+                       const float* sq, const int64_t* off, int nparams, float max_norm, int emulate_bf16,
+                       float* clip_out, uint32_t* counter, const uint32_t* abort, void* stream) {
+  return grad_tail(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec, sq_b_dec, dtype, sq,
+                   off, nparams, max_norm, emulate_bf16, 0, 0, clip_out, counter, stream, abort);
 }
 
 int cc_grad_tail_sums(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,

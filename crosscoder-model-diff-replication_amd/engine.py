@@ -376,13 +376,29 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
             loss_finalize(ws)
 
 
+STEP_ABORTED_MSG = ("crosscoder_hip: the step was aborted -- G2's in-kernel wait for the previous step's decoder-half "
+                    "Adam (side stream) timed out, so G2 ran none of its tiles and this step's Adam launches applied no "
+                    "update (params and Adam moments are those before the step; its batch was consumed).  If that "
+                    "Adam was still running when this step's backward wrote its gradients, the decoder half of the "
+                    "previous update may be inconsistent: reload a checkpoint.")
+
+
+def check_step_abort(ws):
+    """Raise (once: the word is cleared) if a G2 launch of this workspace timed out in its in-kernel wait.  The
+    step's clip finaliser (after G3, which wrote the loss scalars the host just read) still has to see the word, so
+    the device is drained before it is cleared (an error path: the sync costs nothing that matters)."""
+    if ws is not None and ws.wait_err is not None and ws.wait_err.u32[0]:
+        torch.cuda.synchronize(ws.x.device)
+        ws.wait_err.u32[0] = 0
+        raise RuntimeError(STEP_ABORTED_MSG)
+
+
 def _wait_err(ws):
-    """The mapped host word a G2 launch sets if its in-kernel wait times out (raised here, by the next forward)."""
+    """The mapped host word a G2 launch sets if its in-kernel wait times out.  The Trainer raises in the same step
+    (check_step_abort after its loss read); other callers see it here, at the next forward, at the latest."""
     if ws.wait_err is None:
         ws.wait_err = _hip.MappedHostBuffer(4)
-    if ws.wait_err.u32[0]:
-        raise RuntimeError("crosscoder_hip: G2's in-kernel wait for the decoder-half Adam timed out (a step's results "
-                           "are invalid)")
+    check_step_abort(ws)
     return ws.wait_err.device_ptr
 
 
@@ -546,7 +562,8 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
                                   G.W_dec_hk, ws.sq_slice(1), ws.g_pre_t, ws.x_t, G.W_enc_hk, ws.sq_slice(0), n, d,
                                   ws.gpre_colpart, G.b_enc, ws.sq_slice(2), loss_colpart(ws), G.b_dec_flat,
                                   ws.sq_slice(3), ws.sq, ws.sq_off, clip, ws.dtype == torch.bfloat16, ws.clip_out,
-                                  ws.tail_ctr[1:2], ws.tile_sum, tile_ctr=_tile_ctr(ws, 2))
+                                  ws.tail_ctr[1:2], ws.tile_sum, tile_ctr=_tile_ctr(ws, 2),
+                                  abort_ptr=ws.wait_err.device_ptr if ws.wait_err is not None else None)
         ws.clip_ready = True
         return
     with _span("G4G5_wgrad"):

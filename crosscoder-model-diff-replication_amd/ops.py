@@ -32,6 +32,11 @@ def _stream(t):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
+def _vptr(p):
+    """an optional raw device address (int, ctypes.c_void_p or None) as a c_void_p"""
+    return p if isinstance(p, ctypes.c_void_p) else ctypes.c_void_p(p or 0)
+
+
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -462,9 +467,10 @@ def _check_tile_sum(tile_sum, h, K):
 
 def wgrad_both_clip_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, grad_dec, sq_dec, g_preT, xT, grad_enc,
                       sq_enc, n, d, gpre_colpart, g_b_enc, sq_b_enc, loss_colpart, g_b_dec, sq_b_dec, sq, offsets,
-                      max_norm, emulate_bf16, out, counter, tile_sum, tile_ctr=None):
+                      max_norm, emulate_bf16, out, counter, tile_sum, tile_ctr=None, abort_ptr=None):
     """wgrad_both_t + grad_tail in one launch (the bias sums before the GEMM tiles, the clip coefficient
-    in the last workgroup); same outputs."""
+    in the last workgroup); same outputs.  abort_ptr: device address of the step's abort word (when set, out[0] is
+    written as CLIP_ABORTED and the Adam launches reading it apply nothing)."""
     h, B = actsT.shape
     _check_tile_sum(tile_sum, h, n * d)
     arr = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
@@ -473,7 +479,10 @@ def wgrad_both_clip_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, g
         _ptr(sq_dec), _ptr(g_preT), _ptr(xT), _ptr(grad_enc), _ptr(sq_enc), B, h, n, d, _ptr(gpre_colpart),
         gpre_colpart.shape[0], _ptr(g_b_enc), _ptr(sq_b_enc), _ptr(loss_colpart), loss_colpart.shape[0], _ptr(g_b_dec),
         _ptr(sq_b_dec), _ptr(sq), arr, len(offsets) - 1, max_norm, int(emulate_bf16), _ptr(out), _ptr(counter),
-        _ptr(tile_sum), _ctr(tile_ctr), dtype_code(actsT.dtype), _stream(actsT)))
+        _ptr(tile_sum), _ctr(tile_ctr), _vptr(abort_ptr), dtype_code(actsT.dtype), _stream(actsT)))
+
+
+CLIP_ABORTED = -1.0  # clip_out[0] of a step whose update was not applied (include/crosscoder_hip.h)
 
 
 def wgrad_both_sums_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, grad_dec, sq_dec, g_preT, xT, grad_enc,

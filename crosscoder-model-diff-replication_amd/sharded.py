@@ -342,11 +342,23 @@ class ShardedTrainer:
 
     def train(self):
         """trainer.py:69-82 over the shards (logging and checkpoints on rank 0).  The reference saves in a
-        `finally:` (trainer.py:81-82).  Here the save is a collective, so it runs where every rank leaves the
-        loop the same way: on normal completion, and on KeyboardInterrupt (torchrun forwards SIGINT to every
-        rank), after which the interrupt is re-raised.  Any other exception may be one rank's alone: a save
-        would then wait forever for the others, so it propagates without the final checkpoint."""
+        `finally:` (trainer.py:81-82).  Here the save is a collective, so it must run where every rank leaves the
+        loop at the SAME step.  SIGINT (torchrun forwards it to every rank, not necessarily between the same two
+        collectives) therefore only sets a flag; every `stop_check_every` steps (cfg, default 10) the ranks agree
+        on it with a one-word all_reduce(MAX) at a step boundary -- never inside a step's collectives, never
+        between the two Adam halves -- then all of them save and raise KeyboardInterrupt.  Normal completion
+        saves too.  Any other exception may be one rank's alone: a save would then wait forever for the others,
+        so it propagates without the final checkpoint."""
+        import signal
+        import threading
+
         self.step_counter = 0
+        stop = [False]
+        prev = None
+        if threading.current_thread() is threading.main_thread():
+            prev = signal.signal(signal.SIGINT, lambda signum, frame: stop.__setitem__(0, True))
+        every = max(1, int(self.cfg.get("stop_check_every", 10)))
+        interrupted = False
         try:
             for i in range(self.total_steps):
                 loss_dict = self.step()
@@ -354,13 +366,30 @@ class ShardedTrainer:
                     self.log(loss_dict)
                 if (i + 1) % self.cfg["save_every"] == 0:
                     self.save()
-        except KeyboardInterrupt:
-            self.save()
-            raise
+                if (i + 1) % every == 0 and self.agree_stop(stop[0]):
+                    interrupted = True
+                    break
+        finally:
+            if prev is not None:
+                signal.signal(signal.SIGINT, prev)
         self.save()
+        if interrupted:
+            raise KeyboardInterrupt
+
+    def agree_stop(self, flag):
+        """True on every rank if any rank's stop flag is set (a step-boundary collective of one word)."""
+        return agree_stop(flag, self.group)
 
     def gather_state_dict(self, dst=None):
         return gather_state_dict(self.crosscoder, self.cfg["dict_size"], self.group, dst=dst)
+
+
+def agree_stop(flag, group=None):
+    """all_reduce(MAX) of one stop flag over the group: True on every rank if any rank's flag is set."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([1.0 if flag else 0.0], device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return t.item() > 0
 
 
 def gather_state_dict(cc, h_total, group=None, dst=None):

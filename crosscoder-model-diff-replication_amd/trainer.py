@@ -89,6 +89,7 @@ class Trainer:
         self._mapped = None  # mapped host words the step's loss tail writes (allocated on the first step)
         self._seq = 0
         self._side = None  # stream of the decoder half's Adam (created on the first step)
+        self._last_ws = None  # the last step's workspace (its G2 abort word, engine.check_step_abort)
 
     def lr_lambda(self, step):
         if step < 0.8 * self.total_steps:
@@ -138,6 +139,7 @@ class Trainer:
                              side_stream=side)
         self.scheduler.step()
         self._last_l1c = l1c
+        self._last_ws = ws
         return ws.scalars, done
 
     def _side_stream(self):
@@ -152,6 +154,20 @@ class Trainer:
         Adam may still run on the side stream, and its last rows are deferred to the next reader, which
         launches them; CrossCoder's accessors and optimizer.state do this by themselves)."""
         self.crosscoder.arena().wait_pending()
+        self._check_abort()
+
+    def _check_abort(self):
+        """Raise engine.STEP_ABORTED_MSG if the last step's G2 timed out waiting for the side-stream Adam; its
+        launches applied no update, so the optimizer's step count and the LR schedule are rolled back."""
+        try:
+            engine.check_step_abort(self._last_ws)
+        except RuntimeError:
+            self.optimizer.t -= 1
+            self.scheduler.last_epoch -= 1
+            lr = self.scheduler.base_lr * self.lr_lambda(self.scheduler.last_epoch)
+            self.optimizer.param_groups[0]["lr"] = lr
+            self.scheduler._last_lr = [lr]
+            raise
 
     def step(self):
         if self._mapped is None:
@@ -159,6 +175,7 @@ class Trainer:
         self._seq = (self._seq + 1) & 0xFFFFFFFF or 1
         self._launch_step(None, host=self._mapped, seq=self._seq)
         self._mapped.wait(8, self._seq)
+        self._check_abort()  # (G2 timed out: raise in THIS step; its Adam launches applied nothing)
         s = [float(v) for v in self._mapped.f32[:6]]
         l1c = self._last_l1c
         dt = self.crosscoder.dtype

@@ -333,8 +333,13 @@ int cc_grad_tail(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_
  * the order of its fp64 squared-sum accumulation).  nparams must be 4 (sq's segments W_enc, W_dec, b_enc,
  * b_dec); tile_sum: fp32 scratch of cc_wgrad_tile_sums(h, n*d) floats (each output tile's squared sum, which
  * the last workgroup adds in a fixed order: the coefficient's bits do not depend on which workgroup ran which
- * tile); tile_ctr: as cc_encode_fwd_t.  Where the ping-pong GEMM does not serve the shape (or dtype != bf16)
- * it runs exactly those two entries. */
+ * tile) followed by 4 uint64 words the launch accumulates -- shader-clock ticks, 100 MHz ticks and the launch
+ * count over the lifetime of its last workgroup (the clock the chip held; zero them to start a window); tile_ctr:
+ * as cc_encode_fwd_t.  abort_flag (optional, host-mapped or device word): when nonzero at the clip finaliser, clip_out[0] is
+ * written as -1 (CC_CLIP_ABORTED: clip_grad_norm_'s coefficient is never negative) and every cc_adam_step /
+ * cc_adam_dec_norms launch that reads that coefficient leaves p, m, v untouched -- the step's update is not applied
+ * (the single-GPU step passes the word its G2 launch sets when its in-kernel wait times out).  Where the ping-pong
+ * GEMM does not serve the shape (or dtype != bf16) it runs exactly those two entries. */
 int64_t cc_wgrad_tile_sums(int64_t h, int64_t K);
 int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
                          const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_preT,
@@ -342,7 +347,8 @@ int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_
                          const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
                          const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
                          const int64_t* off, int nparams, float max_norm, int emulate_bf16, float* clip_out,
-                         uint32_t* counter, float* tile_sum, uint32_t* tile_ctr, int dtype, void* stream);
+                         uint32_t* counter, float* tile_sum, uint32_t* tile_ctr, const uint32_t* abort_flag, int dtype,
+                         void* stream);
 /* cc_wgrad_both_clip_t whose finaliser is cc_segment_sums instead of the clip (the latent-sharded step,
  * trainer.py:45-46 split across ranks): out[p] = the per-parameter squared sums, 0 where bit p of
  * zero_mask is set, to be all-reduced.  Equal to cc_wgrad_both_t + cc_grad_tail_sums (the sums up to the
@@ -371,7 +377,8 @@ int cc_segment_sums(const float* sq, const int64_t* off, int nparams, int zero_m
  * over `numel` flat elements; step = the Adam step count AFTER increment; lr from LambdaLR.
  * dtype-rounding between torch's ops is reproduced (bf16 state like the reference).
  * max_blocks > 0: grid-stride over at most that many 256-thread workgroups (for an update that
- * runs beside a GEMM on another stream); 0: one pass, one 8-element chunk per thread. */
+ * runs beside a GEMM on another stream); 0: one pass, one 8-element chunk per thread.
+ * coef[0] < 0 (CC_CLIP_ABORTED, see cc_wgrad_both_clip_t): nothing is updated (a done count still arrives). */
 int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const float* coef, double lr,
                  double beta1, double beta2, double eps, int64_t step, int64_t max_blocks, int dtype, void* stream);
 

@@ -551,10 +551,14 @@ def test_delayed_side_stream_adam_still_orders_the_norm_readers(gpu, dbg_lib, mo
     assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
 
 
-def test_g2_kernel_wait_timeout_is_loud(gpu, monkeypatch):
-    """G2's in-kernel wait for the side-stream Adam is bounded (1 s of the constant 100 MHz clock): with the done
-    counter pushed 2^20 below any target the Adam can reach, G2 gives up, sets the workspace's mapped error word,
-    and the next forward raises instead of training on a half-updated W_dec.  (Pushing the counter, not holding the
+def test_g2_kernel_wait_timeout_aborts_the_same_step(gpu, monkeypatch):
+    """G2's in-kernel wait for the side-stream Adam is bounded (1 s of the constant 100 MHz clock).  With the done
+    counter pushed 2^20 below any target the Adam can reach (a producer that never arrives), G2 gives up, runs NONE of
+    its tiles, sets the mapped error word, and THE SAME tr.step() raises.
+    Its clip finaliser turns the coefficient into CC_CLIP_ABORTED, so none of the step's Adam launches (encoder half,
+    side-stream decoder half, the deferred rows) applies anything: params and both moments stay bit for bit those
+    before the step, the optimizer's step count and LR schedule are rolled back, and -- the counter restored -- the
+    next step trains exactly like a trainer that skipped the aborted batch.  (Pushing the counter, not holding the
     side stream back: a side stream that shares a hardware queue with the compute stream runs its Adam before G2
     whatever it waits for.)"""
     from crosscoder_amd import engine
@@ -562,17 +566,46 @@ def test_g2_kernel_wait_timeout_is_loud(gpu, monkeypatch):
     B, n, d, h = 1024, 2, 256, 2048
     cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
                num_tokens=B * 20, device=str(gpu))
+
+    def snapshot(cc, tr):  # params, exp_avg, exp_avg_sq
+        st = tr.optimizer.state  # (orders after the side-stream Adam, launches any deferred rows)
+        out = [t.detach().clone() for p in cc.parameters() for t in (p, st[p]["exp_avg"], st[p]["exp_avg_sq"])]
+        torch.cuda.synchronize()
+        return out
+
+    # the reference run: the same crosscoder trained on batches 0 and 2 (batch 1 is consumed by the aborted step)
+    cc2 = ca.CrossCoder(cfg)
+    buf2 = ca.SyntheticBuffer(cfg, rows=B * 4, seed=5)
+    tr2 = ca.Trainer(cfg, buffer=buf2, crosscoder=cc2)
+    r1 = tr2.step()
+    before = snapshot(cc2, tr2)
+    buf2.next_raw()
+    r3 = tr2.step()
+    final_ref = snapshot(cc2, tr2)
+
     cc = ca.CrossCoder(cfg)
     tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 4, seed=5), crosscoder=cc)
-    tr.step()
+    assert tr.step() == r1
+    lr_before = tr.optimizer.param_groups[0]["lr"]
+    # (no parameter accessor here: it would launch the deferred decoder rows itself, and the next G2 would not wait
+    # in its kernel; a device-wide synchronize orders the counter update after the side-stream Adam's arrivals)
     torch.cuda.synchronize()
     ws = cc._workspace(B, step=True)
     ws.adam_done[0] -= 1 << 20
     torch.cuda.synchronize()
-    tr.step()  # (its G2 times out)
-    with pytest.raises(RuntimeError, match="timed out"):
-        tr.step()
+    with pytest.raises(RuntimeError, match="step was aborted"):
+        tr.step()  # (its G2 times out)
+    assert ws.clip_out[0].item() == -1.0  # CC_CLIP_ABORTED
+    for a, b in zip(before, snapshot(cc, tr)):
+        assert torch.equal(a, b)  # no update applied
+    assert tr.optimizer.t == 1 and tr.step_counter == 1
+    assert tr.optimizer.param_groups[0]["lr"] == lr_before and tr.scheduler.last_epoch == 1
+    assert ws.wait_err.u32[0] == 0  # (raised once, cleared)
+    ws.adam_done[0] += 1 << 20
     torch.cuda.synchronize()
+    assert tr.step() == r3
+    for a, b in zip(final_ref, snapshot(cc, tr)):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("B,n,d,h", [(1024, 2, 256, 2048), (512, 4, 128, 1024)])

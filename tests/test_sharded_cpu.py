@@ -4,6 +4,7 @@ reproduce the unsharded oracle step."""
 import os
 import pathlib
 import random
+import signal
 
 import pytest
 import torch
@@ -282,38 +283,82 @@ def test_sharded_init_is_reference_slice_and_gathers_back(enc_dtype, d_in, tmp_p
         assert torch.equal(sd[k], ref[k]) and sd[k].stride() == ref[k].stride(), k
 
 
+class _Loop:
+    """ShardedTrainer.train's collaborators (step / log / save / agree_stop), counted."""
+    total_steps = 8
+    cfg = {"log_every": 100, "save_every": 1000, "stop_check_every": 2}
+
+    def __init__(self, fail_at=None, exc=None, group=None):
+        self.n, self.saved, self.fail_at, self.exc, self.group = 0, 0, fail_at, exc, group
+
+    def step(self):
+        self.n += 1
+        if self.n == self.fail_at:
+            if self.exc is None:
+                os.kill(os.getpid(), signal.SIGINT)  # (the handler train() installed only sets a flag)
+            else:
+                raise self.exc()
+        return {}
+
+    def log(self, d):
+        pass
+
+    def save(self):
+        self.saved += 1
+
+    def agree_stop(self, flag):
+        return sharded.agree_stop(flag, self.group) if self.group is not None else flag
+
+
 def test_sharded_train_final_save_on_interrupt_only():
     """ShardedTrainer.train keeps the reference's final save (trainer.py:81-82) where every rank leaves the loop
-    the same way: normal completion and KeyboardInterrupt (re-raised after the save); another exception, which
-    may be one rank's alone, propagates without the collective save."""
-
-    class Loop:
-        total_steps = 6
-        cfg = {"log_every": 100, "save_every": 1000}
-
-        def __init__(self, fail_at=None, exc=KeyboardInterrupt):
-            self.n, self.saved, self.fail_at, self.exc = 0, 0, fail_at, exc
-
-        def step(self):
-            self.n += 1
-            if self.n == self.fail_at:
-                raise self.exc()
-            return {}
-
-        def log(self, d):
-            pass
-
-        def save(self):
-            self.saved += 1
-
-    done = Loop()
+    at the same step: normal completion, and SIGINT -- which only sets a flag the ranks agree on at the next
+    `stop_check_every` step boundary (never a collective save started from inside a step's
+    collectives) -- after which KeyboardInterrupt is raised.  Another exception, which may be one rank's alone,
+    propagates without the collective save.  The SIGINT handler is restored afterwards."""
+    prev = signal.getsignal(signal.SIGINT)
+    done = _Loop()
     sharded.ShardedTrainer.train(done)
-    assert (done.n, done.saved) == (6, 1)
-    interrupted = Loop(fail_at=3)
+    assert (done.n, done.saved) == (8, 1)
+    interrupted = _Loop(fail_at=3)
     with pytest.raises(KeyboardInterrupt):
         sharded.ShardedTrainer.train(interrupted)
-    assert (interrupted.n, interrupted.saved) == (3, 1)
-    failed = Loop(fail_at=3, exc=RuntimeError)
+    assert (interrupted.n, interrupted.saved) == (4, 1)  # (the step in flight and the next one finish first)
+    failed = _Loop(fail_at=3, exc=RuntimeError)
     with pytest.raises(RuntimeError):
         sharded.ShardedTrainer.train(failed)
     assert failed.saved == 0
+    assert signal.getsignal(signal.SIGINT) is prev
+
+
+def _interrupt_rank(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        loop = _Loop(fail_at=3 if rank == 0 else None, group=None)
+        loop.group = dist.group.WORLD
+        try:
+            sharded.ShardedTrainer.train(loop)
+            q.put((rank, loop.n, loop.saved, "done"))
+        except KeyboardInterrupt:
+            q.put((rank, loop.n, loop.saved, "interrupt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_train_sigint_on_one_rank_stops_all_ranks_at_one_step():
+    """World 2 over gloo: SIGINT reaches rank 0 only, during its step 3; both ranks leave the loop after step 4
+    (the next agreement point), both run the final save and both raise KeyboardInterrupt."""
+    world = 2
+    port = 29000 + random.randint(0, 900)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_interrupt_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == [(0, 4, 1, "interrupt"), (1, 4, 1, "interrupt")]
