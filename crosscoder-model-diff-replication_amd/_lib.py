@@ -64,6 +64,7 @@ SIGNATURES = {
     "cc_decode_fwd": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_decode_ws_floats": (_i64, [_i64, _i64, _i64, _i]),
     "cc_decode_fwd_ws": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
+    "cc_decode_partial": (_i, [_p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_decode_fwd_ws_t": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_loss_fwd_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i, _p]),
     "cc_loss_fwd_bwd_rows": (_i, [_p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i64, _i64, _i, _p]),

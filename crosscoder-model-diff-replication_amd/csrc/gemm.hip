@@ -969,10 +969,32 @@ static bool dec_plan(int64_t B, int64_t h, int64_t K, int dtype, DecPlan& p) {
 // Sum of the S split-K partial slabs (fixed order) into out[m][n] (ldo): the slabs hold each tile
 // in accumulator-fragment order (EPI_SPLIT: tile, wave, fragment, lane -> 4 floats), so the split
 // passes store whole 1-KB pieces; one thread per (tile, wave, fragment, lane).
+// The decoder norms' finaliser as extra blocks of a launch (NormFin::part NULL: none): finaliser block b does rows
+// 256 b .. +255, one per thread (norms_finalize_row) -- the norms are first read after the launch, their partials
+// are complete before.  The finaliser's blocks come FIRST in the grid, so they run beside the launch's own blocks
+// instead of as a tail after them (appended, the split reduction + finaliser took 31 us vs 21 us as two launches).
+struct NormFin {
+  const float* part;
+  int h, n, bpm;
+  float* norms;
+  float* total;
+  float* inv;
+};
+CC_DEV void norm_fin_block(const NormFin& nf, int b) {
+  const int row = b * 256 + (int)threadIdx.x;
+  if (row < nf.h) norms_finalize_row(nf.part, row, nf.n, nf.bpm, nf.norms, nf.total, nf.inv);
+}
+CC_DEV int norm_fin_blocks(const NormFin& nf) { return nf.part ? (nf.h + 255) / 256 : 0; }
+
 __global__ __launch_bounds__(256) void reduce_splits_kernel(const float* __restrict__ part, int S, int64_t split_stride,
                                                             int M, int N, int nbm, int nbn, float* __restrict__ out,
-                                                            int64_t ldo) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+                                                            int64_t ldo, const NormFin nf) {
+  const int nfb = norm_fin_blocks(nf);
+  if ((int)blockIdx.x < nfb) {  // (the norm finaliser's blocks, cc_decode_partial)
+    norm_fin_block(nf, (int)blockIdx.x);
+    return;
+  }
+  const int64_t t = (int64_t)(blockIdx.x - nfb) * 256 + threadIdx.x;
   if (t >= (int64_t)nbm * nbn * 8 * 32 * 64) return;
   const int lane = (int)(t & 63), f = (int)((t >> 6) & 31), wave = (int)((t >> 11) & 7);
   const int tile = (int)(t >> 14);  // slab tile index tm * nbn + tn (EPI_SPLIT)
@@ -1003,11 +1025,13 @@ int64_t cc_decode_ws_floats(int64_t B, int64_t h, int64_t K, int dtype) {
 // BKC: W_dec given transposed, W_dec_t [K][h] (both operands contract over h contiguously)
 template <bool BKC>
 static int decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, float* ws, int64_t ws_floats,
-                         int64_t B, int64_t h, int64_t K, int dtype, hipStream_t st) {
+                         int64_t B, int64_t h, int64_t K, int dtype, hipStream_t st, const cc_colsum_job* pre = nullptr,
+                         const NormFin& nf = NormFin{}) {
   if (!recon_f32) return CC_ERR_NULL;
   DecPlan p;
   const bool split = dec_plan(B, h, K, dtype, p);
   const int64_t ldb = BKC ? h : K;
+  const int nf_blocks = nf.part ? (nf.h + 255) / 256 : 0;
   if (!split) {
     GemmArgs a = {};
     a.A = acts; a.lda = h; a.B = W_dec; a.ldb = ldb;
@@ -1015,7 +1039,21 @@ static int decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, 
     a.out_f32 = recon_f32; a.ldo = K;
     int rc = check_gemm(a, dtype, true, BKC);
     if (rc) return rc;
-    return launch_dt<EPI_DEC, true, BKC>(dtype, a, st);
+    if (pre) {  // (the job runs in the ping-pong kernels' prologue only: else its stand-alone launches first)
+      if (!use_pp(a.N, true, BKC, dtype)) {
+        if ((rc = cc_reduce_rows(pre->part, pre->rows, pre->cols, pre->ld, pre->scale, pre->out, nullptr, CC_F32,
+                                 nullptr, nullptr, nullptr, st)))
+          return rc;
+      } else if ((rc = set_pre(a, pre))) {
+        return rc;
+      }
+    }
+    rc = launch_dt<EPI_DEC, true, BKC>(dtype, a, st);
+    if (rc || !nf_blocks) return rc;
+    hipLaunchKernelGGL(reduce_splits_kernel, dim3((unsigned)nf_blocks), dim3(256), 0, st, nullptr, 0, (int64_t)0, 0, 0,
+                       0, 0, nullptr, (int64_t)0, nf);
+    CC_LAUNCH_CHECK();
+    return CC_OK;
   }
   if (!ws) return CC_ERR_NULL;
   const int64_t split_stride = split_stride_of(B, p);
@@ -1027,6 +1065,7 @@ static int decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, 
   a.out_f32 = recon_f32; a.ldo = K;
   int rc = check_gemm(a, dtype, true, BKC);
   if (rc) return rc;
+  if (pre && (rc = set_pre(a, pre))) return rc;
   GemmArgs t = {};
   t.A = acts; t.lda = h; t.B = (const bf16_t*)W_dec + (int64_t)p.nbn_main * 256 * (BKC ? h : 1); t.ldb = ldb;
   t.M = (int)B; t.N = p.tail_cols; t.K = (int)h;
@@ -1049,8 +1088,9 @@ static int decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, 
     CC_LAUNCH_CHECK();
   }
   const int64_t threads = (int64_t)t.nbm * t.nbn * 8 * 32 * 64;
-  hipLaunchKernelGGL(reduce_splits_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, ws, p.nsplit,
-                     split_stride, t.M, t.N, t.nbm, t.nbn, recon_f32 + (int64_t)p.nbn_main * 256, (int64_t)K);
+  hipLaunchKernelGGL(reduce_splits_kernel, dim3((unsigned)((threads + 255) / 256 + nf_blocks)), dim3(256), 0, st, ws,
+                     p.nsplit, split_stride, t.M, t.N, t.nbm, t.nbn, recon_f32 + (int64_t)p.nbn_main * 256, (int64_t)K,
+                     nf);
   CC_LAUNCH_CHECK();
   return CC_OK;
 }
@@ -1065,6 +1105,15 @@ int cc_decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, floa
 int cc_decode_fwd_ws_t(const void* acts, const void* W_dec_t, float* recon_f32, float* ws, int64_t ws_floats,
                        int64_t B, int64_t h, int64_t K, int dtype, void* stream) {
   return decode_fwd_ws<true>(acts, W_dec_t, recon_f32, ws, ws_floats, B, h, K, dtype, (hipStream_t)stream);
+}
+
+int cc_decode_partial(const void* acts, const void* W_dec, float* recon_f32, float* ws, int64_t ws_floats,
+                      const float* norm_part, float* norms, float* tn, float* inv_norms, const cc_colsum_job* pre,
+                      int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
+  if (norm_part && (!norms || !tn || d % 64)) return norms && tn ? CC_ERR_SHAPE : CC_ERR_NULL;
+  NormFin nf = {};
+  if (norm_part) nf = NormFin{norm_part, (int)h, (int)n, (int)(d / 64), norms, tn, inv_norms};
+  return decode_fwd_ws<false>(acts, W_dec, recon_f32, ws, ws_floats, B, h, n * d, dtype, (hipStream_t)stream, pre, nf);
 }
 
 }  // extern "C"

@@ -422,6 +422,56 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
   PP_STAMP(1);
 
   bf16x8 bfr[WG::TN][2];
+#if CC_PP_SUPER
+  // Two super-phases per K step instead of four phases: super-phase P = the old phases 2P and 2P+1 (A tiles
+  // 4P..4P+3 x both k-slices, 32 MFMAs; the B fragments of both k-slices read in P = 0), issuing the DMAs of
+  // both old phases, then vmcnt(4) (one super-phase's DMAs in flight) and the barrier.  Half the barriers and
+  // wave-group hand-offs per K step; every accumulator still adds k-slice 0 before k-slice 1 (the same bits).
+  // Regions: P = 0's DMAs (A of step t+1) overwrite what P = 1 of step t-1 read, P = 1's (B of step t+2) what
+  // P = 0 of step t read: both read sections retire their reads (lgkmcnt(0)) before their first barrier.
+  auto kstep = [&](auto tail, int t) {
+    const char* la = smem + (t & 1) * BUF;
+    const char* lb = la + TILE;
+#pragma unroll
+    for (int P = 0; P < 2; ++P) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (P == 0) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int j = 0; j < WG::TN; ++j) {
+            const int c0 = wc * WG::WTN + 16 * j;
+            bfr[j][kk] = BKC ? pp_frag_kc(lb, c0, kc_off[kk]) : pp_frag_mn(lb, c0, kk, mn_off[(c0 >> 4) & 3]);
+          }
+      }
+      bf16x8 afr[4][2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+          const int r0 = wr * WG::WTM + 16 * (4 * P + ii);
+          afr[ii][kk] = AKC ? pp_frag_kc(la, r0, kc_off[kk]) : pp_frag_mn(la, r0, kk, mn_off[(r0 >> 4) & 3]);
+        }
+      issue_t(tail, 2 * P, P == 0 ? t + 1 : t + 2);
+      issue_t(tail, 2 * P + 1, P == 0 ? t + 1 : t + 2);
+      wait_vmcnt<4>();
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int j = 0; j < WG::TN; ++j)
+            acc[4 * P + ii][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii][kk], acc[4 * P + ii][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+    }
+  };
+#else
   auto kstep = [&](auto tail, int t) {
     const char* la = smem + (t & 1) * BUF;
     const char* lb = la + TILE;
@@ -468,6 +518,7 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
       __builtin_amdgcn_s_barrier();
     }
   };
+#endif
   int t = 0;
   // steady state: every DMA is an operand DMA
   if (K % 64 == 0)

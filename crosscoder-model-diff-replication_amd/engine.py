@@ -194,7 +194,7 @@ class StepWorkspace:
         # launch carries the finaliser (decode_loss), or flush_norms runs it before the first reader
         self.norms_fin_pending = False
         self.fork_events = [None, None]  # the step's last stream-fork events (loss tail, decoder-half Adam)
-        self.tail_deferred = None  # (host, seq) of a loss tail the next whole-batch G3 launch carries
+        self.tail_deferred = None  # (host, seq, l1l0_out) of a loss tail the G3 launch of the batch's last rows carries
         self.acts_t = E(h, B, dt=dtype) if self.tr else None
         # G1's activation mask as bits in the GEMM accumulator order: G3 reads 16 B per thread and tile instead
         # of the 128 KB acts tile (1/16 of the bytes, no LDS staging)
@@ -333,7 +333,9 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     # of the prep / G1 partial slabs -- carried in the prologues of G1 and G2 where the step's fused path runs
     # (cc_colsum_job: no launches of their own), else two reduce_rows launches after G1
     fused = bool(loss and ws.fused_ncb)  # (fused_ncb: the transposed-operand step only)
-    x_job = ops.colsum_job(ws.x_colpart, ws.x_colpart.shape[0], K, 1.0 / B, ws.x_mean) if fused else None
+    # (the latent-sharded step's G1 -- loss=False -- carries x.mean(0) too; its G2, decode_partial_jobs, carries
+    # sum_b acts and the decoder norms' finaliser)
+    x_job = ops.colsum_job(ws.x_colpart, ws.x_colpart.shape[0], K, 1.0 / B, ws.x_mean) if ws.tr else None
     with _span("G1_encode"):
         if ws.tr:
             ops.encode_fwd_t(ws.x, P.W_enc_hk, P.b_enc, ws.acts, ws.acts_t, True, colsum_part=ws.acts_colpart,
@@ -341,9 +343,9 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
         else:
             ops.encode_fwd(ws.x, P.W_enc_hk, P.b_enc, ws.acts, True, colsum_part=ws.acts_colpart,
                            l0_part=ws.l0_part)
-    if not fused:
+    if x_job is None:
         ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
-        ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts)
+    acts_job = ops.colsum_job(ws.acts_colpart, ws.acts_colpart.shape[0], h, 1.0, ws.colsum_acts)
     fused_g2 = bool(loss and ws.fused_ncb)
     # (only while the decoder norms are the Adam's own: otherwise decoder_norms below reads W_dec on this stream)
     wait = P.wait_pending(kernel_wait=fused_g2 and G2_WAITS_IN_KERNEL and ws.norms_token == _norms_token(P))
@@ -353,17 +355,19 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
     if fused_g2:
         # (carries a pending norm finaliser and, fused, the activation column sums; waits in its kernel for the
         # side-stream Adam where `wait`)
-        decode_loss(ws, P, grad_scale, pre=ops.colsum_job(ws.acts_colpart, ws.acts_colpart.shape[0], h, 1.0,
-                                                          ws.colsum_acts) if fused else None, wait=wait)
+        decode_loss(ws, P, grad_scale, pre=acts_job, wait=wait)
         ws.acts_pending = True
         if finalize:
             loss_finalize(ws)
         return
     with _span("G2_decode"):
         if ws.W_dec_t is not None:
+            ops.reduce_rows(ws.acts_colpart, ws.acts_colpart.shape[0], h, out_f32=ws.colsum_acts)
             ops.decode_partial_t(ws.acts, ws.W_dec_t, ws.recon, ws.dec_ws)
         else:
-            ops.decode_partial(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws)
+            nf = (ws.norm_part, ws.norms, ws.tn, ws.inv_norms) if ws.norms_fin_pending else None
+            ws.norms_fin_pending = False
+            ops.decode_partial_jobs(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws, ws.n, ws.d, norm_fin=nf, pre=acts_job)
     # (G2 does not read the norms: their finaliser after it, where the latent-sharded step's collective on the
     # reconstruction hides it)
     flush_norms(ws)
@@ -491,7 +495,7 @@ def loss_finalize_with_g3(ws, side_stream, host=None, seq=0):
     shape (LOSS_TAIL_IN_G3, the transposed-operand step); otherwise loss_finalize_beside on `side_stream`.  Returns
     None (G3 carries it; the host reads the scalars through `host`) or loss_finalize_beside's event."""
     if LOSS_TAIL_IN_G3 and ws.tr and ws.acts_pending and host is not None:
-        ws.tail_deferred = (host, seq)
+        ws.tail_deferred = (host, seq, None)
         return None
     return loss_finalize_beside(ws, side_stream, host=host, seq=seq)
 
@@ -510,16 +514,18 @@ def dacts_rows(ws, P, l1_coeff, r0, r1, l1_grad_weight=1.0):
     c0, c1 = ops.col_part_rows(r0), ops.col_part_rows(r1)
     flush_norms(ws)
     tail = None
-    if ws.tail_deferred is not None:
-        host, seq = ws.tail_deferred
+    # a deferred loss tail rides in the launch of the batch's LAST rows: every loss row is written by then (the
+    # latent-sharded step's per-slice loss rows precede their slice's G3 on this stream)
+    if ws.tail_deferred is not None and r1 == ws.B:
+        host, seq, l1l0_out = ws.tail_deferred
         ws.tail_deferred = None
-        if ws.tr and (r0, r1) == (0, ws.B):
+        if ws.tr:
             tail = ops.loss_tail_job(ws.colsum_acts, ws.tn, ws.l1_part, _row_part(ws), ws.l0_part, ws.n_wave, ws.ev,
-                                     ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1], host=host,
-                                     seq=seq, ncb=ws.row_ncb)
+                                     ws.ev_a, ws.ev_b, ws.scalars, ws.B, ws.n, ws.d, ws.tail_ctr[0:1],
+                                     l1l0_out=l1l0_out, host=host, seq=seq, ncb=ws.row_ncb)
             ws.acts_pending = False
         else:
-            loss_finalize(ws, host=host, seq=seq)
+            loss_finalize(ws, l1l0_out=l1l0_out, host=host, seq=seq)
     with _span("G3_dacts"):
         if ws.tr:
             ops.dacts_bwd_t(ws.g_recon[r0:r1], P.W_dec_hk, ws.acts[r0:r1], ws.tn, l1_scale, ws.g_pre_t[:, r0:r1],

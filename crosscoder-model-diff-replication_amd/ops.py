@@ -202,6 +202,17 @@ def decode_partial(acts, W_dec_hk, recon_f32, ws=None):
                                  0 if ws is None else ws.numel(), B, h, K, dtype_code(acts.dtype), _stream(acts)))
 
 
+def decode_partial_jobs(acts, W_dec_hk, recon_f32, ws, n, d, norm_fin=None, pre=None):
+    """decode_partial (the same recon_f32 bits) carrying the step's small jobs (cc_decode_partial): pre, an
+    ops.colsum_job run before the tiles; norm_fin = (part, norms, total, inv_norms), the decoder norms' finaliser
+    (dec_norms_finalize) as extra blocks of the split-K reduction launch."""
+    B, h = acts.shape
+    part, norms, total, inv = norm_fin if norm_fin is not None else (None, None, None, None)
+    check(lib().cc_decode_partial(_ptr(acts), _ptr(W_dec_hk), _ptr(recon_f32), _ptr(ws), 0 if ws is None else ws.numel(),
+                                  _ptr(part), _ptr(norms), _ptr(total), _ptr(inv), pre, B, h, n, d,
+                                  dtype_code(acts.dtype), _stream(acts)))
+
+
 def decode_partial_t(acts, W_dec_t, recon_f32, ws=None):
     """decode_partial from the transposed decoder copy W_dec_t [K][h] (cc_decode_fwd_ws_t); same results."""
     B, h = acts.shape

@@ -150,6 +150,7 @@ class HipShardBackend:
         self.recon_chunks = recon_chunks
         self.ws = None
         self._aux = None
+        self._tail_carried = False  # this step's loss tail rode in the last d_acts launch (carry_tail)
 
     def fork_aux(self):
         """A stream other than the compute stream, ordered after the compute stream's work so far (one
@@ -176,9 +177,20 @@ class HipShardBackend:
     def row_chunks(self):
         return engine.row_chunks(self.ws.B, self.recon_chunks)
 
+    def carry_tail(self):
+        """Let the d_acts launch of the batch's last rows carry the loss tail (l1 / l0 of this rank's latents into
+        the step's reduce buffer, the scalars, the EVs): its first workgroups run it before their tiles, so the step
+        has no loss-tail launch of its own (engine.LOSS_TAIL_IN_G3, as the single-GPU step)."""
+        ws = self.ws
+        if engine.LOSS_TAIL_IN_G3 and ws.tr and ws.acts_pending:
+            ws.tail_deferred = (None, 0, self.red[4:6])
+            self._tail_carried = True
+
     def rows_ready(self, r0, r1, l1c):
         P = self.cc.arena()
         engine.loss_rows(self.ws, P, r0, r1)
+        if r1 == self.ws.B:
+            self.carry_tail()
         engine.dacts_rows(self.ws, P, l1c, r0, r1)
 
     # ---- comm="reduce_scatter"
@@ -212,9 +224,14 @@ class HipShardBackend:
                  .reshape(rp.shape))
         if ws.tr:
             ops.transpose(ws.g_recon, out=ws.g_recon_t)
+        self.carry_tail()
         engine.dacts_rows(ws, self.cc.arena(), l1c, 0, ws.B)
 
     def loss_finalize(self, red):
+        if self._tail_carried:  # (the last d_acts launch ran it, into red[4:6] = self.red[4:6])
+            self._tail_carried = False
+            assert red is self.red
+            return self.ws.scalars
         engine.loss_finalize(self.ws, l1l0_out=red[4:6])
         return self.ws.scalars
 

@@ -156,6 +156,16 @@ int cc_decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, floa
  * cc_adam_step_t): both operands then contract over h contiguously.  Same results. */
 int cc_decode_fwd_ws_t(const void* acts, const void* W_dec_t, float* recon_f32, float* ws, int64_t ws_floats,
                        int64_t B, int64_t h, int64_t K, int dtype, void* stream);
+/* cc_decode_fwd_ws (W_dec [h][K] read as stored) for the latent-sharded step's partial reconstruction
+ * (crosscoder.py:82-89 without b_dec, summed over the ranks), carrying two small jobs so the step saves their
+ * launches: pre (optional) -- a cc_colsum_job the launch runs before its tiles (the step's sum_b acts,
+ * crosscoder.py:126, from G1's column partials) -- and, norm_part given, the decoder norms' finaliser
+ * (cc_dec_norms_finalize(norm_part, h, n, d, norms, tn, inv_norms), d % 64 == 0) as extra blocks of the
+ * split-K leftover's reduction launch.  recon_f32 bit-identical to cc_decode_fwd_ws; the jobs' outputs to
+ * their stand-alone launches. */
+int cc_decode_partial(const void* acts, const void* W_dec, float* recon_f32, float* ws, int64_t ws_floats,
+                      const float* norm_part, float* norms, float* tn, float* inv_norms, const cc_colsum_job* pre,
+                      int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream);
 
 /* get_losses reconstruction terms + their backward (crosscoder.py:104-121, autograd):
  * r = recon_f32 + b_dec; g_recon = dtype(grad_scale * (r - x)) with grad_scale = 2/B.

@@ -1662,3 +1662,41 @@ def test_odd_shapes_match_oracle(gpu, enc_dtype, B, n, d, h):
     Wdec = a.W_dec_hk.view(a.h, n, a.d)
     assert float(Wdec[h:].abs().sum()) == 0.0 and float(Wdec[:, :, d:].abs().sum()) == 0.0
     assert float(a.b_enc[h:].abs().sum()) == 0.0 and float(a.b_dec_flat.view(n, a.d)[:, d:].abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("B,n,d,h", [(4096, 2, 2304, 16384), (1024, 2, 256, 2048), (512, 4, 128, 1024),
+                                     (256, 2, 64, 512)])
+def test_decode_partial_jobs_match_separate_launches(gpu, B, n, d, h):
+    """cc_decode_partial (the latent-sharded step's G2): the fp32 partial reconstruction is
+    bit-identical to cc_decode_fwd_ws, and the two jobs it carries -- sum_b acts as its prologue (cc_colsum_job) and
+    the decoder norms' finaliser as extra blocks of its split-K reduction launch -- to their stand-alone launches
+    (reduce_rows, dec_norms_finalize).  Shapes with and without a split-K leftover."""
+    bf = torch.bfloat16
+    g = torch.Generator(device=gpu).manual_seed(B + h)
+    K = n * d
+    acts = torch.relu(torch.randn(B, h, device=gpu, generator=g)).to(bf)
+    W = (torch.randn(h, K, device=gpu, generator=g) * 0.02).to(bf)
+    rows = ops.col_part_rows(B)
+    colpart = torch.randn(rows, h, device=gpu, generator=g)
+    npart = ops.dec_norms_part_floats(h, n, d)
+    part = torch.rand(npart, device=gpu, generator=g)
+    nws = max(1, int(ops.lib().cc_decode_ws_floats(B, h, K, 1)))
+    dws = torch.empty(nws, device=gpu)
+    out = {}
+    for jobs in (False, True):
+        recon = torch.full((B, K), float("nan"), device=gpu)
+        colsum = torch.full((h,), float("nan"), device=gpu)
+        norms, tn, inv = (torch.full(s, float("nan"), device=gpu) for s in ((h, n), (h,), (h, n)))
+        if jobs:
+            ops.decode_partial_jobs(acts, W, recon, dws, n, d, norm_fin=(part, norms, tn, inv),
+                                    pre=ops.colsum_job(colpart, rows, h, 1.0, colsum))
+        else:
+            ops.decode_partial(acts, W, recon, dws)
+            ops.reduce_rows(colpart, rows, h, out_f32=colsum)
+            ops.dec_norms_finalize(part, h, n, d, norms, tn, inv)
+        torch.cuda.synchronize()
+        out[jobs] = (recon, colsum, norms, tn, inv)
+    for a, b in zip(out[False], out[True]):
+        assert torch.equal(a, b)
+    ref = acts.float() @ W.float()
+    assert torch.allclose(out[True][0], ref, rtol=1e-3, atol=1e-3)

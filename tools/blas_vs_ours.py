@@ -23,14 +23,19 @@ def main():
     r = lambda *s, sc=1.0: (torch.randn(*s, device=dev, generator=g) * sc).to(bf)  # noqa: E731
     x, W = r(B, K), r(h, K, sc=0.02)
     b = torch.zeros(h, device=dev, dtype=bf)
-    acts = torch.empty(B, h, device=dev, dtype=bf)
+    acts = torch.relu(torch.matmul(x, W.t()))  # (G3's activation mask input)
     acts_t = torch.empty(h, B, device=dev, dtype=bf)
     out = torch.empty(B, h, device=dev, dtype=bf)
     xt = x.t().contiguous()
     gp_t = torch.relu(r(h, B))  # a [h][B] operand like g_pre^T
     dW = torch.empty(h, K, device=dev, dtype=bf)
+    g_recon = r(B, K, sc=1e-3)  # G3's data: d_acts = g_recon . W_dec^T
+    gp = torch.empty(h, B, device=dev, dtype=bf)
+    tn = torch.rand(h, device=dev) * 0.1
     cases = {
         "hipBLASLt x.W^T": lambda: torch.matmul(x, W.t(), out=out),
+        "hipBLASLt g_recon.W^T (G3 data)": lambda: torch.matmul(g_recon, W.t(), out=out),
+        "ours G3 d_acts^T (G3 data)": lambda: ops.dacts_bwd_t(g_recon, W, acts, tn, 1e-4, gp),
         "ours G1 encode (bias+relu, bf16 out)": lambda: ops.encode_fwd(x, W, b, acts, True),
         "ours G1 encode + acts^T": lambda: ops.encode_fwd_t(x, W, b, acts, acts_t, True),
         "hipBLASLt g_pre^T.x (h x K, over B)": lambda: torch.matmul(gp_t, xt.t(), out=dW),
