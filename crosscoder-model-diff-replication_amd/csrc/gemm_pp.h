@@ -66,6 +66,12 @@
 #ifndef CC_PP_PRIO
 #define CC_PP_PRIO 0
 #endif
+// timing probes of the K loop's energy (results invalid; never in the product): bit 0 = half the A fragment reads
+// from LDS, bit 1 = the steady-state K steps DMA the operands' first 4 K steps over and over (every operand byte an
+// L2 hit after the first pass, the MFMA operands still changing from step to step)
+#ifndef CC_PP_PROBE
+#define CC_PP_PROBE 0
+#endif
 // Tile anatomy probe (build with -DCC_PP_STAMPS; GemmArgs::stamps set by the debug build's cc_debug_set_stamps):
 // thread 0 keeps s_memtime at tile entry (0), after the prologue's barrier (1), after the K loop (2), after the
 // drain before the epilogue (3) and after the epilogue's stores are issued (4), plus the 100 MHz wall clock at
@@ -351,7 +357,12 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
     if constexpr (TL == 2) {
       const int64_t ld = isA ? args.lda : args.ldb;
       const bool kc = isA ? AKC : BKC;
+#if CC_PP_PROBE & 2
+      const int kp = (kb0 + (T & 3)) * 64;
+      const int kadd = (int)(kc ? (int64_t)kp * 2 : (int64_t)kp * ld * 2);
+#else
       const int kadd = (int)(kc ? (int64_t)k0 * 2 : (int64_t)k0 * ld * 2);
+#endif
 #pragma unroll
       for (int q = 0; q < 2; ++q)  // (vo[p][q] == OOB lanes stay past the record count)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? ra : rb, (lds_void*)(dst + pp_ci(p, q, wave) * 1024), 16,
@@ -493,6 +504,9 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
         const int r0 = wr * WG::WTM + 16 * (ib + ii);
+#if CC_PP_PROBE & 1  // timing probe (results invalid): half the A fragment reads (A tiles 2, 3 reuse 0, 1)
+        if (ii >= 2) { afr[ii] = afr[ii - 2]; continue; }
+#endif
         afr[ii] = AKC ? pp_frag_kc(la, r0, kc_off[kk]) : pp_frag_mn(la, r0, kk, mn_off[(r0 >> 4) & 3]);
       }
       issue_t(tail, p, p < 2 ? t + 1 : t + 2);

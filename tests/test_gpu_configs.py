@@ -41,8 +41,8 @@ def test_baseline_config_full_size_trainer_step(gpu, name):
     tr = ca.Trainer(cfg, buffer=buf, crosscoder=cc)
     tr.step_counter = 10_000  # past the l1 warm-up: l1_coeff = 2 (trainer.py:34-39)
     gi = torch.Generator().manual_seed(B + h)
-    rows = torch.randint(0, B, (16,), generator=gi).to(gpu)
-    lat = torch.randint(0, h, (8,), generator=gi).to(gpu)
+    rows = torch.randint(0, B, (64,), generator=gi).to(gpu)
+    lat = torch.randint(0, h, (64,), generator=gi).to(gpu)
     a = cc.arena()
     D = lambda t: t.double()  # noqa: E731  (fp64 on the GPU: the operands are too large for the host)
     We0, Wd0, be0, bd0 = (D(t).clone() for t in (a.W_enc_hk, a.W_dec_hk, a.b_enc, a.b_dec_flat))

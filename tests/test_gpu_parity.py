@@ -700,18 +700,33 @@ def test_dynamic_tile_order_is_bit_identical(gpu, dbg_lib, monkeypatch):
 def test_full_size_config2_trainer_steps_match_oracle(gpu, full_size_case):
     """BASELINE config 2 through the shipped schedule (Trainer.step: fused G2 + loss, G4G5 + grad tail + clip
     in one launch, encoder / decoder Adam halves on two streams) vs the oracle's fp32 OracleTrainer.step
-    (trainer.py:41-63) on the same bf16-valued inputs and init, two steps (l1_coeff 0 then 2): the 9-key loss
-    dicts, the clip total norm / coefficient, and params + both Adam moments after each step, within the
-    SURVEY 8c bf16 envelope (bounds ~2x the values measured on MI355X)."""
-    cfg, P, buf, factor, x = full_size_case
-    cfg = dict(cfg, batch_size=4096, num_tokens=4096 * 20, lr=5e-5, beta1=0.9, beta2=0.999, l1_coeff=2)
+    (trainer.py:41-63) on the same bf16-valued inputs and init: FIVE steps on five different batches, through
+    the l1_coeff warm-up (num_tokens = 100 batches: l1_coeff 0, 0.4, 0.8, 1.2, 1.6): the 9-key loss dicts, the
+    clip total norm / coefficient, and params + both Adam moments after every step, within the SURVEY 8c bf16
+    envelope (bounds ~2x the values measured on MI355X; the parameter bounds grow with the step, as the two
+    precisions' Adam trajectories drift apart)."""
+    cfg, P, buf0, factor0, _ = full_size_case
+    steps = 5
+    B, n, d = 4096, 2, 2304
+    bufs, factors = [], []
+    for s in range(steps):
+        if s == 0:
+            b, f = buf0, factor0
+        else:
+            g = torch.Generator().manual_seed(100 + s)
+            b = (torch.randn(B, n, d, generator=g) * torch.tensor([1 / 0.2759, 1 / 0.2442])[None, :, None]).to(
+                torch.bfloat16)
+            f = factor0  # (Buffer's factor is estimated once and kept: buffer.py:34-41)
+        bufs.append(b)
+        factors.append(f)
+    cfg = dict(cfg, batch_size=B, num_tokens=B * 100, lr=5e-5, beta1=0.9, beta2=0.999, l1_coeff=2)
     cc = make_cc(cfg, P, gpu, 2)
-    tr = ca.Trainer(dict(cc.cfg), buffer=_Replay([buf, buf], [factor, factor], gpu), crosscoder=cc)
+    tr = ca.Trainer(dict(cc.cfg), buffer=_Replay(bufs, factors, gpu), crosscoder=cc)
     torch.set_num_threads(max(1, torch.get_num_threads()))
     orc = O.OracleTrainer(dict(cfg, enc_dtype="fp32"), {k: v.float() for k, v in P.items()})
-    x32 = x.to(torch.bfloat16).float()
     lr = cfg["lr"]
-    for s in range(2):
+    for s in range(steps):
+        x32 = O.buffer_next(bufs[s], factors[s]).to(torch.bfloat16).float()
         d = tr.step()
         clip = cc._ws.clip_out[:2].cpu()
         st = tr.optimizer.state  # (orders after the side-stream decoder half)
@@ -733,17 +748,19 @@ def test_full_size_config2_trainer_steps_match_oracle(gpu, full_size_case):
             p, m, v = ours[k]
             pr = orc.P[k].detach()
             # Adam's update is ~lr * sign(m): params agree to the bf16 rounding of the result except where a
-            # small gradient's sign or the m / sqrt(v) ratio differs between the two precisions (<= ~2 lr)
+            # small gradient's sign or the m / sqrt(v) ratio differs between the two precisions (<= ~2 lr per step)
             diff = (p - pr).abs()
-            close = (diff <= _bf16_ulp(pr) + 0.05 * lr).float().mean().item()
+            close = (diff <= _bf16_ulp(pr) + 0.05 * lr * (s + 1)).float().mean().item()
             worst = ((diff - 2 * _bf16_ulp(pr)).clamp_min(0) / lr).max().item()
             stats[k] = (close, worst, rel(m, orc.m[k]), rel(v, orc.v[k]))
             print(f"step {s} {k}: params close {close:.4f}, worst (diff - 2 ulp) / lr {worst:.3f}, "
-                  f"exp_avg rel {stats[k][2]:.2e}, exp_avg_sq rel {stats[k][3]:.2e}")
+                  f"exp_avg rel {stats[k][2]:.2e}, exp_avg_sq rel {stats[k][3]:.2e}", flush=True)
         for k, (close, worst, em, ev) in stats.items():
-            tol = 0.2 if k == "W_enc" else 3e-2
-            assert close >= (0.93 if k == "W_enc" else 0.97), (s, k, close)  # (measured >= 0.965 / 0.9885)
-            assert worst <= 5.0, (s, k, worst)  # (measured <= 3.5: W_enc at step 2)
+            # (measured over the 5 steps: close >= 0.994 W_enc / 0.996 others; worst <= 3.7 lr; W_enc's exp_avg
+            # rel grows 0.009 -> 0.045, the others' moments stay <= 0.034)
+            assert close >= (0.98 if k == "W_enc" else 0.99), (s, k, close)
+            assert worst <= 6.0, (s, k, worst)
+            tol = 0.1 if k == "W_enc" else 3e-2
             assert em <= tol and ev <= 2 * tol, (s, k, em, ev)
 
 

@@ -75,12 +75,20 @@ def test_sharded_world2_on_one_gpu_matches_trainer(gpu, comm, tmp_path):
     tr = ca.Trainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 3, seed=1), crosscoder=ca.CrossCoder(cfg))
     ref = [tr.step() for _ in range(STEPS)]
     ref_sd = {k: v.detach().cpu() for k, v in tr.crosscoder.state_dict().items()}
+    worst = {}
     for r in range(world):
         for a, b in zip(res[r][0], ref):
             assert list(a) == list(b)
             for k in ("loss", "l2_loss", "l1_loss", "l0_loss", "explained_variance"):
-                assert math.isclose(a[k], b[k], rel_tol=2e-3, abs_tol=2e-3), (r, k, a[k], b[k])
+                e = abs(a[k] - b[k]) / max(abs(b[k]), 1e-6)
+                worst[k] = max(worst.get(k, 0.0), e)
             assert a["lr"] == b["lr"] and a["l1_coeff"] == b["l1_coeff"]
+    print("sharded vs single-GPU loss dict, worst relative difference:", worst, flush=True)
+    # (the partial reconstructions and the clip sums are combined in another order: fp32 reassociation, then the
+    # bf16 roundings of the params it moves; measured on MI355X over 3 steps: l2 / l1 / loss identical, EV 1.5e-7,
+    # l0 2.9e-6 -- one latent at the ReLU edge)
+    for k, e in worst.items():
+        assert e <= (5e-5 if k == "l0_loss" else 1e-5), (k, e)
     sd = res[0][1]
     assert list(sd) == list(ref_sd)
     for k, v in ref_sd.items():
