@@ -48,7 +48,7 @@ def main():
             torch.cuda.synchronize()
             err = ((C2.float() - ref.float()).norm() / ref.float().norm()).item()
             print(f"{sname} {name}: rel err vs hipBLASLt {err:.2e}", flush=True)
-            assert err < 1e-2
+            assert err < 1e-2 or "nostore" in name or name.endswith("ns.so")  # (timing-only builds store nothing)
             cases[name] = (lambda L=L, C2=C2: L.g4_gemm_bf16(P(A), P(Bm), P(C2), M, N, K, K, K, N, st))
         res = {k: [] for k in cases}
         for _ in range(3):
