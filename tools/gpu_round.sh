@@ -35,8 +35,8 @@ for s in $STEPS; do
     smoke) run smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ;;
     configs) for c in 3 4 5; do run bench_config$c 400 python bench.py --config $c --no-cpu-baseline --steps 10 --warmup 3; done ;;
-    rehearse) for n in 2 4; do CC_BENCH_ONE_DEVICE=1 run rehearse_n$n 400 python -m torch.distributed.run --nnodes=1 \
-                --nproc-per-node $n --master-addr 127.0.0.1 --master-port 2951$n bench.py --gpus $n --steps 5 --warmup 2; done ;;
+    rehearse) for n in 2 4; do CC_BENCH_ONE_DEVICE=1 run rehearse_n$n 400 python bench.py --gpus $n --steps 5 \
+                --warmup 2 --deadline 360 --no-cpu-baseline; done ;;
     sharded) run bench_sharded 300 python bench.py --no-cpu-baseline --force-sharded
              run bench_sharded_rs 300 python bench.py --no-cpu-baseline --force-sharded --comm reduce_scatter ;;
     prof) run rocprof_stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
