@@ -66,3 +66,20 @@ def test_gpus_n_relays_rank0_line(n):
     assert p.returncode == 0, p.stderr[-2000:]
     (line,) = json_lines(p.stdout)
     assert line["n_gpus"] == n and line["rank_sum"] == float(sum(range(n)))
+
+
+def test_effective_clock_from_tile_sum_words():
+    """bench.py's clock report: shader-clock ticks over 100 MHz wall ticks (gemm.hip WgradTail::clock layout:
+    [sclk ticks, wall ticks, launches, ...]); no launch recorded gives no report."""
+    import importlib.util
+    import torch
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    words = torch.zeros(8, dtype=torch.int64)
+    assert bench.effective_clock(words) is None
+    words[0], words[1], words[2] = 1_720_000_000, 100_000_000, 3     # 1 s of wall ticks at 1.72 GHz
+    rep = bench.effective_clock(words)
+    assert rep["effective_sclk_ghz"] == pytest.approx(1.72)
+    assert rep["launches"] == 3 and rep["window_ms"] == pytest.approx(1000.0)
+    assert bench.effective_clock(None) is None
