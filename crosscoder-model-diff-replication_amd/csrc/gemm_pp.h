@@ -72,6 +72,12 @@
 #ifndef CC_PP_PROBE
 #define CC_PP_PROBE 0
 #endif
+// experiment switch: epilogue kinds (bitmask over Epi) whose K loop runs the super-phase form (pp_tile).  Default
+// 0 (every GEMM on the four-phase form): G3 alone on it is 6-10 µs faster, the step is not (2.5140 vs 2.5153 ms
+// over 4 alternating same-box rounds; profiles/r05_gemm_superphase_ab.txt, r05_ab_g3_superphase.txt)
+#ifndef CC_PP_SUPER_EPIS
+#define CC_PP_SUPER_EPIS 0
+#endif
 // Tile anatomy probe (build with -DCC_PP_STAMPS; GemmArgs::stamps set by the debug build's cc_debug_set_stamps):
 // thread 0 keeps s_memtime at tile entry (0), after the prologue's barrier (1), after the K loop (2), after the
 // drain before the epilogue (3) and after the epilogue's stores are issued (4), plus the 100 MHz wall clock at
@@ -433,14 +439,17 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
   PP_STAMP(1);
 
   bf16x8 bfr[WG::TN][2];
-#if CC_PP_SUPER
-  // Two super-phases per K step instead of four phases: super-phase P = the old phases 2P and 2P+1 (A tiles
+  // Two K-step forms, picked per epilogue kind at compile time (CC_PP_SUPER_EPIS, a bitmask over Epi):
+  // Super form -- two super-phases per K step instead of four phases: super-phase P = the old phases 2P and 2P+1 (A tiles
   // 4P..4P+3 x both k-slices, 32 MFMAs; the B fragments of both k-slices read in P = 0), issuing the DMAs of
   // both old phases, then vmcnt(4) (one super-phase's DMAs in flight) and the barrier.  Half the barriers and
   // wave-group hand-offs per K step; every accumulator still adds k-slice 0 before k-slice 1 (the same bits).
   // Regions: P = 0's DMAs (A of step t+1) overwrite what P = 1 of step t-1 read, P = 1's (B of step t+2) what
   // P = 0 of step t read: both read sections retire their reads (lgkmcnt(0)) before their first barrier.
-  auto kstep = [&](auto tail, int t) {
+  // +16 VGPRs (both k-slices' A fragments of a super-phase in flight; G3 212 -> 228).  Never for G1: beside it
+  // the side-stream decoder Adam (80 VGPRs) needs 2 x 216 + 80 <= 512 registers per SIMD lane; G2 and G4 + G5
+  // measured slower or neutral with it (profiles/r05_gemm_superphase_ab.txt).
+  auto kstep_super = [&](auto tail, int t) {
     const char* la = smem + (t & 1) * BUF;
     const char* lb = la + TILE;
 #pragma unroll
@@ -482,8 +491,8 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
       __builtin_amdgcn_s_barrier();
     }
   };
-#else
-  auto kstep = [&](auto tail, int t) {
+  // Phase form: four phases per K step.
+  auto kstep_phase = [&](auto tail, int t) {
     const char* la = smem + (t & 1) * BUF;
     const char* lb = la + TILE;
 #pragma unroll
@@ -532,7 +541,12 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
       __builtin_amdgcn_s_barrier();
     }
   };
-#endif
+  auto kstep = [&](auto tail, int t) {
+    if constexpr ((CC_PP_SUPER_EPIS >> EPI) & 1)
+      kstep_super(tail, t);
+    else
+      kstep_phase(tail, t);
+  };
   int t = 0;
   // steady state: every DMA is an operand DMA
   if (K % 64 == 0)
