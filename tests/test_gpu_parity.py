@@ -490,6 +490,39 @@ def test_full_size_step_deterministic(gpu, full_size_case):
     assert outs[0][1]["l2_loss"] < outs[0][0]["l2_loss"]
 
 
+def test_full_size_long_run_deterministic(gpu, full_size_case):
+    """150 Trainer steps of BASELINE config 2 over 8 distinct batches of a seeded SyntheticBuffer, twice from the
+    same init: every loss dict, the params and both Adam moments at the end are bit-identical between the two runs
+    (the per-XCD tile claims, the side-stream decoder Adam with G2's in-kernel wait, the split-K and clip sums and
+    the deferred decoder rows change no bit), every loss is finite, the run passes through the l1_coeff warm-up
+    (first 5 %) and the LR decay (last 20 %, trainer.py:28-34), and the loss falls."""
+    cfg, P, _, _, _ = full_size_case
+    steps, B = 150, 4096
+    base = dict(cfg, batch_size=B, num_tokens=B * steps, lr=5e-5, beta1=0.9, beta2=0.999, l1_coeff=2)
+    runs = []
+    for _ in range(2):
+        cc = make_cc(base, P, gpu, 2)
+        buf = ca.SyntheticBuffer(dict(cc.cfg), rows=8 * B, n_models=2, seed=1, device=gpu)
+        tr = ca.Trainer(dict(cc.cfg), buffer=buf, crosscoder=cc)
+        dicts = [tr.step() for _ in range(steps)]
+        tr.synchronize()
+        st = tr.optimizer.state
+        moments = [torch.cat([st[getattr(cc, k)][m].detach().float().flatten() for k in O.PARAM_ORDER])
+                   for m in ("exp_avg", "exp_avg_sq")]
+        runs.append((dicts, cc.arena().data.clone(), moments))
+        del tr, cc, buf
+        torch.cuda.empty_cache()
+    (d_a, p_a, m_a), (d_b, p_b, m_b) = runs
+    assert d_a == d_b
+    assert torch.equal(p_a, p_b)
+    assert all(torch.equal(x, y) for x, y in zip(m_a, m_b))
+    for d in d_a:
+        assert all(math.isfinite(v) for v in d.values()), d
+    assert d_a[0]["l1_coeff"] == 0.0 and d_a[-1]["l1_coeff"] == 2.0
+    assert d_a[0]["lr"] == 5e-5 and d_a[-1]["lr"] < 5e-5 * 0.1
+    assert sum(d["l2_loss"] for d in d_a[-8:]) < sum(d["l2_loss"] for d in d_a[:8])
+
+
 @pytest.mark.parametrize("side_rows", [0.0, 0.5, 1.0, "serial"])
 def test_decoder_adam_split_is_bit_identical(gpu, side_rows, monkeypatch):
     """The decoder half of Adam split between the side stream (W_dec's first rows, beside the next G1) and the
