@@ -69,7 +69,13 @@ template <class F, int... Ms>
 __device__ __forceinline__ void for_each_slot(F& f, std::integer_sequence<int, Ms...>) {
   (f(std::integral_constant<int, Ms>{}), ...);
 }
-constexpr int IMG = 256 * 128;  // one operand's K-step image (32 KB)
+#ifndef G4H_VLAYOUT
+#define G4H_VLAYOUT 0
+#endif
+// G4H_VLAYOUT 1: the vendor kernel's LDS image -- 1-KB pieces p = 16 h + r16 holding rows {128 h + 16 i + r16, i < 8}
+// x 64 K (16 B per (i, 16-B K chunk), i-major), four pieces per 4160-B block (64 B of padding per 4 KB); a DMA moves
+// one piece (8 rows 16 apart), a lane's fragment of row group i / k-slice kk sits at 128 i + 64 kk in its piece
+constexpr int IMG = G4H_VLAYOUT ? 8 * 4160 : 256 * 128;  // one operand's K-step image
 constexpr int BUF = 2 * IMG;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint64_t bytes) {
@@ -107,10 +113,19 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(const void* __restrict__ A
   const __amdgpu_buffer_rsrc_t rb = rsrc((const char*)B + (int64_t)n0 * ldb * 2, (uint64_t)256 * ldb * 2);
   // DMA: wave w moves image pieces 8w .. 8w + 7 of A and of B (piece ci = rows 8ci .. 8ci + 7, 1 KB); lane ->
   // row 8ci + (lane >> 3), logical chunk (lane & 7) ^ (lane >> 3) (the swizzle through the source address)
+#if G4H_VLAYOUT
+  // piece of DMA q (0..7 per operand) and wave w: p = 4 q + w -> h = q >> 2, r16 = 4 (q & 3) + w; lane -> row
+  // 128 h + 16 (lane >> 3) + r16, K chunk lane & 7
+  const uint32_t va = (uint32_t)(((int64_t)(16 * (lane >> 3) + wave) * lda + 8 * (lane & 7)) * 2);
+  const uint32_t vb = (uint32_t)(((int64_t)(16 * (lane >> 3) + wave) * ldb + 8 * (lane & 7)) * 2);
+  auto qrow = [](int q) { return 128 * (q >> 2) + 4 * (q & 3); };
+  const int sa = (int)(lda * 2), sb = (int)(ldb * 2);  // (times qrow)
+#else
   const int rl = lane >> 3, cl = (lane & 7) ^ rl;
   const uint32_t va = (uint32_t)(((int64_t)(64 * wave + rl) * lda + 8 * cl) * 2);
   const uint32_t vb = (uint32_t)(((int64_t)(64 * wave + rl) * ldb + 8 * cl) * 2);
   const int sa = (int)(8 * lda * 2), sb = (int)(8 * ldb * 2);  // one piece further (8 rows)
+#endif
   const int nk = K / 64;
   // K stagger (G4H_SU > 1): the tile's K loop starts at K step (stagger index * G4H_SS) mod nk and wraps, so the
   // tiles that share an operand panel read different K slices of it at any moment (the vendor kernel's StaggerU);
@@ -126,12 +141,26 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(const void* __restrict__ A
 #endif
   const int koff = __builtin_amdgcn_readfirstlane((((tn + G4H_SM * tm) % G4H_SU) * G4H_SS) % nk);
   auto dma = [&](int s, int q) {  // piece q (0..7: A, 8..15: B) of step s into buffer s & 1
-    char* dst = smem + (s & 1) * BUF + (q < 8 ? 0 : IMG) + (8 * wave + (q & 7)) * 1024;
     const int ks = s + koff >= nk ? s + koff - nk : s + koff;  // (the stagger's wrapped K step)
+#if G4H_VLAYOUT
+    char* dst = smem + (s & 1) * BUF + (q < 8 ? 0 : IMG) + (q & 7) * 4160 + wave * 1024;
+    const int so = qrow(q & 7) * (q < 8 ? sa : sb) + ks * 128;
+#else
+    char* dst = smem + (s & 1) * BUF + (q < 8 ? 0 : IMG) + (8 * wave + (q & 7)) * 1024;
     const int so = (q & 7) * (q < 8 ? sa : sb) + ks * 128;
+#endif
     __builtin_amdgcn_raw_ptr_buffer_load_lds(q < 8 ? ra : rb, (lds_void*)dst, 16, (int)(q < 8 ? va : vb), so, 0, 0);
   };
   // fragment lane offset: row (lane & 15) of a 16-row group, chunk 4 kk + (lane >> 4), swizzled
+#if G4H_VLAYOUT
+  auto pbase = [](int p) { return (p >> 2) * 4160 + (p & 3) * 1024; };
+  const int vA = pbase(16 * wr + (lane & 15)) + 16 * (lane >> 4);
+  const int vB = IMG + pbase(16 * wc + (lane & 15)) + 16 * (lane >> 4);
+  auto frag = [&](int s, int kk, int f) {  // f 0..7: A row group f of the wave; 8..15: B column group f - 8
+    const char* base = smem + (s & 1) * BUF + (f < 8 ? vA + 128 * f : vB + 128 * (f - 8)) + 64 * kk;
+    return *(const bf16x8*)base;
+  };
+#else
   int foff[2];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) foff[kk] = (lane & 15) * 128 + (((4 * kk + (lane >> 4)) ^ (lane & 7)) << 4);
@@ -139,6 +168,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(const void* __restrict__ A
     const char* base = smem + (s & 1) * BUF + (f < 8 ? (wr * 128 + 16 * f) * 128 : IMG + (wc * 128 + 16 * (f - 8)) * 128);
     return *(const bf16x8*)(base + foff[kk]);
   };
+#endif
 
   f32x4 acc[8][8];
 #pragma unroll
