@@ -52,6 +52,12 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 #define G4H_RD_EVERY 4
 #endif
 
+#ifndef G4H_PIN
+#define G4H_PIN 0
+#endif
+#if G4H_PIN
+#include "g4h3_pin.h"
+#endif
 namespace g4h {
 // vendor schedule slots (after the MFMA with that 0-based index), see the header
 constexpr int RA[8] = {0, 2, 4, 6, 8, 10, 12, 14};
@@ -211,8 +217,13 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(const void* __restrict__ A
       // (G4H_SRC0_CONST: j outer, i inner -- src0, the B fragment, stays the same over 8 consecutive MFMAs, as in the
       // vendor loop; else i outer, src1 constant)
       constexpr int i = G4H_SRC0_CONST ? (m & 7) : ((m & 63) >> 3), j = G4H_SRC0_CONST ? ((m & 63) >> 3) : (m & 7);
+#if G4H_PIN
+      if constexpr (m < 64) mfma_pin<0, i, j>(acc[i][j], F0[8 + j], F0[i]);
+      else mfma_pin<1, i, j>(acc[i][j], F1[8 + j], F1[i]);
+#else
       if constexpr (m < 64) G4H_MFMA(acc[i][j], F0[8 + j], F0[i]);
       else G4H_MFMA(acc[i][j], F1[8 + j], F1[i]);
+#endif
       constexpr int qa = find_slot(RA, m), qb = find_slot(RB, m), da = find_slot(DA, m), db = find_slot(DB, m),
                     r0 = find_slot(R0, m);
       if constexpr (qa >= 0) F1[qa] = frag(t, 1, qa);
