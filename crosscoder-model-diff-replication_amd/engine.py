@@ -643,6 +643,8 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
             step_(P.data, G.data, M.data, V.data, clip_out=ws.clip_out)
         return
     dev = P.data.device
+    if ENC_ADAM_SIDE_PROBE and not (DEC_ADAM_BESIDE_G1 and ws.W_dec_t is None and ws.norm_part is not None):
+        raise RuntimeError("ENC_ADAM_SIDE_PROBE: only the side-stream decoder-row path carries the encoder half")
     if not ENC_ADAM_SIDE_PROBE:
         with _span("adam"):
             step_(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), clip_out=ws.clip_out)
