@@ -1,4 +1,4 @@
-"""CPU, world_size 2 over gloo: the latent-sharded step orchestration (sharded.ShardedStep —
+"""CPU, world_size 2 (and 4) over gloo: the latent-sharded step orchestration (sharded.ShardedStep —
 the same collectives and combine rules the GPU path uses) driven by a torch-CPU backend must
 reproduce the unsharded oracle step."""
 import os
@@ -160,7 +160,7 @@ def _worker(rank, world, port, q, comm, slices=2):
 
 
 @pytest.mark.parametrize("comm,slices", [("all_reduce", 2), ("all_reduce", 1), ("reduce_scatter", 1)])
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_sharded_step_matches_unsharded(world, comm, slices):
     """Both exchanges of the partial reconstructions: the all-reduce (in two batch slices, or
     one synchronous collective), and the reduce-scatter by batch rows -> loss on B/G rows -> all-gather
