@@ -604,10 +604,6 @@ DEC_SIDE_ROWS = 0.92
 # stream, nothing deferred) -- the alternative DESIGN.md section 3.3 measures against the overlap with G1
 DEC_ADAM_BESIDE_G1 = True
 SERIAL_DEC_BLOCKS = 0  # (0: the library's default grid for the serial form)
-# timing probe only (results INVALID, never set by the product): the encoder half of Adam goes to the side stream
-# after the decoder half, unordered with the next step's G1 -- the upper bound of overlapping it with G1
-# (tools/enc_adam_probe.py)
-ENC_ADAM_SIDE_PROBE = False
 
 
 def clip_and_adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, max_norm=1.0, side_stream=None):
@@ -643,11 +639,8 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
             step_(P.data, G.data, M.data, V.data, clip_out=ws.clip_out)
         return
     dev = P.data.device
-    if ENC_ADAM_SIDE_PROBE and not (DEC_ADAM_BESIDE_G1 and ws.W_dec_t is None and ws.norm_part is not None):
-        raise RuntimeError("ENC_ADAM_SIDE_PROBE: only the side-stream decoder-row path carries the encoder half")
-    if not ENC_ADAM_SIDE_PROBE:
-        with _span("adam"):
-            step_(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), clip_out=ws.clip_out)
+    with _span("adam"):
+        step_(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), clip_out=ws.clip_out)
     if not DEC_ADAM_BESIDE_G1 and ws.W_dec_t is None and ws.norm_part is not None:
         # serial: the decoder half (+ the next step's norm partials) on this stream, the whole chip
         dec = [A.dec_part() for A in (P, G, M, V)]
@@ -703,8 +696,6 @@ def adam(ws, P, G, M, V, lr, beta1, beta2, eps, step, side_stream=None, clip_sum
                 done.wait(cur)
                 return None
 
-            if ENC_ADAM_SIDE_PROBE:
-                step_(P.enc_part(), G.enc_part(), M.enc_part(), V.enc_part(), clip_out=ws.clip_out)
             ws.norms_token = _norms_token(P)
             P.pending_rest = rest
             P.pending = None
