@@ -284,7 +284,9 @@ def launch_ranks(args, argv):
     n = args.gpus
     one_device = os.environ.get("CC_BENCH_ONE_DEVICE") == "1"  # rehearsal: every rank on cuda:0, gloo
     if not one_device and not args.launcher_check:
-        have = torch.cuda.device_count()  # (does not initialise the GPU)
+        # (torch counts through amdsmi on ROCm -- falling back to hipGetDeviceCount, which loads the HIP runtime
+        # without creating a context; the parent launches no kernel and never execs)
+        have = torch.cuda.device_count()
         if have < n:
             print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}; no measurement made",
                   file=sys.stderr, flush=True)

@@ -61,23 +61,6 @@
 #ifndef CC_EPI_STORE_WG_AUX
 #define CC_EPI_STORE_WG_AUX 2
 #endif
-// experiment switch (default 0): bit 0 = s_setprio 1 around each MFMA cluster; bit 1 = static priority 1 for
-// the second wave group (waves 4-7) from kernel start
-#ifndef CC_PP_PRIO
-#define CC_PP_PRIO 0
-#endif
-// timing probes of the K loop's energy (results invalid; never in the product): bit 0 = half the A fragment reads
-// from LDS, bit 1 = the steady-state K steps DMA the operands' first 4 K steps over and over (every operand byte an
-// L2 hit after the first pass, the MFMA operands still changing from step to step)
-#ifndef CC_PP_PROBE
-#define CC_PP_PROBE 0
-#endif
-// experiment switch: epilogue kinds (bitmask over Epi) whose K loop runs the super-phase form (pp_tile).  Default
-// 0 (every GEMM on the four-phase form): G3 alone on it is 6-10 µs faster, the step is not (2.5140 vs 2.5153 ms
-// over 4 alternating same-box rounds; profiles/r05_gemm_superphase_ab.txt, r05_ab_g3_superphase.txt)
-#ifndef CC_PP_SUPER_EPIS
-#define CC_PP_SUPER_EPIS 0
-#endif
 // Tile anatomy probe (build with -DCC_PP_STAMPS; GemmArgs::stamps set by the debug build's cc_debug_set_stamps):
 // thread 0 keeps s_memtime at tile entry (0), after the prologue's barrier (1), after the K loop (2), after the
 // drain before the epilogue (3) and after the epilogue's stores are issued (4), plus the 100 MHz wall clock at
@@ -99,12 +82,6 @@
 #define PP_STAMP_WRITE(args, bid)
 #endif
 // (PP_EPI_STAMP: gemm_epilogue.h)
-CC_DEV void pp_static_prio() {
-#if CC_PP_PRIO & 2
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
-}
-
 CC_DEV int pp_h(int k) { return ((k >> 1) & 1) | ((k >> 2) & 2); }
 
 // Per-lane source offset (bytes, step k0 = 0) of DMA ci (0..31) of a 256 x 64 operand tile, or
@@ -293,7 +270,6 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
   constexpr int BUF = 2 * TILE;
 
   PP_STAMP_DECL;
-  pp_static_prio();
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -363,12 +339,7 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
     if constexpr (TL == 2) {
       const int64_t ld = isA ? args.lda : args.ldb;
       const bool kc = isA ? AKC : BKC;
-#if CC_PP_PROBE & 2
-      const int kp = (kb0 + (T & 3)) * 64;
-      const int kadd = (int)(kc ? (int64_t)kp * 2 : (int64_t)kp * ld * 2);
-#else
       const int kadd = (int)(kc ? (int64_t)k0 * 2 : (int64_t)k0 * ld * 2);
-#endif
 #pragma unroll
       for (int q = 0; q < 2; ++q)  // (vo[p][q] == OOB lanes stay past the record count)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? ra : rb, (lds_void*)(dst + pp_ci(p, q, wave) * 1024), 16,
@@ -439,60 +410,8 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
   PP_STAMP(1);
 
   bf16x8 bfr[WG::TN][2];
-  // Two K-step forms, picked per epilogue kind at compile time (CC_PP_SUPER_EPIS, a bitmask over Epi):
-  // Super form -- two super-phases per K step instead of four phases: super-phase P = the old phases 2P and 2P+1 (A tiles
-  // 4P..4P+3 x both k-slices, 32 MFMAs; the B fragments of both k-slices read in P = 0), issuing the DMAs of
-  // both old phases, then vmcnt(4) (one super-phase's DMAs in flight) and the barrier.  Half the barriers and
-  // wave-group hand-offs per K step; every accumulator still adds k-slice 0 before k-slice 1 (the same bits).
-  // Regions: P = 0's DMAs (A of step t+1) overwrite what P = 1 of step t-1 read, P = 1's (B of step t+2) what
-  // P = 0 of step t read: both read sections retire their reads (lgkmcnt(0)) before their first barrier.
-  // +16 VGPRs (both k-slices' A fragments of a super-phase in flight; G3 212 -> 228).  Never for G1: beside it
-  // the side-stream decoder Adam (80 VGPRs) needs 2 x 216 + 80 <= 512 registers per SIMD lane; G2 and G4 + G5
-  // measured slower or neutral with it (profiles/r05_gemm_superphase_ab.txt).
-  auto kstep_super = [&](auto tail, int t) {
-    const char* la = smem + (t & 1) * BUF;
-    const char* lb = la + TILE;
-#pragma unroll
-    for (int P = 0; P < 2; ++P) {
-      __builtin_amdgcn_sched_barrier(0);
-      if (P == 0) {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int j = 0; j < WG::TN; ++j) {
-            const int c0 = wc * WG::WTN + 16 * j;
-            bfr[j][kk] = BKC ? pp_frag_kc(lb, c0, kc_off[kk]) : pp_frag_mn(lb, c0, kk, mn_off[(c0 >> 4) & 3]);
-          }
-      }
-      bf16x8 afr[4][2];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-          const int r0 = wr * WG::WTM + 16 * (4 * P + ii);
-          afr[ii][kk] = AKC ? pp_frag_kc(la, r0, kc_off[kk]) : pp_frag_mn(la, r0, kk, mn_off[(r0 >> 4) & 3]);
-        }
-      issue_t(tail, 2 * P, P == 0 ? t + 1 : t + 2);
-      issue_t(tail, 2 * P + 1, P == 0 ? t + 1 : t + 2);
-      wait_vmcnt<4>();
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-          for (int j = 0; j < WG::TN; ++j)
-            acc[4 * P + ii][j] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii][kk], acc[4 * P + ii][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-    }
-  };
-  // Phase form: four phases per K step.
-  auto kstep_phase = [&](auto tail, int t) {
+  // One K step: four phases.
+  auto kstep = [&](auto tail, int t) {
     const char* la = smem + (t & 1) * BUF;
     const char* lb = la + TILE;
 #pragma unroll
@@ -513,9 +432,6 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
         const int r0 = wr * WG::WTM + 16 * (ib + ii);
-#if CC_PP_PROBE & 1  // timing probe (results invalid): half the A fragment reads (A tiles 2, 3 reuse 0, 1)
-        if (ii >= 2) { afr[ii] = afr[ii - 2]; continue; }
-#endif
         afr[ii] = AKC ? pp_frag_kc(la, r0, kc_off[kk]) : pp_frag_mn(la, r0, kk, mn_off[(r0 >> 4) & 3]);
       }
       issue_t(tail, p, p < 2 ? t + 1 : t + 2);
@@ -526,26 +442,14 @@ CC_DEV float pp_tile(const GemmArgs& args, char* smem, int bid, int tid = thread
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-#if CC_PP_PRIO & 1
-      __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
         for (int j = 0; j < WG::TN; ++j)
           acc[ib + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], afr[ii], acc[ib + ii][j], 0, 0, 0);
-#if CC_PP_PRIO & 1
-      __builtin_amdgcn_s_setprio(0);
-#endif
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
     }
-  };
-  auto kstep = [&](auto tail, int t) {
-    if constexpr ((CC_PP_SUPER_EPIS >> EPI) & 1)
-      kstep_super(tail, t);
-    else
-      kstep_phase(tail, t);
   };
   int t = 0;
   // steady state: every DMA is an operand DMA
@@ -695,7 +599,11 @@ CC_DEV bool pp_wait_ready(const GemmArgs& a, char* smem) {
     ok = ready;
   }
   __syncthreads();
-  return ok != 0;
+  // every wave takes the word into a register before anyone may write PP_SLOT again (the abort path's tile claims
+  // broadcast through it at once): the waves of the workgroup all take the same branch
+  const bool r = __builtin_amdgcn_readfirstlane(ok) != 0;
+  __syncthreads();
+  return r;
 }
 
 // The launch's prologue reduction (GemmArgs::pre: reduce_rows' two phases, the same bits as cc_reduce_rows):

@@ -466,13 +466,15 @@ WGRAD_CLOCK_WORDS = 8  # floats at the end of the tile-sum scratch: 4 uint64 clo
 
 def wgrad_clock(tile_sum):
     """The clock words the fused G4G5 launches accumulate at the end of their tile-sum scratch, as a view
-    [shader-clock ticks, 100 MHz ticks, launches, reserved] (int64; zero them to start a window)."""
+    [shader-clock ticks, 100 MHz ticks, launches, reserved] (int64; zero them to start a window).  The scratch is
+    exactly cc_wgrad_tile_sums floats (_check_tile_sum), so the kernel's clock words are its last 8."""
     return tile_sum[-WGRAD_CLOCK_WORDS:].view(torch.int64)
 
 
 def _check_tile_sum(tile_sum, h, K):
-    if tile_sum.dtype != torch.float32 or not tile_sum.is_contiguous() or tile_sum.numel() < wgrad_tile_sums(h, K):
-        raise ValueError(f"tile_sum must be a contiguous fp32 buffer of >= {wgrad_tile_sums(h, K)} floats "
+    # (exactly: the launch writes its clock words after the tile sums, and wgrad_clock reads the buffer's last 8)
+    if tile_sum.dtype != torch.float32 or not tile_sum.is_contiguous() or tile_sum.numel() != wgrad_tile_sums(h, K):
+        raise ValueError(f"tile_sum must be a contiguous fp32 buffer of exactly {wgrad_tile_sums(h, K)} floats "
                          f"(cc_wgrad_tile_sums({h}, {K})), got {tuple(tile_sum.shape)} {tile_sum.dtype}")
 
 

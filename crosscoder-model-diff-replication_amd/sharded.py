@@ -32,6 +32,7 @@ import torch
 import torch.distributed as dist
 
 from . import engine, ops
+from .buffer import fingerprint as buffer_fingerprint
 from .crosscoder import CrossCoder, reference_init, write_checkpoint
 from .trainer import reference_loss, rounded
 
@@ -171,6 +172,9 @@ class HipShardBackend:
     def forward_partial(self, raw, factor):
         cc = self.cc
         ws = self.ws = cc._workspace(raw.shape[0])
+        # (a step that raised between carry_tail and loss_finalize must not leave the next step skipping its tail)
+        self._tail_carried = False
+        ws.tail_deferred = None
         engine.forward(ws, cc.arena(), cc.pad_input(raw), factor, loss=False)  # G1, norms, G2 -> fp32 partial recon
         return ws.recon
 
@@ -230,7 +234,9 @@ class HipShardBackend:
     def loss_finalize(self, red):
         if self._tail_carried:  # (the last d_acts launch ran it, into red[4:6] = self.red[4:6])
             self._tail_carried = False
-            assert red is self.red
+            if red is not self.red:
+                raise RuntimeError("loss_finalize: the carried loss tail wrote l1 / l0 into the backend's own reduce "
+                                   "buffer, not the one passed")
             return self.ws.scalars
         engine.loss_finalize(self.ws, l1l0_out=red[4:6])
         return self.ws.scalars
@@ -296,6 +302,7 @@ class ShardedTrainer:
         self.lr = cfg["lr"] * self.lr_lambda(0)
         self._host = None
         self.save_dir, self.save_version = None, 0  # rank 0's checkpoint directory (save())
+        self._verified = None  # the buffer's refresh_count whose fingerprint the ranks last compared
 
     def lr_lambda(self, step):
         if step < 0.8 * self.total_steps:
@@ -323,8 +330,23 @@ class ShardedTrainer:
         """Order torch's current stream after the last step's side-stream (decoder-half) Adam."""
         self.crosscoder.arena().wait_pending()
 
+    def _verify_buffer(self):
+        # once per buffer state: at the first step and after every refresh (next_raw refreshes after slicing the
+        # batch it returns, so each state is compared before the first batch taken from it)
+        gen = getattr(self.buffer, "refresh_count", 0)
+        if gen != self._verified:
+            verify_replicated(self.buffer.fingerprint(), self.group, gen)
+            self._verified = gen
+
     def step(self):
+        whole = hasattr(self.buffer, "fingerprint")
+        if whole:
+            self._verify_buffer()
         raw, factor = self.buffer.next_raw()
+        if whole:
+            self._verify_buffer()
+        else:  # (a batch source without the buffer protocol's fingerprint: every batch is compared, a host sync)
+            verify_replicated(buffer_fingerprint(raw, factor), self.group, self.step_counter)
         l1c = self.get_l1_coeff()
         self.t += 1
         self.engine.step(raw, factor, l1c, self.lr, (self.cfg["beta1"], self.cfg["beta2"]), 1e-8, self.t,
@@ -365,15 +387,22 @@ class ShardedTrainer:
         on it with a one-word all_reduce(MAX) at a step boundary -- never inside a step's collectives, never
         between the two Adam halves -- then all of them save and raise KeyboardInterrupt.  Normal completion
         saves too.  Any other exception may be one rank's alone: a save would then wait forever for the others,
-        so it propagates without the final checkpoint."""
+        so it propagates without the final checkpoint.  A second SIGINT on a rank whose flag is already set raises
+        KeyboardInterrupt at once (no checkpoint): the way out of a rank stuck in a collective."""
         import signal
         import threading
 
         self.step_counter = 0
         stop = [False]
         prev = None
+        def on_sigint(signum, frame):
+            if stop[0]:
+                signal.signal(signal.SIGINT, prev)
+                raise KeyboardInterrupt
+            stop[0] = True
+
         if threading.current_thread() is threading.main_thread():
-            prev = signal.signal(signal.SIGINT, lambda signum, frame: stop.__setitem__(0, True))
+            prev = signal.signal(signal.SIGINT, on_sigint)
         every = max(1, int(self.cfg.get("stop_check_every", 10)))
         interrupted = False
         try:
@@ -386,6 +415,9 @@ class ShardedTrainer:
                 if (i + 1) % every == 0 and self.agree_stop(stop[0]):
                     interrupted = True
                     break
+            # (a SIGINT after the last stop check: the ranks agree once more before the final save)
+            if not interrupted and self.total_steps % every and self.agree_stop(stop[0]):
+                interrupted = True
         finally:
             if prev is not None:
                 signal.signal(signal.SIGINT, prev)
@@ -399,6 +431,24 @@ class ShardedTrainer:
 
     def gather_state_dict(self, dst=None):
         return gather_state_dict(self.crosscoder, self.cfg["dict_size"], self.group, dst=dst)
+
+
+REPLICA_MISMATCH_MSG = ("latent-sharded step: the ranks' activation buffers differ (fingerprint {lo} .. {hi} across "
+                        "ranks after refresh {gen}) -- every rank must train on the same batch rows (SURVEY 8e): build "
+                        "the Buffer with group=<the trainer's group> so that one harvest and one permutation are "
+                        "shared, or give every rank an identically seeded SyntheticBuffer")
+
+
+def verify_replicated(fp, group=None, gen=0):
+    """Compare a fingerprint (buffer.fingerprint: the rows, their order and the normalisation factors) across the
+    group's ranks -- one all_reduce(MIN) and one all_reduce(MAX) of two int64 words -- and raise on every rank if
+    they differ (the all-reduced reconstruction would otherwise mix different batches silently)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    lo, hi = fp.to(dev), fp.to(dev).clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    if not torch.equal(lo, hi):
+        raise RuntimeError(REPLICA_MISMATCH_MSG.format(lo=lo.tolist(), hi=hi.tolist(), gen=gen))
 
 
 def agree_stop(flag, group=None):

@@ -101,19 +101,11 @@ class Trainer:
             return self.cfg["l1_coeff"] * self.step_counter / (0.05 * self.total_steps)
         return self.cfg["l1_coeff"]
 
-    def step_async(self, on_losses=None):
-        """Launch one full step (no host sync); returns the device scalars tensor, which torch's current
-        stream may read right away (it is ordered after the side-stream loss tail that writes it).
-        on_losses(scalars): called (on the side stream) right after the loss scalars are enqueued, before
-        the backward / clip / Adam launches."""
-        scalars, done = self._launch_step(on_losses)
-        done.wait(torch.cuda.current_stream(scalars.device))
-        return scalars
-
-    def _launch_step(self, on_losses, host=None, seq=0):
-        """The step's launches; returns (ws.scalars, the event that marks the loss tail's end, or None when
-        the tail writes the scalars to `host`, a _hip.MappedHostBuffer, and then `seq`).  step() does not
-        order torch's stream after the tail (the host waits for the sequence word instead)."""
+    def _launch_step(self, host, seq):
+        """The step's launches; the loss tail writes the scalars to `host` (a _hip.MappedHostBuffer), then `seq`:
+        the host waits for that word, not for a stream.  Only step() launches a step, and it checks the step's abort
+        word before the next one is launched (_check_abort): a timed-out G2 aborts exactly one step, whose rollback
+        of the optimizer's step count and LR schedule happens in that same step()."""
         cc = self.crosscoder
         raw, factor = self.buffer.next_raw()
         raw = cc.pad_input(raw)  # (zero columns only when d_in % 8 != 0)
@@ -123,12 +115,9 @@ class Trainer:
         side = self._side_stream()
         # prep, G1, G2 + the loss rows (one pass where decode_loss_t serves the shape)
         engine.forward(ws, P, raw, factor if getattr(self.buffer, "normalize", True) else None, finalize=False)
-        # the loss scalars: into mapped host memory from the G3 launch (host given), or on the side stream beside
-        # G3 (read by nothing on this stream) with on_losses
-        if on_losses is None:
-            done = engine.loss_finalize_with_g3(ws, side, host=host, seq=seq)
-        else:
-            done = engine.loss_finalize_beside(ws, side, on_losses, host=host, seq=seq)
+        # the loss scalars: into mapped host memory from the G3 launch (or, where G3 cannot carry the tail, from a
+        # launch on the side stream beside G3)
+        engine.loss_finalize_with_g3(ws, side, host=host, seq=seq)
         l1c = self.get_l1_coeff()
         # clip_grad_norm_(max_norm=1.0), trainer.py:46
         engine.backward(ws, P, opt.grads, l1c, clip=1.0)
@@ -140,7 +129,6 @@ class Trainer:
         self.scheduler.step()
         self._last_l1c = l1c
         self._last_ws = ws
-        return ws.scalars, done
 
     def _side_stream(self):
         # the decoder half of Adam (+ the next step's decoder norms / W_dec^T) runs here, beside the
@@ -173,7 +161,7 @@ class Trainer:
         if self._mapped is None:
             self._mapped = _hip.MappedHostBuffer(16)
         self._seq = (self._seq + 1) & 0xFFFFFFFF or 1
-        self._launch_step(None, host=self._mapped, seq=self._seq)
+        self._launch_step(self._mapped, self._seq)
         self._mapped.wait(8, self._seq)
         self._check_abort()  # (G2 timed out: raise in THIS step; its Adam launches applied nothing)
         s = [float(v) for v in self._mapped.f32[:6]]

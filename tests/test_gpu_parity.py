@@ -730,16 +730,18 @@ def test_dynamic_tile_order_is_bit_identical(gpu, dbg_lib, monkeypatch):
     assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
 
 
-def test_full_size_config2_trainer_steps_match_oracle(gpu, full_size_case):
+@pytest.mark.parametrize("total_batches,steps", [(100, 5), (10, 10)])
+def test_full_size_config2_trainer_steps_match_oracle(gpu, full_size_case, total_batches, steps):
     """BASELINE config 2 through the shipped schedule (Trainer.step: fused G2 + loss, G4G5 + grad tail + clip
     in one launch, encoder / decoder Adam halves on two streams) vs the oracle's fp32 OracleTrainer.step
-    (trainer.py:41-63) on the same bf16-valued inputs and init: FIVE steps on five different batches, through
-    the l1_coeff warm-up (num_tokens = 100 batches: l1_coeff 0, 0.4, 0.8, 1.2, 1.6): the 9-key loss dicts, the
-    clip total norm / coefficient, and params + both Adam moments after every step, within the SURVEY 8c bf16
-    envelope (bounds ~2x the values measured on MI355X; the parameter bounds grow with the step, as the two
-    precisions' Adam trajectories drift apart)."""
+    (trainer.py:41-63) on the same bf16-valued inputs and init, one different batch per step, every step:
+      * num_tokens = 100 batches, 5 steps: through the l1_coeff warm-up (l1_coeff 0, 0.4, 0.8, 1.2, 1.6);
+      * num_tokens = 10 batches, 10 steps -- the whole schedule: step 0 pure L2 (l1_coeff 0), then l1_coeff 2,
+        and steps 8-9 in lr_lambda's decay branch (trainer.py:28-32: lr 5e-5, then 2.5e-5 at step 9).
+    Checked: the 9-key loss dicts, the clip total norm / coefficient, and params + both Adam moments after every
+    step, within the SURVEY 8c bf16 envelope (bounds ~2x the values measured on MI355X; the parameter bounds grow
+    with the step, as the two precisions' Adam trajectories drift apart)."""
     cfg, P, buf0, factor0, _ = full_size_case
-    steps = 5
     B, n, d = 4096, 2, 2304
     bufs, factors = [], []
     for s in range(steps):
@@ -752,9 +754,10 @@ def test_full_size_config2_trainer_steps_match_oracle(gpu, full_size_case):
             f = factor0  # (Buffer's factor is estimated once and kept: buffer.py:34-41)
         bufs.append(b)
         factors.append(f)
-    cfg = dict(cfg, batch_size=B, num_tokens=B * 100, lr=5e-5, beta1=0.9, beta2=0.999, l1_coeff=2)
+    cfg = dict(cfg, batch_size=B, num_tokens=B * total_batches, lr=5e-5, beta1=0.9, beta2=0.999, l1_coeff=2)
     cc = make_cc(cfg, P, gpu, 2)
     tr = ca.Trainer(dict(cc.cfg), buffer=_Replay(bufs, factors, gpu), crosscoder=cc)
+    seen_decay = False
     torch.set_num_threads(max(1, torch.get_num_threads()))
     orc = O.OracleTrainer(dict(cfg, enc_dtype="fp32"), {k: v.float() for k, v in P.items()})
     lr = cfg["lr"]
@@ -768,6 +771,8 @@ def test_full_size_config2_trainer_steps_match_oracle(gpu, full_size_case):
         ref = orc.step(x32)
         assert list(d) == list(ref)
         assert d["l1_coeff"] == ref["l1_coeff"] and d["lr"] == ref["lr"], s
+        seen_decay |= d["lr"] < cfg["lr"]
+        print(f"step {s}: l1_coeff {d['l1_coeff']}, lr {d['lr']:.3e}, loss {d['loss']:.4f} (oracle {ref['loss']:.4f})")
         for k, tol in (("l2_loss", 1e-2), ("l1_loss", 1e-2), ("loss", 1e-2)):
             assert math.isclose(d[k], ref[k], rel_tol=tol, abs_tol=1e-6), (s, k, d[k], ref[k])
         for k in ("explained_variance", "explained_variance_A", "explained_variance_B"):
@@ -789,12 +794,63 @@ def test_full_size_config2_trainer_steps_match_oracle(gpu, full_size_case):
             print(f"step {s} {k}: params close {close:.4f}, worst (diff - 2 ulp) / lr {worst:.3f}, "
                   f"exp_avg rel {stats[k][2]:.2e}, exp_avg_sq rel {stats[k][3]:.2e}", flush=True)
         for k, (close, worst, em, ev) in stats.items():
-            # (measured over the 5 steps: close >= 0.994 W_enc / 0.996 others; worst <= 3.7 lr; W_enc's exp_avg
-            # rel grows 0.009 -> 0.045, the others' moments stay <= 0.034)
+            # (measured over the 5 warm-up steps: close >= 0.994 W_enc / 0.996 others; worst <= 3.7 lr; W_enc's
+            # exp_avg rel grows 0.009 -> 0.045, the others' moments stay <= 0.034)
             assert close >= (0.98 if k == "W_enc" else 0.99), (s, k, close)
-            assert worst <= 6.0, (s, k, worst)
-            tol = 0.1 if k == "W_enc" else 3e-2
+            assert worst <= 6.0 + 0.5 * max(0, s - 4), (s, k, worst)
+            tol = (0.1 if k == "W_enc" else 3e-2) * (1 + 0.25 * max(0, s - 4))
             assert em <= tol and ev <= 2 * tol, (s, k, em, ev)
+    assert d["l1_coeff"] == cfg["l1_coeff"] if total_batches == 10 else d["l1_coeff"] < cfg["l1_coeff"]
+    assert seen_decay == (total_batches == 10)
+
+
+def test_full_size_config2_fp32_mode_matches_oracle(gpu):
+    """north_star: "the set of active (ReLU > 0) latents must be bit-exact in an fp32 mode" -- at BASELINE config 2
+    (B 4096, 2x2304 -> 16384, K 4608) with enc_dtype "fp32", through the drop-in API (cc.encode, cc.get_losses,
+    backward through the autograd node) against the oracle's fp32 get_losses + autograd (crosscoder.py:69-130) on the
+    same inputs and init.  The active set must be identical wherever the oracle's pre-activation lies outside a
+    1e-5 * max|pre| guard band around 0 (inside it the two fp32 summation orders may round a near-zero sum to either
+    side); the in-band count is printed.  Losses and the four gradients: rel <= 1e-5."""
+    B, n, d, h = 4096, 2, 2304, 16384
+    cfg = {"seed": 49, "dict_size": h, "d_in": d, "enc_dtype": "fp32", "dec_init_norm": 0.08, "device": "cpu"}
+    P = O.init_params(cfg)
+    g = torch.Generator().manual_seed(7)
+    raw = torch.randn(B, n, d, generator=g) * torch.tensor([1 / 0.2759, 1 / 0.2442])[None, :, None]
+    factor = torch.tensor([(d ** 0.5) / raw[:, i].norm(dim=-1).mean().item() for i in range(n)])
+    x = O.buffer_next(raw, factor)
+    cc = make_cc(cfg, P, gpu, n)
+    xg = x.to(gpu)
+    with torch.no_grad():
+        acts = cc.encode(xg).cpu()
+    lo = cc.get_losses(xg)
+    (lo.l2_loss + 2.0 * lo.l1_loss).backward()
+    torch.cuda.synchronize()
+    ours = {k: getattr(lo, k).detach().cpu() for k in lo._fields}
+    grads = {k: getattr(cc, k).grad.detach().cpu() for k in O.PARAM_ORDER}
+    del lo
+    torch.set_num_threads(max(1, torch.get_num_threads()))
+    P32 = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    ref = O.get_losses(x, P32, torch.float32)
+    (ref["l2_loss"] + 2.0 * ref["l1_loss"]).backward()
+    with torch.no_grad():
+        pre = O.encode(x, P32, apply_relu=False)
+    band = pre.abs() > 1e-5 * pre.abs().max()
+    in_band = int((~band).sum().item())
+    flips_out = int(((acts > 0) != (pre > 0))[band].sum().item())
+    flips_in = int(((acts > 0) != (pre > 0))[~band].sum().item())
+    print(f"fp32 config 2: {pre.numel()} pre-activations, {in_band} inside the guard band "
+          f"({flips_in} of them on the other side of 0), {flips_out} flips outside it")
+    assert flips_out == 0
+    assert in_band <= 1e-4 * pre.numel()
+    for k in ("l2_loss", "l1_loss", "l0_loss", "explained_variance", "explained_variance_A", "explained_variance_B"):
+        e = rel(ours[k], ref[k].detach())
+        print(f"  {k}: rel {e:.2e}")
+        assert ours[k].dtype == ref[k].dtype and ours[k].shape == ref[k].shape, k
+        assert e <= 1e-5, (k, e)
+    for k in O.PARAM_ORDER:
+        e = rel(grads[k], P32[k].grad)
+        print(f"  grad {k}: rel {e:.2e}")
+        assert grads[k].stride() == P32[k].grad.stride() and e <= 1e-5, (k, e)
 
 
 # ----------------------------------------------------------------------------- batch slices / sharded

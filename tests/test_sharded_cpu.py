@@ -362,3 +362,129 @@ def test_sharded_train_sigint_on_one_rank_stops_all_ranks_at_one_step():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res == [(0, 4, 1, "interrupt"), (1, 4, 1, "interrupt")]
+
+
+# ----------------------------------------------------------------------------- one buffer for the whole group
+def _torch_gather(src, perm, out=None):
+    # (the tests of the group logic run the buffer on the CPU: torch indexing in place of cc_gather_rows)
+    out = torch.empty_like(src) if out is None else out
+    out.copy_(src[perm])
+    return out
+
+
+class _NoisyLM:
+    """The golden fake LM (table[token] + pos), plus `noise` x a rank-dependent offset: a stand-in for LM
+    forwards that are not bit-identical across ranks."""
+
+    class _C:
+        pass
+
+    def __init__(self, table, pos, noise=0.0):
+        self.table, self.pos, self.noise = table, pos, noise
+        self.cfg = _NoisyLM._C()
+        self.cfg.d_model = table.shape[1]
+
+    def run_with_cache(self, tokens, names_filter=None, return_type=None):
+        a = self.table[tokens] + self.pos[None, : tokens.shape[1]]
+        if self.noise:
+            a = a + self.noise * (1 + dist.get_rank())
+        return None, {names_filter: a}
+
+
+def _buffer_worker(rank, world, port, q, grouped, noise):
+    import json
+
+    import crosscoder_amd as ca
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        r = torch.load(os.path.join(os.path.dirname(__file__), "golden", "buffer_fake_lm.pt"), weights_only=True)
+        cfg = json.loads(r["cfg"])
+        ca.Buffer.gather_rows = staticmethod(_torch_gather)
+        # rank 0 draws the reference's permutations (seed 49, as the fixture); the other ranks' generators differ
+        torch.manual_seed(49 + 1000 * rank)
+        lms = [_NoisyLM(r[f"{m}_table"], r[f"{m}_pos"], noise) for m in ("A", "B")]
+        buf = ca.Buffer(cfg, *lms, r["tokens"], group=dist.group.WORLD if grouped else None)
+        batches, errors = [], []
+
+        class _T:  # ShardedTrainer's collaborators of _verify_buffer
+            buffer, group, _verified = buf, None, None
+
+        for _ in range(len(r["next"])):
+            try:
+                sharded.ShardedTrainer._verify_buffer(_T)
+            except RuntimeError as e:
+                errors.append(str(e))
+                _T._verified = buf.refresh_count
+            batches.append(buf.next().numpy().copy())
+        q.put((rank, batches, buf.normalisation_factor.numpy().copy(), buf.refresh_count, errors))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_buffer_ranks(world, grouped, noise):
+    port = 28000 + random.randint(0, 900)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_buffer_worker, args=(r, world, port, q, grouped, noise)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rk, batches, factor, refreshes, errors = q.get(timeout=300)
+        res[rk] = (batches, factor, refreshes, errors)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_grouped_buffer_equals_reference_buffer_on_every_rank(world):
+    """Buffer(group=...) (SURVEY 8e "replicate x"): each rank harvests a contiguous share of the LM batches and the
+    norm-estimate batches, the shares are broadcast, the permutation is drawn on rank 0 (torch's global CPU
+    generator, as buffer.py:111-113) and broadcast.  Every rank's normalisation factors and every next() batch,
+    across two refreshes, equal the reference Buffer's own outputs (tests/golden/buffer_fake_lm.pt, made by running
+    the reference), although the ranks' CPU generators differ; the fingerprint check passes at every refresh."""
+    r = torch.load(os.path.join(os.path.dirname(__file__), "golden", "buffer_fake_lm.pt"), weights_only=True)
+    res = _run_buffer_ranks(world, grouped=True, noise=0.0)
+    for rk in range(world):
+        batches, factor, refreshes, errors = res[rk]
+        assert errors == [] and refreshes >= 3
+        assert torch.equal(torch.from_numpy(factor), r["normalisation_factor"])
+        for got, want in zip(batches, r["next"]):
+            assert torch.equal(torch.from_numpy(got), want)
+
+
+def test_fingerprint_check_fires_when_ranks_harvest_alone():
+    """LM forwards that differ across ranks (a rank-dependent offset): with every rank harvesting on its own (the
+    reference Buffer per rank, group=None) the ranks' buffers differ and ShardedTrainer's fingerprint check raises
+    on every rank at every buffer state; with group=... the ranks share one harvest, their batches are identical and
+    the check passes."""
+    alone = _run_buffer_ranks(2, grouped=False, noise=1e-3)
+    for rk in range(2):
+        batches, _, refreshes, errors = alone[rk]
+        # (every buffer state a batch was taken from: the last refresh, by the last next(), served none)
+        assert len(errors) == refreshes - 1 and all("buffers differ" in e for e in errors), errors
+    assert not all(torch.equal(torch.from_numpy(a), torch.from_numpy(b)) for a, b in zip(alone[0][0], alone[1][0]))
+    shared = _run_buffer_ranks(2, grouped=True, noise=1e-3)
+    assert shared[0][3] == [] and shared[1][3] == []
+    for a, b in zip(shared[0][0], shared[1][0]):
+        assert torch.equal(torch.from_numpy(a), torch.from_numpy(b))
+
+
+def test_sigint_after_the_last_stop_check_still_stops_all_ranks():
+    """a SIGINT that arrives after the last `stop_check_every` boundary (total_steps not a multiple of
+    it) is not dropped: the ranks agree once more after the loop, save and raise KeyboardInterrupt."""
+
+    class _Odd(_Loop):
+        total_steps = 7
+
+    prev = signal.getsignal(signal.SIGINT)
+    late = _Odd(fail_at=7)
+    with pytest.raises(KeyboardInterrupt):
+        sharded.ShardedTrainer.train(late)
+    assert (late.n, late.saved) == (7, 1)
+    assert signal.getsignal(signal.SIGINT) is prev
