@@ -15,7 +15,7 @@ all-reduce of the fp32 partial reconstructions; every rank processes the same ba
 metric's own unit, on whatever workload runs.  At N = 1 that is config 2, the metric's config.  N > 1 runs
 config 3 (2^17 latents, as BASELINE.json's north_star asks), whose rows cost 8x a config-2 row, so its
 `value` is not comparable with the N = 1 line: the strong-scaling point of comparison is `n1_same_workload`
-(config 3 on one GPU, committed measurement), and `metric_equiv_acts_per_s` = value x n.d.h / (2.2304.16384)
+(config 3 on one GPU, measured in the same job on rank 0 before the sharded run), and `metric_equiv_acts_per_s` = value x n.d.h / (2.2304.16384)
 restates the throughput in config-2 rows of equal FLOP (10.n.d.h FLOP of step work per row).
 `latent_acts_per_s` = value x dict_size.
 
@@ -137,26 +137,105 @@ def rocprof_average(span):
     return None
 
 
-def n1_same_workload(B, n, d, h):
-    """The committed one-GPU bench line of the same workload (profiles/*_bench_configs.jsonl, measured by this
-    bench with --config on one MI355X), the 1-GPU point of an N > 1 strong-scaling curve -- or None."""
-    import glob
+def n1_same_workload(cfg, steps=10, warmup=3):
+    """The 1-GPU point of the N > 1 strong-scaling curve, measured INSIDE this job: rank 0 runs the same workload
+    (the whole dictionary) as a single-GPU Trainer on its own GPU before the sharded trainer is built, `warmup`
+    untimed then `steps` timed steps (barrier-free: one process), and frees it again.  Same synthetic buffer and
+    init as the sharded run."""
+    B = cfg["batch_size"]
+    cc = ca.CrossCoder(cfg)
+    buf = ca.SyntheticBuffer(cfg, rows=B * 8, n_models=cfg["n_models"], seed=0)
+    tr = ca.Trainer(cfg, buffer=buf, crosscoder=cc)
+    for _ in range(warmup):
+        tr.step()
+    tr.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.step()
+    tr.synchronize()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    words = clock_words(tr)
+    clk = effective_clock(words)
+    del tr, cc, buf
+    torch.cuda.empty_cache()
+    return {"value": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 4), "steps": steps, "warmup": warmup,
+            "effective_sclk_ghz": clk["effective_sclk_ghz"] if clk else None,
+            "source": "measured in this job: rank 0, one GPU, single-GPU Trainer on the whole dictionary, before "
+                      "the sharded run"}
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_bench_configs.jsonl")))
-    if not files:
-        return None
-    for line in open(files[-1]):
-        line = line.strip()
-        if not line.startswith("{"):
-            continue
-        r = json.loads(line)
-        c = r.get("config", {})
-        if r.get("n_gpus") == 1 and (c.get("global_batch"), c.get("n_models"), c.get("d_model"),
-                                       c.get("dict_size")) == (B, n, d, h):
-            # (value = rows / s, from the line's own step time)
-            return {"value": round(B / (r["ms_per_step"] * 1e-3), 1), "ms_per_step": r["ms_per_step"],
-                    "source": os.path.relpath(files[-1], ROOT)}
-    return None
+
+def _sync(dev):
+    if torch.device(dev).type == "cuda":
+        torch.cuda.synchronize()
+
+
+def timed_steps(tr, steps, dev="cuda"):
+    """Wall time per step of `steps` steps between barrier + synchronize on both sides, max over ranks."""
+    dist.barrier()
+    _sync(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.step()
+    _sync(dev)
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item() / steps
+
+
+def allreduce_algbw(rows, K, iters=10, dev="cuda"):
+    """Achieved bandwidth of one exchange slice's all-reduce alone (fp32 [rows, K], synchronous), the collective the
+    sharded step issues: algbw = bytes / time (max over ranks), busbw = algbw x 2 (G - 1) / G (ring traffic)."""
+    x = torch.ones(rows, K, device=dev)
+    for _ in range(2):
+        dist.all_reduce(x)
+    _sync(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(x)
+    _sync(dev)
+    t = torch.tensor([(time.perf_counter() - t0) / iters], device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = t.item() * 1e3
+    G = dist.get_world_size()
+    algbw = x.numel() * 4 / (ms * 1e-3) / 1e9
+    del x
+    return {"bytes": rows * K * 4, "ms": round(ms, 4), "algbw_GB_s": round(algbw, 1),
+            "busbw_GB_s": round(algbw * 2 * (G - 1) / G, 1)}
+
+
+def measure_exchange(tr, comm, K, dev="cuda", steps=5):
+    """The latent-sharded step's exchange, measured in warm-up (not the timed region): each candidate form ("auto":
+    all_reduce and reduce_scatter) runs one settling step and `steps` timed steps (max over ranks); the faster one
+    is left set on the trainer; plus the bandwidth one slice's all-reduce reaches alone.  Every rank picks the same
+    form (the times are all-reduced)."""
+    trial = {}
+    for c in (("all_reduce", "reduce_scatter") if comm == "auto" else (comm,)):
+        tr.engine.comm = c
+        tr.step()
+        trial[c] = round(timed_steps(tr, steps, dev) * 1e3, 4)
+    pick = min(trial, key=trial.get)
+    tr.engine.comm = pick
+    chunks = tr.backend.row_chunks()
+    return {"comm": pick, "chosen_by": "auto (faster in warm-up)" if comm == "auto" else "--comm",
+            "trial_ms_per_step": trial, "slices": len(chunks),
+            "slice_allreduce": allreduce_algbw(chunks[0][1] - chunks[0][0], K, dev=dev)}
+
+
+def exchange_exposed(kern, exchange):
+    """Move the attribution pass's exchange spans out of `kern` into `exchange`: the compute stream's idle time in
+    the exchange per step (events around each slice's wait / synchronous collective on the compute stream; each
+    bracketing event costs a few us) and in the 24-byte sums all-reduce."""
+    waits = {k: v for k, v in kern.items() if k.startswith("exchange_wait")}
+    exchange["exposed_ms_per_step"] = round(sum(waits.values()), 4)
+    exchange["exposed_ms_by_slice"] = {k[len("exchange_wait"):]: round(v, 4) for k, v in sorted(waits.items())}
+    exchange["sums_allreduce_ms"] = round(kern.get("sums_allreduce", 0.0), 4)
+    for k in list(waits) + ["sums_allreduce"]:
+        kern.pop(k, None)
+    return exchange
 
 
 def clock_words(tr):
@@ -375,8 +454,11 @@ def main():
     ap.add_argument("--d-model", type=int)
     ap.add_argument("--dict-size", type=int, help="the WHOLE dictionary (split over the ranks when N > 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--comm", choices=("all_reduce", "reduce_scatter"), default="all_reduce",
-                    help="latent-sharded step: the partial-reconstruction exchange")
+    ap.add_argument("--comm", choices=("auto", "all_reduce", "reduce_scatter"), default=None,
+                    help="latent-sharded step: the partial-reconstruction exchange (default N > 1: auto = time both "
+                         "during warm-up, run the faster; one rank: all_reduce)")
+    ap.add_argument("--no-n1", action="store_true",
+                    help="N > 1: skip the in-job one-GPU measurement of the same workload (n1_same_workload)")
     ap.add_argument("--recon-chunks", type=int, default=None,
                     help="latent-sharded step: batch slices the exchange is overlapped by (default 2)")
     ap.add_argument("--force-sharded", action="store_true",
@@ -448,13 +530,22 @@ def run_rank(args):
     else:
         from crosscoder_amd import sharded
 
+        n1 = None
+        if world > 1 and not args.no_n1:
+            # the strong-scaling curve's own 1-GPU point, measured in this job before the sharded trainer exists
+            if rank == 0:
+                n1 = n1_same_workload(cfg)
+            dist.barrier()
+        comm = args.comm or ("auto" if world > 1 else "all_reduce")
         buf = ca.SyntheticBuffer(cfg, rows=B * 8, n_models=n, seed=0)  # same seed on every rank: replicated batch
-        tr = sharded.ShardedTrainer(cfg, buffer=buf, comm=args.comm, recon_chunks=args.recon_chunks)
+        tr = sharded.ShardedTrainer(cfg, buffer=buf, comm="all_reduce" if comm == "auto" else comm,
+                                    recon_chunks=args.recon_chunks)
 
     timer = EventTimer()
     engine.TIMER = timer
     for _ in range(args.warmup):
         tr.step()
+    exchange = measure_exchange(tr, comm, K) if sharded_path else None
     # attribution pass (not timed): every kernel bracketed by events
     attrib = EventTimer()
     engine.TIMER = attrib
@@ -463,6 +554,8 @@ def run_rank(args):
         tr.step()
     torch.cuda.synchronize()
     kern = attrib.averages_ms()
+    if exchange is not None:
+        exchange_exposed(kern, exchange)
     gemms = {k: v for k, v in kern.items() if k.startswith("G")}
     dom = max(gemms, key=gemms.get)
     engine.TIMER = timer
@@ -540,9 +633,11 @@ def run_rank(args):
         "metric_equiv_acts_per_s": round(rows_per_s * per_row, 1),
         "metric_equiv_per_row": per_row,
         "latent_acts_per_s": round(rows_per_s * h_total, 1),
-        # N > 1: the same workload on one GPU (committed measurement), so the strong-scaling curve has its
-        # own 1-GPU point (the driver's N = 1 run is the metric's config 2, a different dictionary)
-        "n1_same_workload": n1_same_workload(B, n, d, h_total) if world > 1 else None,
+        # N > 1: the same workload on one GPU, measured in this job on rank 0 before the sharded run, so the
+        # strong-scaling curve has its own 1-GPU point (the driver's N = 1 run is the metric's config 2, a
+        # different dictionary): efficiency = value / (N x n1_same_workload.value)
+        "n1_same_workload": n1 if world > 1 else None,
+        "exchange": exchange,
         "step_mfma_frac": round(step_flop / step_s / 1e12 / (PEAK_BF16_TFLOPS * world), 4),
         "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items())},
         "roofline": {"bound": "mfma", "kernel": dom, "kernel_name": SPAN_KERNEL.get(dom), "kernel_ms": round(dom_ms, 4),

@@ -89,25 +89,32 @@ class ShardedStep:
         if len(chunks) == 1:
             # one slice: nothing to overlap, so a synchronous collective on the compute stream itself (torch
             # runs it there: no event hand-off to the collective stream and back, ~55 us on one GPU)
-            dist.all_reduce(recon, op=dist.ReduceOp.SUM, group=self.group)
+            with engine._span("exchange_wait0"):  # (bench attribution pass: the compute stream's time in it)
+                dist.all_reduce(recon, op=dist.ReduceOp.SUM, group=self.group)
             b.rows_ready(0, recon.shape[0], l1c)
             return
         # every slice's all-reduce is queued at once on the collective stream; the compute stream
         # waits for slice c only when it needs it
         works = [dist.all_reduce(recon[r0:r1], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
                  for r0, r1 in chunks]
-        for (r0, r1), w in zip(chunks, works):
-            w.wait()
+        for c, ((r0, r1), w) in enumerate(zip(chunks, works)):
+            # (bench attribution pass: events around the wait on the compute stream = the time the compute stream
+            # sits idle for slice c -- the exchange's exposed part)
+            with engine._span(f"exchange_wait{c}"):
+                w.wait()
             b.rows_ready(r0, r1, l1c)                # loss rows + g_recon + d_acts rows of the slice
 
     def _combine_reduce_scatter(self, recon, l1c):
         b = self.b
         r0, r1 = own_rows(recon.shape[0], self.world, self.rank, getattr(b, "row_align", 32))
         mine = b.own_recon_buffer(r1 - r0)
-        dist.reduce_scatter_tensor(mine, recon, op=dist.ReduceOp.SUM, group=self.group)
+        with engine._span("exchange_wait0"):
+            dist.reduce_scatter_tensor(mine, recon, op=dist.ReduceOp.SUM, group=self.group)
         b.loss_own_rows(mine, r0, r1)                # this rank's loss rows: g_recon rows, row terms
-        for out, inp in b.gather_pairs(r0, r1, self.world):
-            dist.all_gather_into_tensor(out, inp, group=self.group)
+        pairs = b.gather_pairs(r0, r1, self.world)
+        with engine._span("exchange_wait1"):
+            for out, inp in pairs:
+                dist.all_gather_into_tensor(out, inp, group=self.group)
         b.after_gather(l1c)                          # the whole batch's g_recon (+^T) -> d_acts (G3)
 
     def step(self, raw, factor, l1c, lr, betas, eps, t, max_norm=1.0, on_losses=None):
@@ -126,7 +133,8 @@ class ShardedStep:
         b.backward(l1c, red, self.rank)              # red[0:4] = local squared sums (b_dec on rank 0 only)
         # one 24-byte collective for the squared sums and l1 / l0: a synchronous collective runs on torch's
         # current stream (no hand-off to the collective stream and back)
-        dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
+        with engine._span("sums_allreduce"):
+            dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
         if on_losses is not None:
             # the host copy from the backend's auxiliary stream (forked here, one event): the compute
             # stream goes straight on to the clip + Adam launches

@@ -83,3 +83,84 @@ def test_effective_clock_from_tile_sum_words():
     assert rep["effective_sclk_ghz"] == pytest.approx(1.72)
     assert rep["launches"] == 3 and rep["window_ms"] == pytest.approx(1000.0)
     assert bench.effective_clock(None) is None
+
+
+def _load_bench():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    return bench
+
+
+class _FakeShardedTrainer:
+    """ShardedTrainer's surface measure_exchange uses (engine.comm, backend.row_chunks, step), with a step whose time
+    depends on the exchange form (reduce_scatter slower on rank 1: every rank must still pick the same form)."""
+
+    def __init__(self, rank):
+        import torch.distributed as dist
+
+        self.rank, self.dist = rank, dist
+        self.engine = type("E", (), {"comm": "all_reduce"})()
+        self.backend = type("Bk", (), {"row_chunks": staticmethod(lambda: [(0, 16), (16, 32)])})()
+        self.comms = []
+
+    def step(self):
+        import torch
+
+        self.comms.append(self.engine.comm)
+        time.sleep(0.002 if self.engine.comm == "all_reduce" else 0.004 + 0.004 * self.rank)
+        t = torch.ones(4)
+        self.dist.all_reduce(t)
+
+
+def _exchange_rank(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        bench = _load_bench()
+        tr = _FakeShardedTrainer(rank)
+        ex = bench.measure_exchange(tr, "auto", K=8, dev="cpu", steps=3)
+        kern = {"G1_encode": 0.5, "exchange_wait0": 0.12, "exchange_wait1": 0.01, "sums_allreduce": 0.02}
+        bench.exchange_exposed(kern, ex)
+        q.put((rank, ex, kern, tr.engine.comm, sorted(set(tr.comms))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_bench_exchange_fields_over_two_gloo_ranks():
+    """The N > 1 line's exchange evidence, its host logic over 2 gloo ranks: both exchange
+    forms are timed in warm-up (max over ranks), the faster is left set on the trainer -- the same on every rank --,
+    one slice's all-reduce bandwidth is measured, and the attribution pass's exchange spans become the exposed time
+    per step (removed from the kernel table)."""
+    import random
+
+    import torch.multiprocessing as mp
+
+    world, port = 2, 27000 + random.randint(0, 900)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_exchange_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in range(world):
+        ex, kern, comm, tried = res[rank]
+        assert tried == ["all_reduce", "reduce_scatter"] and comm == "all_reduce" == ex["comm"]
+        assert set(ex) == {"comm", "chosen_by", "trial_ms_per_step", "slices", "slice_allreduce",
+                           "exposed_ms_per_step", "exposed_ms_by_slice", "sums_allreduce_ms"}
+        assert ex["trial_ms_per_step"]["reduce_scatter"] > ex["trial_ms_per_step"]["all_reduce"] > 0
+        assert ex["slices"] == 2 and ex["slice_allreduce"]["bytes"] == 16 * 8 * 4
+        assert ex["slice_allreduce"]["busbw_GB_s"] == pytest.approx(ex["slice_allreduce"]["algbw_GB_s"], rel=0.01)
+        assert ex["exposed_ms_per_step"] == pytest.approx(0.13) and ex["sums_allreduce_ms"] == 0.02
+        assert ex["exposed_ms_by_slice"] == {"0": 0.12, "1": 0.01}
+        assert kern == {"G1_encode": 0.5}
+    # (the forms' times are all-reduced: both ranks report the same trial table)
+    assert res[0][0]["trial_ms_per_step"] == res[1][0]["trial_ms_per_step"]

