@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libcrosscoder_hip.so")
 DEBUG_LIB_PATH = os.path.join(_HERE, "libcrosscoder_hip_dbg.so")
 DEFAULT_PP_MASK = 7  # the ping-pong layouts both libraries default to (csrc/gemm.hip: g_pp_mask)
 DEBUG_SETTERS = ("cc_debug_set_pp_mask", "cc_debug_set_pp_fast", "cc_debug_set_dec_one_launch",
-                 "cc_debug_set_wave_sync", "cc_debug_set_epi_store")
+                 "cc_debug_set_wave_sync", "cc_debug_set_epi_store", "cc_debug_set_q4")
 
 CC_BF16 = 1
 CC_F32 = 2
@@ -162,6 +162,9 @@ def load_debug():
         lib.cc_debug_set_stamps.argtypes = [_p]
         lib.cc_debug_spin_ev.restype = _i
         lib.cc_debug_spin_ev.argtypes = [_i64, _i64, _p, _p]
+        lib.cc_debug_get_q4.restype = _i
+        lib.cc_debug_get_q4.argtypes = []
+        lib.q4_default = lib.cc_debug_get_q4()  # (the build's CC_Q4_MASK: the product library's fixed form)
         _debug = lib
     return _debug
 
@@ -182,6 +185,7 @@ def debug_library():
         dbg.cc_debug_set_dec_one_launch(1)
         dbg.cc_debug_set_wave_sync(0)
         dbg.cc_debug_set_epi_store(1)
+        dbg.cc_debug_set_q4(dbg.q4_default)
         _lib = prev
 
 

@@ -562,6 +562,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GemmArgs args) {
 }
 
 #include "gemm_pp.h"
+#include "gemm_q4_tile.h"
 
 // ---- G4 + G5 with the gradient tail in the same launch (the single-GPU step's backward end).
 // What the stand-alone tail kernel (cc_grad_tail) runs after the weight-gradient GEMMs, here inside
@@ -670,9 +671,16 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmAr
 //               (G1, G3), bit 1 KC/MN (G2), bit 2 MN/MN (G4, G5); the others run gemm_kernel
 //   pp_fast     the whole-tile ReLU epilogue form of G1 / G3 (same bits as the general form)
 //   dec_one     G2's main tiles and split-K units as one launch (0: two launches, same bits)
+//   q4          GEMMs on the 4-wave assembly K loop (gemm_q4_tile.h): bit 0 G1 (EPI_ENC, whole tiles), bit 1 G3 (EPI_DACTS,
+//               whole tiles); the same bits as their ping-pong launches
+#ifndef CC_Q4_MASK
+#define CC_Q4_MASK 0
+#endif
 #ifdef CC_DEBUG_HOOKS
-static int g_pp_mask = 7, g_pp_fast = 1, g_dec_one_launch = 1;
+static int g_pp_mask = 7, g_pp_fast = 1, g_dec_one_launch = 1, g_q4 = CC_Q4_MASK;
 #define CC_DEBUG_API extern "C" __attribute__((visibility("default")))
+CC_DEBUG_API void cc_debug_set_q4(int mask) { g_q4 = mask; }
+CC_DEBUG_API int cc_debug_get_q4() { return CC_Q4_MASK; }
 CC_DEBUG_API void cc_debug_set_pp_mask(int mask) { g_pp_mask = mask; }
 CC_DEBUG_API void cc_debug_set_pp_fast(int on) { g_pp_fast = on; }
 CC_DEBUG_API void cc_debug_set_dec_one_launch(int on) { g_dec_one_launch = on; }
@@ -728,7 +736,7 @@ CC_DEBUG_API int cc_debug_spin_ev(int64_t blocks, int64_t ns, void* stream, void
   return CC_OK;
 }
 #else
-constexpr int g_pp_mask = 7, g_pp_fast = 1, g_dec_one_launch = 1;
+constexpr int g_pp_mask = 7, g_pp_fast = 1, g_dec_one_launch = 1, g_q4 = CC_Q4_MASK;
 #endif
 // N = n*d multiple of 288 (and an MN-contiguous bf16 B operand): 256 x 288 tiles.  (The fp32
 // parity mode keeps 256 x 256: its 288-wide variant exceeds 256 VGPRs.)
@@ -808,6 +816,13 @@ static int launch_pp(GemmArgs a, hipStream_t st) {
     // whole tiles, ReLU on (encode: no l1 partials; d_acts: with G1's mask bits)
     if (g_pp_fast && a.M % BM == 0 && a.N % 256 == 0 &&
         (EPI == EPI_DACTS ? a.mask_bits != nullptr : a.flag && !a.wave_part0)) {
+      if constexpr (AKC && BKC) {
+        if ((g_q4 >> (EPI == EPI_ENC ? 0 : 1)) & 1 && a.K % 64 == 0 && a.K >= 128 && a.lda == a.ldb) {
+          hipLaunchKernelGGL((gemm_q4_kernel<EPI, true>), dim3(pp_grid(a.nbm * a.nbn)), dim3(Q4_THREADS), 0, st, a);
+          CC_LAUNCH_CHECK();
+          return CC_OK;
+        }
+      }
       hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, EPI, true>), dim3(pp_grid(a.nbm * a.nbn)), dim3(NTHR), 0, st, a);
       CC_LAUNCH_CHECK();
       return CC_OK;

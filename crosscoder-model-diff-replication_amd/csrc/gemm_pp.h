@@ -178,7 +178,7 @@ CC_DEV uint32_t piece_off(int ci, int lane, int rows, int cols, int ldo) {
 // writes transposed rows (tile columns) 32w .. 32w+31, 16 at a time; per store a row gets 64
 // contiguous bytes (lane groups g = 0..3 take row chunks 8g.. of a 32-row band), and a wave's 8
 // bands complete its 16 rows of 512 B.
-template <int AUX>
+template <int AUX, int NW = 8>  // (NW: waves of the workgroup; each writes 256 / NW tile columns)
 CC_DEV void pp_store_transposed(const GemmArgs& args, const char* smem, const int (&qb)[4], int m0, int n0, int rows,
                                 int cols, int lane, int wave) {
   const int64_t ldt = args.ldt;
@@ -186,8 +186,8 @@ CC_DEV void pp_store_transposed(const GemmArgs& args, const char* smem, const in
       make_rsrc((const char*)args.out_t + ((int64_t)n0 * ldt + m0) * 2, ((uint64_t)(cols - 1) * ldt + rows) * 2);
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int c0 = wave * 32 + s * 16;
+  for (int s = 0; s < 16 / NW; ++s) {
+    const int c0 = wave * (256 / NW) + s * 16;
     const int ca = c0 + 4 * p;  // address column of this lane
     const int c = c0 + i;       // column delivered to this lane
 #pragma unroll
@@ -557,14 +557,15 @@ struct TileLoop {
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  // after the tile and pp_tile_boundary()
-  CC_DEV void advance(char* smem) {
+  // after the tile and pp_tile_boundary(); slot_off: the broadcast word's LDS offset (the 4-wave q4 kernels keep it
+  // past their K-loop images, whose next prologue writes all of them)
+  CC_DEV void advance(char* smem, int slot_off = PP_SLOT) {
     if (!ctr) {
       if (wsync) wave_wait();
       i += nwx;
       return;
     }
-    int* slot = (int*)(smem + PP_SLOT);
+    int* slot = (int*)(smem + slot_off);
     if (threadIdx.x == 0) *slot = (int)nxt;
     __syncthreads();
     i = nwx + __builtin_amdgcn_readfirstlane(*slot);
@@ -579,9 +580,9 @@ struct TileLoop {
 // applying an update.
 // (smem: the broadcast word is the tile-claim slot, PP_SLOT, which no DMA writes before the first tile's prologue
 // barrier)
-CC_DEV bool pp_wait_ready(const GemmArgs& a, char* smem) {
+CC_DEV bool pp_wait_ready(const GemmArgs& a, char* smem, int slot_off = PP_SLOT) {
   if (!a.wait_ctr) return true;
-  int& ok = *(int*)(smem + PP_SLOT);
+  int& ok = *(int*)(smem + slot_off);
   if (threadIdx.x == 0) {
     const uint64_t t0 = wall_clock64();  // (the 100 MHz constant clock: the bound does not depend on sclk)
     int ready = 1;

@@ -1818,3 +1818,80 @@ def test_decode_partial_jobs_match_separate_launches(gpu, B, n, d, h):
         assert torch.equal(a, b)
     ref = acts.float() @ W.float()
     assert torch.allclose(out[True][0], ref, rtol=1e-3, atol=1e-3)
+
+
+# ----------------------------------------------------------------------------- the 4-wave assembly K loop (q4)
+@pytest.fixture
+def q4(dbg_lib):
+    """Selects which GEMMs run the 4-wave assembly K loop (debug build: cc_debug_set_q4 bit mask); restored after."""
+    yield dbg_lib.cc_debug_set_q4
+
+
+@pytest.mark.parametrize("B,h,K", [(4096, 16384, 4608), (512, 512, 256), (1024, 2048, 128), (768, 768, 192),
+                                   (2048, 1024, 4608)])
+@pytest.mark.parametrize("dynamic", [False, True])
+def test_q4_gemms_match_pingpong(gpu, q4, B, h, K, dynamic):
+    """G1 (encode: acts, acts^T, the activation-mask bits, column-sum and l0 slabs, with x.mean(0) as its prologue
+    job) and G3 (d_acts: g_pre^T, its column-sum slab, with the loss tail as its prologue job) on the 4-wave
+    assembly K loop (gemm_q4.h / q4_kloop.inc: two per-SIMD loop copies, nk = 2 and 3 through the tail steps) are
+    bit-identical to the 8-wave ping-pong launches -- the q4 wave's two halves run the ping-pong's epilogues as its
+    two "virtual waves" and the K loop accumulates in the same order.  Static and dynamic (per-XCD claims) tile
+    orders; every claim counter is back at 0 afterwards."""
+    g = torch.Generator().manual_seed(B + h + K)
+    bf = torch.bfloat16
+    x = torch.randn(B, K, generator=g).to(bf).to(gpu)
+    W = (torch.randn(h, K, generator=g) * 0.05).to(bf).to(gpu)
+    b_enc = (torch.randn(h, generator=g) * 0.1).to(bf).to(gpu)
+    tn = torch.rand(h, generator=g).to(gpu)
+    g_recon = (torch.randn(B, K, generator=g) * 1e-3).to(bf).to(gpu)
+    xpart = torch.randn(ops.prep_part_rows(B), K, generator=g).to(gpu)
+
+    def run(mask):
+        q4(mask)
+        ctr = torch.zeros(2, ops.TILE_CTR_WORDS, dtype=torch.int32, device=gpu) if dynamic else None
+        acts, acts_t = torch.empty(B, h, device=gpu, dtype=bf), torch.empty(h, B, device=gpu, dtype=bf)
+        colp = torch.zeros(ops.col_part_rows(B), h, device=gpu)
+        l0p = torch.zeros(ops.wave_parts(B, h), device=gpu)
+        bits = torch.zeros(ops.mask_bits_words(B, h), dtype=torch.int32, device=gpu)
+        xm = torch.zeros(K, device=gpu)
+        job = ops.colsum_job(xpart, xpart.shape[0], K, 1.0 / B, xm)
+        ops.encode_fwd_t(x, W, b_enc, acts, acts_t, True, colsum_part=colp, l0_part=l0p, mask_bits=bits,
+                         tile_ctr=ctr[0] if dynamic else None, pre=job)
+        gp_t = torch.empty(h, B, device=gpu, dtype=bf)
+        colp3 = torch.zeros(ops.col_part_rows(B), h, device=gpu)
+        ops.dacts_bwd_t(g_recon, W, acts, tn, 1e-4, gp_t, colsum_part=colp3, mask_bits=bits,
+                        tile_ctr=ctr[1] if dynamic else None)
+        torch.cuda.synchronize()
+        if dynamic:
+            assert int(ctr.abs().sum().item()) == 0
+        return acts, acts_t, colp, l0p, bits, xm, gp_t, colp3
+
+    pp = run(0)
+    q = run(3)
+    names = ("acts", "acts_t", "colsum_part", "l0_part", "mask_bits", "x_mean", "g_pre_t", "gpre_colpart")
+    for name, a, b in zip(names, q, pp):
+        assert torch.equal(a.view(torch.int16) if a.dtype == bf else a, b.view(torch.int16) if b.dtype == bf else b), name
+    assert pp[0].float().max() > 0 and (pp[6] != 0).any()
+
+
+def test_q4_trainer_steps_bit_identical(gpu, q4, full_size_case):
+    """Three full config-2 Trainer steps with G1 and G3 on the 4-wave assembly K loop (debug build) give the same
+    loss dicts, parameters and Adam moments, bit for bit, as the ping-pong step -- the G3 launch carries the loss tail
+    (its prologue job), G1 the x.mean(0) job, both take their tiles from the per-XCD counters."""
+    cfg, P, buf, factor, _ = full_size_case
+    outs = []
+    for mask in (0, 3):
+        q4(mask)
+        cc = make_cc(dict(cfg, batch_size=4096, num_tokens=4096 * 100, lr=5e-5, beta1=0.9, beta2=0.999,
+                          l1_coeff=2), P, gpu, 2)
+        tr = ca.Trainer(dict(cc.cfg), buffer=_Replay([buf] * 3, [factor] * 3, gpu), crosscoder=cc)
+        ds = [tr.step() for _ in range(3)]
+        tr.synchronize()
+        st = tr.optimizer.state
+        mom = [st[getattr(cc, k)][m].detach().clone() for k in O.PARAM_ORDER for m in ("exp_avg", "exp_avg_sq")]
+        outs.append((ds, cc.arena().data.clone(), mom))
+        del tr, cc
+    (d0, p0, m0), (d1, p1, m1) = outs
+    assert d0 == d1
+    assert torch.equal(p0, p1)
+    assert all(torch.equal(a, b) for a, b in zip(m0, m1))

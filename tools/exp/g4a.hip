@@ -9,7 +9,9 @@
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(4))) short bf16x4;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+namespace cc {
 #include "../../crosscoder-model-diff-replication_amd/csrc/gemm_q4.h"
+}  // namespace cc
 
 namespace g4a {
 __device__ __forceinline__ void tile_of_block(int bid, int nbm, int nbn, int& tm, int& tn) {
@@ -38,7 +40,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(const char* __restrict__ A
   tile_of_block(blockIdx.x, nbm, nbn, tm, tn);
   const int m0 = tm * 256, n0 = tn * 256;
   f32x4 acc[8][8];
-  cc::q4_kloop(acc, A + (int64_t)m0 * lda * 2, lda, (uint64_t)(M - m0) * lda * 2, B + (int64_t)n0 * ldb * 2, ldb,
+  cc::q4_kloop(acc, A + (int64_t)m0 * lda * 2, B + (int64_t)n0 * ldb * 2, lda, (uint64_t)(M - m0) * lda * 2,
                (uint64_t)(N - n0) * ldb * 2, K / 64, smem, lane, wave);
   const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C + ((int64_t)m0 * ldc + n0) * 2, (short)0,
                                                                      (int)(((uint64_t)255 * ldc + 256) * 2), 0x00020000);
@@ -64,7 +66,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(const char* __restrict__ A
 
 extern "C" int g4_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                             int64_t ldb, int64_t ldc, void* stream) {
-  if (M <= 0 || N <= 0 || K < 128 || (K % 64) || (N % 256) || (M % 256)) return 1;
+  if (M <= 0 || N <= 0 || K < 128 || (K % 64) || (N % 256) || (M % 256) || lda != ldb) return 1;
   const int nbm = (int)(M / 256), nbn = (int)(N / 256);
   hipLaunchKernelGGL(g4a::gemm_kernel, dim3(nbm * nbn), dim3(256), 0, (hipStream_t)stream, (const char*)A,
                      (const char*)B, (char*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, nbm, nbn);

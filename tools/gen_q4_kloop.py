@@ -23,7 +23,8 @@ SIMD id (HW_REG_HW_ID bit 4).  Tail: step nk - 2 (no DMAs; vmcnt(0) before the l
 (the ping-pong's KC layout: conflict-free ds_read_b128).
 
 No instruction here writes through the scalar data cache; M0 is saved and restored by the statement.
-Usage: python tools/gen_q4_kloop.py  (rewrites the .inc; the build compiles it, the generator is not run by it)
+Usage: python tools/gen_q4_kloop.py [out.inc [split|even|odd]]  (default: rewrites csrc/q4_kloop.inc, the per-SIMD
+split; the build compiles the .inc, it does not run the generator)
 """
 import os
 
@@ -90,7 +91,7 @@ def op(kind, arg):
         so = "0" if arg == 0 else f"%[oa{arg}]"
         return f"buffer_load_dwordx4 %[vda], %[rsa], {so} offen lds"
     if kind == "db":
-        so = "0" if arg == 0 else f"%[ob{arg}]"
+        so = "0" if arg == 0 else f"%[oa{arg}]"  # (the operands share their row stride: one set of piece offsets)
         return f"buffer_load_dwordx4 %[vdb], %[rsb], {so} offen lds"
     if kind == "m0inc":
         return "s_add_u32 m0, m0, 0x400"
@@ -143,7 +144,7 @@ def prologue():
         for opnd, m0 in (("a", "%[ma]"), ("b", "%[mb]")):
             out += [f"s_mov_b32 m0, {m0}", "s_nop 0"]
             for q in range(8):
-                so = "0" if q == 0 else f"%[o{opnd}{q}]"
+                so = "0" if q == 0 else f"%[oa{q}]"
                 out.append(f"buffer_load_dwordx4 %[vd{opnd}], %[rs{opnd}], {so} offen lds")
                 if q < 7:
                     out += ["s_add_u32 m0, m0, 0x400", "s_nop 0"]
@@ -158,13 +159,15 @@ def prologue():
     return out
 
 
-def program():
+def program(variant="split"):
+    """variant (experiments only): "split" = the per-SIMD copies; "even" / "odd" = every wave runs that copy."""
+    even, odd = {"split": (EVEN, ODD), "even": (EVEN, EVEN), "odd": (ODD, ODD)}[variant]
     L = prologue()
     L += ["s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 L_q4tail_%=",
           "s_getreg_b32 %[tmp], hwreg(HW_REG_HW_ID, 4, 1)", "s_cmp_eq_u32 %[tmp], 0", "s_cbranch_scc0 L_q4odd_%=",
           "L_q4even_%=:"]
-    L += step(EVEN) + ["s_cbranch_scc0 L_q4even_%=", "s_branch L_q4tail_%=", "L_q4odd_%=:"]
-    L += step(ODD) + ["s_cbranch_scc0 L_q4odd_%=", "L_q4tail_%=:"]
+    L += step(even) + ["s_cbranch_scc0 L_q4even_%=", "s_branch L_q4tail_%=", "L_q4odd_%=:"]
+    L += step(odd) + ["s_cbranch_scc0 L_q4odd_%=", "L_q4tail_%=:"]
     L += step(TAIL_A) + step(TAIL_B)
     # (the last MFMAs' results are read by the epilogue's v_accvgpr_read: 19 wait states)
     L += ["s_nop 7", "s_nop 7", "s_nop 2", "s_mov_b32 m0, %[msave]"]
@@ -172,7 +175,10 @@ def program():
 
 
 def main():
-    prog = program()
+    import sys
+
+    out = sys.argv[1] if len(sys.argv) > 1 else OUT
+    prog = program(sys.argv[2] if len(sys.argv) > 2 else "split")
     n_mfma = sum(1 for l in prog if l.startswith("v_mfma"))
     assert n_mfma == 4 * 128, n_mfma
     lines = []
@@ -182,13 +188,13 @@ def main():
     acc_ops = ", ".join(f'"+{{a[{4 * (8 * j + i)}:{4 * (8 * j + i) + 3}]}}"(ACC[{i}][{j}])'
                         for j in range(8) for i in range(8))
     clob = ", ".join(f'"v{r}"' for r in range(4, 132))
-    with open(OUT, "w") as f:
+    with open(out, "w") as f:
         f.write("// GENERATED by tools/gen_q4_kloop.py -- do not edit.  The 4-wave GEMM's K loop as one inline-asm\n"
                 "// statement (see the generator's docstring for the schedule).\n")
         f.write("#define Q4_KLOOP_ASM \\\n" + " \\\n".join(lines) + "\n")
         f.write(f"#define Q4_ACC_OPERANDS(ACC) {acc_ops}\n")
         f.write(f"#define Q4_FRAG_CLOBBERS {clob}\n")
-    print(f"wrote {OUT}: {len(prog)} instructions ({n_mfma} MFMAs)")
+    print(f"wrote {out}: {len(prog)} instructions ({n_mfma} MFMAs)")
 
 
 if __name__ == "__main__":
