@@ -818,7 +818,10 @@ static int launch_pp(GemmArgs a, hipStream_t st) {
         (EPI == EPI_DACTS ? a.mask_bits != nullptr : a.flag && !a.wave_part0)) {
       if constexpr (AKC && BKC) {
         if ((g_q4 >> (EPI == EPI_ENC ? 0 : 1)) & 1 && a.K % 64 == 0 && a.K >= 128 && a.lda == a.ldb) {
-          hipLaunchKernelGGL((gemm_q4_kernel<EPI, true>), dim3(pp_grid(a.nbm * a.nbn)), dim3(Q4_THREADS), 0, st, a);
+          if constexpr (EPI == EPI_ENC)
+            hipLaunchKernelGGL((gemm_q4_enc_kernel<true>), dim3(pp_grid(a.nbm * a.nbn)), dim3(Q4_THREADS), 0, st, a);
+          else
+            hipLaunchKernelGGL((gemm_q4_kernel<EPI, true>), dim3(pp_grid(a.nbm * a.nbn)), dim3(Q4_THREADS), 0, st, a);
           CC_LAUNCH_CHECK();
           return CC_OK;
         }

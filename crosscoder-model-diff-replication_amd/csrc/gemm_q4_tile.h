@@ -138,7 +138,7 @@ CC_DEV void q4_tile(const GemmArgs& args, char* smem, int bid, int tid, float (&
 
 // G1 / G3 (EPI_ENC / EPI_DACTS) as a persistent q4 launch: gemm_pp_kernel's jobs and tile loop, q4 tiles.
 template <int EPI, bool FAST>
-__global__ __launch_bounds__(Q4_THREADS, 1) void gemm_q4_kernel(const GemmArgs args) {
+CC_DEV void q4_kernel_body(const GemmArgs& args) {
   __shared__ __attribute__((aligned(16))) char smem[Q4_LDS_ALL];
   q4_prologue_reduce(args, smem);
   q4_prologue_loss_tail(args, smem);
@@ -156,4 +156,18 @@ __global__ __launch_bounds__(Q4_THREADS, 1) void gemm_q4_kernel(const GemmArgs a
     pp_tile_boundary();
     L.advance(smem, Q4_SLOT);
   }
+}
+template <int EPI, bool FAST>
+__global__ __launch_bounds__(Q4_THREADS, 1) void gemm_q4_kernel(const GemmArgs args) {
+  q4_kernel_body<EPI, FAST>(args);
+}
+// G1 runs beside the side-stream decoder-half Adam (80 VGPRs per wave): capped so that a q4 wave (this many VGPRs +
+// its 256 AGPRs) leaves one Adam wave room on each SIMD, as the ping-pong's 2 x 216 registers did
+#ifndef CC_Q4_ENC_VGPRS
+#define CC_Q4_ENC_VGPRS 160
+#endif
+template <bool FAST>
+__global__ __launch_bounds__(Q4_THREADS, 1) __attribute__((amdgpu_num_vgpr(CC_Q4_ENC_VGPRS))) void gemm_q4_enc_kernel(
+    const GemmArgs args) {
+  q4_kernel_body<EPI_ENC, FAST>(args);
 }
