@@ -98,7 +98,7 @@ SPAN_EVERY = 4  # timed steps per roofline-kernel sample (events around the laun
 
 # span name -> kernel-name prefix in the rocprofv3 traces
 SPAN_KERNEL = {"G1_encode": "gemm_pp_kernel<true, true, 1", "G2_decode": "gemm_pp_main_splitk_kernel<true, false, 7",
-               "G3_dacts": "gemm_pp_kernel<true, true, 3", "G4G5_wgrad": "gemm_pp_dual_tail_kernel<true, true, 4, 5>",
+               "G3_dacts": "gemm_q4_kernel<3, true>", "G4G5_wgrad": "gemm_pp_dual_tail_kernel<true, true, 4, 5>",
                "adam": "adam_bulk_kernel"}
 
 

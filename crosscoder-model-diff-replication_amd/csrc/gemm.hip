@@ -672,9 +672,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp_dual_tail_kernel(const GemmAr
 //   pp_fast     the whole-tile ReLU epilogue form of G1 / G3 (same bits as the general form)
 //   dec_one     G2's main tiles and split-K units as one launch (0: two launches, same bits)
 //   q4          GEMMs on the 4-wave assembly K loop (gemm_q4_tile.h): bit 0 G1 (EPI_ENC, whole tiles), bit 1 G3 (EPI_DACTS,
-//               whole tiles); the same bits as their ping-pong launches
+//               whole tiles); the same bits as their ping-pong launches.  The product runs G3 on it (its kernel -10 us, the
+//               step -2.5 / -4 us); G1 on it is faster alone but slows the side-stream decoder-half Adam beside it, +14 to
+//               +27 us per step (profiles/r06_ab_q4_step.txt)
 #ifndef CC_Q4_MASK
-#define CC_Q4_MASK 0
+#define CC_Q4_MASK 2
 #endif
 #ifdef CC_DEBUG_HOOKS
 static int g_pp_mask = 7, g_pp_fast = 1, g_dec_one_launch = 1, g_q4 = CC_Q4_MASK;
