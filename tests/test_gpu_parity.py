@@ -859,10 +859,25 @@ def test_full_size_config2_fp32_mode_matches_oracle(gpu):
         print(f"  {k}: rel {e:.2e}")
         assert ours[k].dtype == ref[k].dtype and ours[k].shape == ref[k].shape, k
         assert e <= 1e-5, (k, e)
+    # The gradients: the few in-band latents whose ReLU went the other way route a batch row's whole d_acts into (or
+    # out of) g_pre, which moves W_enc / b_enc's gradients by ~1e-3 relative (measured 1.0e-3 with 14 flips) -- an
+    # active-set effect, not accumulation error.  So the oracle's backward is also run with the GPU's active set
+    # (acts = pre * [GPU acts > 0], the same crosscoder.py:96-130 loss): against that, every gradient within 1e-5.
+    mask = (acts > 0).float()
+    P32m = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    pre_m = O.encode(x, P32m, apply_relu=False)
+    acts_m = pre_m * mask
+    recon_m = O.decode(acts_m, P32m)
+    l2_m = (recon_m.float() - x.float()).pow(2).sum(dim=(1, 2)).mean()
+    l1_m = (acts_m * P32m["W_dec"].norm(dim=-1).sum(dim=1)[None, :]).sum(-1).mean(0)
+    (l2_m + 2.0 * l1_m).backward()
     for k in O.PARAM_ORDER:
         e = rel(grads[k], P32[k].grad)
-        print(f"  grad {k}: rel {e:.2e}")
-        assert grads[k].stride() == P32[k].grad.stride() and e <= 1e-5, (k, e)
+        em = rel(grads[k], P32m[k].grad)
+        print(f"  grad {k}: rel {e:.2e} (oracle's own active set), {em:.2e} (the GPU's active set)")
+        assert grads[k].stride() == P32[k].grad.stride(), k
+        assert em <= 1e-5, (k, em)
+        assert e <= 5e-3, (k, e)
 
 
 # ----------------------------------------------------------------------------- batch slices / sharded
