@@ -11,6 +11,7 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 40
     short = lambda s: s.split("(")[0].replace("void ", "").replace("cc::", "")[:52]  # noqa: E731
     starts = [i for i, r in enumerate(tr) if "prep_kernel" in r["Kernel_Name"]]
+    n = min(n, len(starts) - 1)  # (consecutive prep launches: n + 1 of them bound n steps)
     steps = list(zip(starts[-n - 1:-1], starts[-n:]))
     spans, rows, idle = [], {}, []
     for a, b in steps:
