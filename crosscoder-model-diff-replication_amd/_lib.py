@@ -64,7 +64,8 @@ SIGNATURES = {
     "cc_decode_fwd": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "cc_decode_ws_floats": (_i64, [_i64, _i64, _i64, _i]),
     "cc_decode_fwd_ws": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
-    "cc_decode_partial": (_i, [_p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
+    "cc_decode_partial": (_i, [_p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _p, _i64, _i64, _i64,
+                               _i64, _i, _p]),
     "cc_decode_fwd_ws_t": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_loss_fwd_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i, _p]),
     "cc_loss_fwd_bwd_rows": (_i, [_p, _p, _p, _p, _p, _p, _p, _f, _i64, _i64, _i64, _i64, _i64, _i, _p]),
@@ -81,7 +82,7 @@ SIGNATURES = {
     "cc_wgrad_both_clip_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p,
                                   _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_i64), _i, _f, _i, _p, _p, _p, _p, _p, _i, _p]),
     "cc_wgrad_both_sums_t": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p,
-                                  _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_i64), _i, _i, _p, _p, _p, _p, _i, _p]),
+                                  _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_i64), _i, _i, _p, _p, _p, _p, _p, _i, _p]),
     "cc_wgrad_both": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "cc_clip_finalize": (_i, [_p, ctypes.POINTER(_i64), _i, _f, _i, _p, _p]),
     "cc_grad_tail": (_i, [_p, _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _i, _p, ctypes.POINTER(_i64), _i, _f, _i, _p,

@@ -1046,8 +1046,11 @@ int64_t cc_decode_ws_floats(int64_t B, int64_t h, int64_t K, int dtype) {
 template <bool BKC>
 static int decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, float* ws, int64_t ws_floats,
                          int64_t B, int64_t h, int64_t K, int dtype, hipStream_t st, const cc_colsum_job* pre = nullptr,
-                         const NormFin& nf = NormFin{}) {
+                         const NormFin& nf = NormFin{}, const uint32_t* wait_ctr = nullptr, uint32_t wait_target = 0,
+                         uint32_t* wait_err = nullptr) {
   if (!recon_f32) return CC_ERR_NULL;
+  // (the in-kernel wait: the ping-pong kernels' pp_wait_ready, bf16 only)
+  if (wait_ctr && (dtype != CC_BF16 || !use_pp(K, true, BKC, dtype))) return CC_ERR_SHAPE;
   DecPlan p;
   const bool split = dec_plan(B, h, K, dtype, p);
   const int64_t ldb = BKC ? h : K;
@@ -1057,6 +1060,7 @@ static int decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, 
     a.A = acts; a.lda = h; a.B = W_dec; a.ldb = ldb;
     a.M = (int)B; a.N = (int)K; a.K = (int)h;
     a.out_f32 = recon_f32; a.ldo = K;
+    a.wait_ctr = wait_ctr; a.wait_target = wait_target; a.wait_err = wait_err;
     int rc = check_gemm(a, dtype, true, BKC);
     if (rc) return rc;
     if (pre) {  // (the job runs in the ping-pong kernels' prologue only: else its stand-alone launches first)
@@ -1083,6 +1087,7 @@ static int decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, 
   a.A = acts; a.lda = h; a.B = W_dec; a.ldb = ldb;
   a.M = (int)B; a.N = p.nbn_main * 256; a.K = (int)h;
   a.out_f32 = recon_f32; a.ldo = K;
+  a.wait_ctr = wait_ctr; a.wait_target = wait_target; a.wait_err = wait_err;
   int rc = check_gemm(a, dtype, true, BKC);
   if (rc) return rc;
   if (pre && (rc = set_pre(a, pre))) return rc;
@@ -1090,6 +1095,7 @@ static int decode_fwd_ws(const void* acts, const void* W_dec, float* recon_f32, 
   t.A = acts; t.lda = h; t.B = (const bf16_t*)W_dec + (int64_t)p.nbn_main * 256 * (BKC ? h : 1); t.ldb = ldb;
   t.M = (int)B; t.N = p.tail_cols; t.K = (int)h;
   t.out = ws; t.ldo = p.tail_cols;
+  t.wait_ctr = wait_ctr; t.wait_target = wait_target; t.wait_err = wait_err;
   t.nbm = (t.M + BM - 1) / BM;
   t.nbn = (t.N + 255) / 256;
   if (g_dec_one_launch) {
@@ -1129,11 +1135,13 @@ int cc_decode_fwd_ws_t(const void* acts, const void* W_dec_t, float* recon_f32, 
 
 int cc_decode_partial(const void* acts, const void* W_dec, float* recon_f32, float* ws, int64_t ws_floats,
                       const float* norm_part, float* norms, float* tn, float* inv_norms, const cc_colsum_job* pre,
-                      int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream) {
+                      const uint32_t* wait_ctr, uint32_t wait_target, uint32_t* wait_err, int64_t B, int64_t h,
+                      int64_t n, int64_t d, int dtype, void* stream) {
   if (norm_part && (!norms || !tn || d % 64)) return norms && tn ? CC_ERR_SHAPE : CC_ERR_NULL;
   NormFin nf = {};
   if (norm_part) nf = NormFin{norm_part, (int)h, (int)n, (int)(d / 64), norms, tn, inv_norms};
-  return decode_fwd_ws<false>(acts, W_dec, recon_f32, ws, ws_floats, B, h, n * d, dtype, (hipStream_t)stream, pre, nf);
+  return decode_fwd_ws<false>(acts, W_dec, recon_f32, ws, ws_floats, B, h, n * d, dtype, (hipStream_t)stream, pre, nf,
+                              wait_ctr, wait_target, wait_err);
 }
 
 }  // extern "C"
@@ -1472,7 +1480,12 @@ int cc_wgrad_both_t(const void* actsT, const void* g_reconT, const void* W_dec, 
   return CC_OK;
 }
 
-// (step_kernels.hip, library-internal: cc_grad_tail with the step's abort word)
+// (step_kernels.hip, library-internal: cc_grad_tail / cc_grad_tail_sums with the step's abort word)
+extern "C" int cc_grad_tail_sums_abort(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc,
+                                       float* sq_b_enc, const float* loss_colpart, int64_t R_dec, int64_t K,
+                                       void* g_b_dec, float* sq_b_dec, int dtype, const float* sq, const int64_t* off,
+                                       int nparams, int zero_mask, float* out, uint32_t* counter,
+                                       const uint32_t* abort, void* stream);
 extern "C" int cc_grad_tail_abort(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,
                                   const float* loss_colpart, int64_t R_dec, int64_t K, void* g_b_dec, float* sq_b_dec,
                                   int dtype, const float* sq, const int64_t* off, int nparams, float max_norm,
@@ -1504,8 +1517,8 @@ static int wgrad_both_tail(const void* actsT, const void* g_reconT, const void* 
                          grad_W_enc, sq_enc, B, h, n, d, dtype, stream);
     if (rc) return rc;
     if (sums_only)
-      return cc_grad_tail_sums(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec, sq_b_dec,
-                               dtype, sq, off, nparams, zero_mask, out, counter, stream);
+      return cc_grad_tail_sums_abort(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec,
+                                     sq_b_dec, dtype, sq, off, nparams, zero_mask, out, counter, abort, stream);
     return cc_grad_tail_abort(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec, sq_b_dec,
                               dtype, sq, off, nparams, max_norm, emulate_bf16, out, counter, abort, stream);
   }
@@ -1561,11 +1574,11 @@ int cc_wgrad_both_sums_t(const void* actsT, const void* g_reconT, const void* W_
                          const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
                          const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
                          const int64_t* off, int nparams, int zero_mask, float* out, uint32_t* counter, float* tile_sum,
-                         uint32_t* tile_ctr, int dtype, void* stream) {
+                         uint32_t* tile_ctr, const uint32_t* abort, int dtype, void* stream) {
   return wgrad_both_tail(actsT, g_reconT, W_dec, inv_norms, colsum_acts, l1_scale, grad_W_dec, sq_dec, g_preT, xT,
                          grad_W_enc, sq_enc, B, h, n, d, gpre_colpart, R_enc, g_b_enc, sq_b_enc, loss_colpart, R_dec,
                          g_b_dec, sq_b_dec, sq, off, nparams, 0.f, 0, 1, zero_mask, out, counter, tile_sum, tile_ctr,
-                         nullptr, dtype, stream);
+                         abort, dtype, stream);
 }
 
 int cc_wgrad_both(const void* acts, const void* g_recon, const void* W_dec, const float* inv_norms,

@@ -146,9 +146,13 @@ CC_DEV void clip_finish(const ClipArgs& a, const double* s, double (*red)[NT / 6
   if (a.sums_only) {
     if (threadIdx.x < a.nparams) {
       const int p = threadIdx.x;
+      // (the step was aborted -- G2's in-kernel wait timed out, ClipArgs::abort: -inf for every parameter, so the
+      // sums' all-reduce carries the abort to every rank and each Adam launch that forms its coefficient from them
+      // applies nothing, adam_coef.  Each of these threads reads the word itself.)
+      const bool ab = a.abort && __hip_atomic_load(a.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
       double t = 0.0;
       for (int w = 0; w < NT / 64; ++w) t += red[p][w];
-      a.out[p] = (a.zero_mask >> p) & 1 ? 0.f : (float)t;
+      a.out[p] = ab ? -__builtin_inff() : ((a.zero_mask >> p) & 1 ? 0.f : (float)t);
     }
     return;
   }

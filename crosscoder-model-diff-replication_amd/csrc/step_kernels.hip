@@ -395,8 +395,12 @@ CC_DEV void adam_signal_done(unsigned* ctr) {
 CC_DEV float adam_coef(const AdamArgs& a) {
   if (a.clip_sums) {
     float norms[8], total;
-    for (int p = 0; p < a.clip_np; ++p) norms[p] = clip_param_norm((double)a.clip_sums[p], a.clip_emulate);
-    const float c = clip_coef(norms, a.clip_np, a.clip_max_norm, a.clip_emulate, total);
+    bool aborted = false;  // (a negative squared sum: a rank's step was aborted -- ClipArgs::sums_only writes -inf)
+    for (int p = 0; p < a.clip_np; ++p) {
+      aborted |= a.clip_sums[p] < 0.f;
+      norms[p] = clip_param_norm((double)a.clip_sums[p], a.clip_emulate);
+    }
+    const float c = aborted ? CC_CLIP_ABORTED : clip_coef(norms, a.clip_np, a.clip_max_norm, a.clip_emulate, total);
     if (a.clip_out && blockIdx.x == 0 && threadIdx.x == 0) {
       a.clip_out[0] = c;
       a.clip_out[1] = total;
@@ -1058,6 +1062,16 @@ int cc_grad_tail_abort(const float* gpre_colpart, int64_t R_enc, int64_t h, void
                        float* clip_out, uint32_t* counter, const uint32_t* abort, void* stream) {
   return grad_tail(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec, sq_b_dec, dtype, sq,
                    off, nparams, max_norm, emulate_bf16, 0, 0, clip_out, counter, stream, abort);
+}
+
+// (library-internal: cc_grad_tail_sums with the step's abort word -- the latent-sharded step's fallback form)
+extern "C" int cc_grad_tail_sums_abort(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc,
+                                       float* sq_b_enc, const float* loss_colpart, int64_t R_dec, int64_t K,
+                                       void* g_b_dec, float* sq_b_dec, int dtype, const float* sq, const int64_t* off,
+                                       int nparams, int zero_mask, float* out, uint32_t* counter,
+                                       const uint32_t* abort, void* stream) {
+  return grad_tail(gpre_colpart, R_enc, h, g_b_enc, sq_b_enc, loss_colpart, R_dec, K, g_b_dec, sq_b_dec, dtype, sq,
+                   off, nparams, 0.f, 0, 1, zero_mask, out, counter, stream, abort);
 }
 
 int cc_grad_tail_sums(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,

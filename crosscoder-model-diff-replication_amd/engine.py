@@ -347,8 +347,11 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
         ops.reduce_rows(ws.x_colpart, ws.x_colpart.shape[0], K, scale=1.0 / B, out_f32=ws.x_mean)
     acts_job = ops.colsum_job(ws.acts_colpart, ws.acts_colpart.shape[0], h, 1.0, ws.colsum_acts)
     fused_g2 = bool(loss and ws.fused_ncb)
+    # the latent-sharded step's G2 (decode_partial_jobs: W_dec read as stored, bf16) waits in its kernel too
+    partial_g2 = bool(not loss and ws.tr and ws.W_dec_t is None)
     # (only while the decoder norms are the Adam's own: otherwise decoder_norms below reads W_dec on this stream)
-    wait = P.wait_pending(kernel_wait=fused_g2 and G2_WAITS_IN_KERNEL and ws.norms_token == _norms_token(P))
+    wait = P.wait_pending(kernel_wait=(fused_g2 or partial_g2) and G2_WAITS_IN_KERNEL
+                          and ws.norms_token == _norms_token(P))
     if wait is not None:
         wait = (*wait, _wait_err(ws))
     decoder_norms(ws, P)  # (+ W_dec^T), unless launched already after the last Adam
@@ -367,7 +370,10 @@ def forward(ws, P, x_in, factor=None, grad_scale=None, want_grad=True, loss=True
         else:
             nf = (ws.norm_part, ws.norms, ws.tn, ws.inv_norms) if ws.norms_fin_pending else None
             ws.norms_fin_pending = False
-            ops.decode_partial_jobs(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws, ws.n, ws.d, norm_fin=nf, pre=acts_job)
+            ops.decode_partial_jobs(ws.acts, P.W_dec_hk, ws.recon, ws.dec_ws, ws.n, ws.d, norm_fin=nf, pre=acts_job,
+                                    wait=wait)
+            if wait is not None:
+                P.pending_ordered = torch.cuda.current_stream(ws.x.device)
     # (G2 does not read the norms: their finaliser after it, where the latent-sharded step's collective on the
     # reconstruction hides it)
     flush_norms(ws)
@@ -559,7 +565,8 @@ def backward(ws, P, G, l1_coeff, l1_grad_weight=1.0, dacts_done=False, clip=None
                                   G.W_dec_hk, ws.sq_slice(1), ws.g_pre_t, ws.x_t, G.W_enc_hk, ws.sq_slice(0), n, d,
                                   ws.gpre_colpart, G.b_enc, ws.sq_slice(2), loss_colpart(ws), G.b_dec_flat,
                                   ws.sq_slice(3), ws.sq, ws.sq_off, sums_out, ws.tail_ctr[1:2], ws.tile_sum,
-                                  zero_mask=zero_mask, tile_ctr=_tile_ctr(ws, 2))
+                                  zero_mask=zero_mask, tile_ctr=_tile_ctr(ws, 2),
+                                  abort_ptr=ws.wait_err.device_ptr if ws.wait_err is not None else None)
         return
     if clip is not None and ws.tr:
         # G4 + G5 and the grad tail (bias sums + clip coefficient) in one launch

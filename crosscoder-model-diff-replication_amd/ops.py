@@ -202,15 +202,17 @@ def decode_partial(acts, W_dec_hk, recon_f32, ws=None):
                                  0 if ws is None else ws.numel(), B, h, K, dtype_code(acts.dtype), _stream(acts)))
 
 
-def decode_partial_jobs(acts, W_dec_hk, recon_f32, ws, n, d, norm_fin=None, pre=None):
+def decode_partial_jobs(acts, W_dec_hk, recon_f32, ws, n, d, norm_fin=None, pre=None, wait=None):
     """decode_partial (the same recon_f32 bits) carrying the step's small jobs (cc_decode_partial): pre, an
     ops.colsum_job run before the tiles; norm_fin = (part, norms, total, inv_norms), the decoder norms' finaliser
-    (dec_norms_finalize) as extra blocks of the split-K reduction launch."""
+    (dec_norms_finalize) as extra blocks of the split-K reduction launch; wait = (ctr, target, err_addr): the launch
+    waits in the kernel for a done counter of adam_dec_norms on another stream (as decode_loss)."""
     B, h = acts.shape
     part, norms, total, inv = norm_fin if norm_fin is not None else (None, None, None, None)
+    wctr, wtarget, werr = wait if wait is not None else (None, 0, None)
     check(lib().cc_decode_partial(_ptr(acts), _ptr(W_dec_hk), _ptr(recon_f32), _ptr(ws), 0 if ws is None else ws.numel(),
-                                  _ptr(part), _ptr(norms), _ptr(total), _ptr(inv), pre, B, h, n, d,
-                                  dtype_code(acts.dtype), _stream(acts)))
+                                  _ptr(part), _ptr(norms), _ptr(total), _ptr(inv), pre, _ptr(wctr),
+                                  int(wtarget) & 0xFFFFFFFF, werr, B, h, n, d, dtype_code(acts.dtype), _stream(acts)))
 
 
 def decode_partial_t(acts, W_dec_t, recon_f32, ws=None):
@@ -500,8 +502,9 @@ CLIP_ABORTED = -1.0  # clip_out[0] of a step whose update was not applied (inclu
 
 def wgrad_both_sums_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, grad_dec, sq_dec, g_preT, xT, grad_enc,
                       sq_enc, n, d, gpre_colpart, g_b_enc, sq_b_enc, loss_colpart, g_b_dec, sq_b_dec, sq, offsets, out,
-                      counter, tile_sum, zero_mask=0, tile_ctr=None):
-    """wgrad_both_t + grad_tail_sums in one launch (the latent-sharded step); same outputs."""
+                      counter, tile_sum, zero_mask=0, tile_ctr=None, abort_ptr=None):
+    """wgrad_both_t + grad_tail_sums in one launch (the latent-sharded step); same outputs.  abort_ptr: device address
+    of the step's abort word (when set, every out[p] is -inf: the all-reduced sums abort every rank's Adam)."""
     h, B = actsT.shape
     _check_tile_sum(tile_sum, h, n * d)
     arr = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
@@ -510,7 +513,7 @@ def wgrad_both_sums_t(actsT, g_reconT, W_dec_hk, norms, colsum_acts, l1_scale, g
         _ptr(sq_dec), _ptr(g_preT), _ptr(xT), _ptr(grad_enc), _ptr(sq_enc), B, h, n, d, _ptr(gpre_colpart),
         gpre_colpart.shape[0], _ptr(g_b_enc), _ptr(sq_b_enc), _ptr(loss_colpart), loss_colpart.shape[0], _ptr(g_b_dec),
         _ptr(sq_b_dec), _ptr(sq), arr, len(offsets) - 1, int(zero_mask), _ptr(out), _ptr(counter), _ptr(tile_sum),
-        _ctr(tile_ctr), dtype_code(actsT.dtype), _stream(actsT)))
+        _ctr(tile_ctr), _vptr(abort_ptr), dtype_code(actsT.dtype), _stream(actsT)))
 
 
 def clip_finalize(sq, offsets, max_norm, emulate_bf16, out):

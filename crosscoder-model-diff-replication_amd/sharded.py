@@ -361,6 +361,17 @@ class ShardedTrainer:
                          on_losses=self._copy_losses)
         self.lr = self.cfg["lr"] * self.lr_lambda(self.t)
         self._copied.synchronize()
+        if min(self._host_red[:4].tolist()) < 0:
+            # a rank's G2 timed out in its in-kernel wait for its side-stream Adam: its squared sums came out -inf
+            # (cc_wgrad_both_sums_t's abort), so the all-reduced sums made EVERY rank's Adam launches apply nothing
+            # (cc_adam_step_clip); every rank rolls back its step count and LR and raises in this same step
+            self.t -= 1
+            self.lr = self.cfg["lr"] * self.lr_lambda(self.t)
+            try:
+                engine.check_step_abort(self.backend.ws)  # (clears this rank's word, if it was this rank's G2)
+            except RuntimeError:
+                pass
+            raise RuntimeError(engine.STEP_ABORTED_MSG)
         s = self._host[:6].tolist()
         s[1], s[2] = self._host_red[4:6].tolist()  # l1, l0 over all ranks' latents
         # the reference's l1 / EV_A / EV_B are param-dtype tensors (crosscoder.py:115-126): same rounding as Trainer.step

@@ -162,10 +162,14 @@ int cc_decode_fwd_ws_t(const void* acts, const void* W_dec_t, float* recon_f32, 
  * crosscoder.py:126, from G1's column partials) -- and, norm_part given, the decoder norms' finaliser
  * (cc_dec_norms_finalize(norm_part, h, n, d, norms, tn, inv_norms), d % 64 == 0) as extra blocks of the
  * split-K leftover's reduction launch.  recon_f32 bit-identical to cc_decode_fwd_ws; the jobs' outputs to
- * their stand-alone launches. */
+ * their stand-alone launches.  wait_ctr (optional, bf16): the launch first waits IN ITS KERNEL until
+ * *wait_ctr - wait_target >= 0 (mod 2^32) -- the side-stream decoder-half Adam's done count, cc_adam_dec_norms --
+ * instead of the stream waiting for that Adam's event, as cc_decode_loss does; past ~1 s it runs no tile and sets
+ * *wait_err (host-visible), which the same step's cc_wgrad_both_sums_t (abort) turns into -inf squared sums. */
 int cc_decode_partial(const void* acts, const void* W_dec, float* recon_f32, float* ws, int64_t ws_floats,
                       const float* norm_part, float* norms, float* tn, float* inv_norms, const cc_colsum_job* pre,
-                      int64_t B, int64_t h, int64_t n, int64_t d, int dtype, void* stream);
+                      const uint32_t* wait_ctr, uint32_t wait_target, uint32_t* wait_err, int64_t B, int64_t h,
+                      int64_t n, int64_t d, int dtype, void* stream);
 
 /* get_losses reconstruction terms + their backward (crosscoder.py:104-121, autograd):
  * r = recon_f32 + b_dec; g_recon = dtype(grad_scale * (r - x)) with grad_scale = 2/B.
@@ -362,14 +366,16 @@ int cc_wgrad_both_clip_t(const void* actsT, const void* g_reconT, const void* W_
 /* cc_wgrad_both_clip_t whose finaliser is cc_segment_sums instead of the clip (the latent-sharded step,
  * trainer.py:45-46 split across ranks): out[p] = the per-parameter squared sums, 0 where bit p of
  * zero_mask is set, to be all-reduced.  Equal to cc_wgrad_both_t + cc_grad_tail_sums (the sums up to the
- * order of their fp64 accumulation), which it runs itself where the ping-pong GEMM does not serve. */
+ * order of their fp64 accumulation), which it runs itself where the ping-pong GEMM does not serve.  abort
+ * (optional): the step's abort word (cc_decode_partial's wait_err); when set, out[p] = -inf for every p, so the
+ * all-reduced sums carry the abort to every rank and cc_adam_step_clip (a negative sum) applies nothing. */
 int cc_wgrad_both_sums_t(const void* actsT, const void* g_reconT, const void* W_dec, const float* inv_norms,
                          const float* colsum_acts, float l1_scale, void* grad_W_dec, float* sq_dec, const void* g_preT,
                          const void* xT, void* grad_W_enc, float* sq_enc, int64_t B, int64_t h, int64_t n, int64_t d,
                          const float* gpre_colpart, int64_t R_enc, void* g_b_enc, float* sq_b_enc,
                          const float* loss_colpart, int64_t R_dec, void* g_b_dec, float* sq_b_dec, const float* sq,
                          const int64_t* off, int nparams, int zero_mask, float* out, uint32_t* counter, float* tile_sum,
-                         uint32_t* tile_ctr, int dtype, void* stream);
+                         uint32_t* tile_ctr, const uint32_t* abort, int dtype, void* stream);
 /* cc_grad_tail whose finaliser is cc_segment_sums instead of the clip (the latent-sharded step:
  * out[p] = the per-parameter squared sums, 0 where bit p of zero_mask is set, to be all-reduced). */
 int cc_grad_tail_sums(const float* gpre_colpart, int64_t R_enc, int64_t h, void* g_b_enc, float* sq_b_enc,
@@ -395,7 +401,9 @@ int cc_adam_step(void* p, const void* g, void* m, void* v, int64_t numel, const 
 /* cc_adam_step with clip_grad_norm_'s coefficient formed in the kernel from the per-parameter squared
  * gradient sums `sums` [nparams] (trainer.py:46 over parameters whose sums were combined elsewhere, e.g.
  * all-reduced over the latent shards): the arithmetic of cc_clip_finalize over one element per parameter.
- * clip_out (optional): [coef, total norm, per-parameter norms] as cc_clip_finalize writes them. */
+ * clip_out (optional): [coef, total norm, per-parameter norms] as cc_clip_finalize writes them.  A negative
+ * sum (an aborted step's -inf, cc_wgrad_both_sums_t's abort) makes the coefficient CC_CLIP_ABORTED: nothing is
+ * updated. */
 int cc_adam_step_clip(void* p, const void* g, void* m, void* v, int64_t numel, const float* sums, int nparams,
                       float max_norm, int emulate_bf16, float* clip_out, double lr, double beta1, double beta2,
                       double eps, int64_t step, int64_t max_blocks, int dtype, void* stream);

@@ -52,7 +52,8 @@ def test_library_exports_only_the_header():
     kernel handles); the test-only debug build adds only its launch-form setters."""
     syms = set(declared_symbols())
     assert _dynamic_exports(_lib.LIB_PATH) == syms
-    assert _dynamic_exports(_lib.DEBUG_LIB_PATH) == syms | set(_lib.DEBUG_SETTERS) | {"cc_debug_spin", "cc_debug_spin_ev", "cc_debug_set_stamps"}
+    assert _dynamic_exports(_lib.DEBUG_LIB_PATH) == syms | set(_lib.DEBUG_SETTERS) | {"cc_debug_spin", "cc_debug_spin_ev",
+                                                                       "cc_debug_set_stamps", "cc_debug_get_q4"}
 
 
 def test_argument_validation_without_gpu():

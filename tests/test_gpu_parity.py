@@ -1910,3 +1910,61 @@ def test_q4_trainer_steps_bit_identical(gpu, q4, full_size_case):
     assert d0 == d1
     assert torch.equal(p0, p1)
     assert all(torch.equal(a, b) for a, b in zip(m0, m1))
+
+
+def test_sharded_g2_kernel_wait_timeout_aborts_the_same_step(gpu, monkeypatch):
+    """The latent-sharded step's G2 (cc_decode_partial) waits for the side-stream decoder-half Adam in its kernel,
+    as the single-GPU step's G2 does (no event hand-off before G2).  Its abort must reach every
+    rank: on a timeout G2 runs no tile and sets the rank's abort word, the same step's G4G5 sums launch writes -inf
+    squared sums, the 24-byte all-reduce carries them to every rank, and each Adam launch forming its coefficient from
+    them (cc_adam_step_clip) applies nothing.  On a 1-rank RCCL group: the step raises, params and both moments are
+    bit for bit those before it, the step count and LR are rolled back, the word is cleared, and -- the counter
+    restored -- the next step equals a sharded trainer that skipped the aborted batch."""
+    import os
+
+    import torch.distributed as dist
+    from crosscoder_amd import engine, sharded
+
+    monkeypatch.setattr(engine, "G2_WAITS_IN_KERNEL", True)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(28600 + os.getpid() % 1000)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
+    try:
+        B, n, d, h = 1024, 2, 256, 2048
+        cfg = dict(load(STEP_FIXTURES[0])["cfg"], d_in=d, dict_size=h, batch_size=B, enc_dtype="bf16",
+                   num_tokens=B * 20, device=str(gpu))
+
+        def snapshot(tr):  # params, exp_avg, exp_avg_sq (after the deferred decoder rows)
+            tr.synchronize()
+            torch.cuda.synchronize()
+            return [a.data.clone() for a in (tr.crosscoder.arena(), tr.backend.M, tr.backend.V)]
+
+        ref = sharded.ShardedTrainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 4, seed=5))
+        r1 = ref.step()
+        before = snapshot(ref)
+        ref.buffer.next_raw()  # (the batch the aborted step consumes)
+        r3 = ref.step()
+        final_ref = snapshot(ref)
+
+        tr = sharded.ShardedTrainer(cfg, buffer=ca.SyntheticBuffer(cfg, rows=B * 4, seed=5))
+        assert tr.step() == r1
+        lr_before, t_before = tr.lr, tr.t
+        torch.cuda.synchronize()  # (no parameter accessor: the next G2 must wait in its kernel)
+        ws = tr.backend.ws
+        assert tr.crosscoder.arena().pending_rest is not None  # (the kernel-wait path is the one under test)
+        ws.adam_done[0] -= 1 << 20
+        torch.cuda.synchronize()
+        with pytest.raises(RuntimeError, match="step was aborted"):
+            tr.step()  # (its G2 times out)
+        assert all(v == float("-inf") for v in tr._host_red[:4].tolist())
+        for a, b in zip(before, snapshot(tr)):
+            assert torch.equal(a, b)  # no update applied on the rank
+        assert tr.t == t_before == 1 and tr.step_counter == 1 and tr.lr == lr_before
+        assert ws.wait_err.u32[0] == 0  # (cleared)
+        ws.adam_done[0] += 1 << 20
+        torch.cuda.synchronize()
+        assert tr.step() == r3
+        for a, b in zip(final_ref, snapshot(tr)):
+            assert torch.equal(a, b)
+    finally:
+        dist.destroy_process_group()
