@@ -798,19 +798,17 @@ def test_full_size_config2_trainer_steps_match_oracle(gpu, full_size_case, total
     # (all steps printed first, then checked)
     for s, l1c, stats in history:
         for k, (close, worst, em, ev) in stats.items():
-            # measured over the 5 warm-up steps (l1_coeff <= 1.6): close >= 0.994 W_enc / 0.996 others; worst <= 3.7 lr;
-            # W_enc's exp_avg rel grows 0.009 -> 0.045, the others' moments stay <= 0.034.  With l1_coeff 2 from step 1
-            # the encoder side's gradient g_pre = g_recon W_dec^T + l1_coeff tn / B partly cancels, and bf16 vs fp32
-            # differ most there (the reference's own bf16 mode shows the same cancellation, SURVEY 8c: dW_enc 6.3e-2):
-            # W_enc's params drift apart faster (close 0.985 / 0.977 at steps 1 / 2), b_enc's exp_avg rel 0.058.
+            # Measured on MI355X (round 6, both runs): the warm-up steps (l1_coeff <= 1.6) close >= 0.994 W_enc / 0.996
+            # others, worst <= 3.7 lr, W_enc's exp_avg rel 0.009 -> 0.045, the others' moments <= 0.034.  Under the
+            # full l1_coeff 2 the encoder side's gradient g_pre = g_recon W_dec^T + l1_coeff tn / B partly cancels and
+            # bf16 vs fp32 differ most there (the reference's own bf16 mode shows the same cancellation, SURVEY 8c:
+            # dW_enc 6.3e-2): W_enc close 0.969-0.985 over steps 1-9, worst <= 4.41 lr, W_enc's exp_avg rel
+            # 0.045 -> 0.101 by step 9, b_enc's 0.058 at step 1; the decoder side stays <= 0.015.  Bounds ~2x those.
             enc = k in ("W_enc", "b_enc")
-            if k == "W_enc":  # (provisional under the full l1 term: 1 % per step)
-                cmin = 0.99 - 0.01 * (s + 1) if l1c >= 2.0 else 0.98
-            else:
-                cmin = 0.99
+            cmin = (0.98 if l1c < 2.0 else 0.94) if k == "W_enc" else 0.99
             assert close >= cmin, (s, k, close, cmin)
-            assert worst <= 6.0 + 0.5 * max(0, s - 4), (s, k, worst)
-            tol = (0.1 if enc else 3e-2) * (1 + 0.25 * max(0, s - 4))
+            assert worst <= 6.0, (s, k, worst)
+            tol = (0.12 if s <= 4 else 0.2) if enc else 3e-2
             assert em <= tol and ev <= 2 * tol, (s, k, em, ev)
     assert d["l1_coeff"] == cfg["l1_coeff"] if total_batches == 10 else d["l1_coeff"] < cfg["l1_coeff"]
     assert seen_decay == (total_batches == 10)
