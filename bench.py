@@ -207,20 +207,27 @@ def allreduce_algbw(rows, K, iters=10, dev="cuda"):
             "busbw_GB_s": round(algbw * 2 * (G - 1) / G, 1)}
 
 
-def measure_exchange(tr, comm, K, dev="cuda", steps=5):
-    """The latent-sharded step's exchange, measured in warm-up (not the timed region): each candidate form ("auto":
-    all_reduce and reduce_scatter) runs one settling step and `steps` timed steps (max over ranks); the faster one
-    is left set on the trainer; plus the bandwidth one slice's all-reduce reaches alone.  Every rank picks the same
-    form (the times are all-reduced)."""
-    trial = {}
+def measure_exchange(tr, comm, K, dev="cuda", steps=5, slices=None):
+    """The latent-sharded step's exchange, measured in warm-up (not the timed region): each candidate form runs one
+    settling step and `steps` timed steps (max over ranks); the fastest is left set on the trainer; plus the
+    bandwidth one slice's all-reduce reaches alone.  "auto": the all-reduce in 1, 2 and 4 batch slices (unless
+    `slices` fixes the count) and the reduce-scatter.  Every rank picks the same form (the times are all-reduced)."""
+    cands = []
     for c in (("all_reduce", "reduce_scatter") if comm == "auto" else (comm,)):
-        tr.engine.comm = c
+        if c == "all_reduce" and comm == "auto" and slices is None:
+            cands += [(f"all_reduce x{s}", c, s) for s in (1, 2, 4)]
+        else:
+            s = slices or tr.backend.recon_chunks
+            cands.append((c if c == "reduce_scatter" or comm != "auto" else f"all_reduce x{s}", c, s))
+    trial = {}
+    for name, c, s in cands:
+        tr.engine.comm, tr.backend.recon_chunks = c, s
         tr.step()
-        trial[c] = round(timed_steps(tr, steps, dev) * 1e3, 4)
+        trial[name] = round(timed_steps(tr, steps, dev) * 1e3, 4)
     pick = min(trial, key=trial.get)
-    tr.engine.comm = pick
+    _, tr.engine.comm, tr.backend.recon_chunks = next(x for x in cands if x[0] == pick)
     chunks = tr.backend.row_chunks()
-    return {"comm": pick, "chosen_by": "auto (faster in warm-up)" if comm == "auto" else "--comm",
+    return {"comm": tr.engine.comm, "chosen_by": "auto (fastest in warm-up)" if comm == "auto" else "--comm",
             "trial_ms_per_step": trial, "slices": len(chunks),
             "slice_allreduce": allreduce_algbw(chunks[0][1] - chunks[0][0], K, dev=dev)}
 
@@ -460,7 +467,8 @@ def main():
     ap.add_argument("--no-n1", action="store_true",
                     help="N > 1: skip the in-job one-GPU measurement of the same workload (n1_same_workload)")
     ap.add_argument("--recon-chunks", type=int, default=None,
-                    help="latent-sharded step: batch slices the exchange is overlapped by (default 2)")
+                    help="latent-sharded step: batch slices the all-reduce is overlapped by (default N > 1: timed "
+                         "in warm-up with --comm auto, 1 / 2 / 4; one rank: 1)")
     ap.add_argument("--force-sharded", action="store_true",
                     help="diagnostic: run the latent-sharded step even on one rank (1-rank RCCL group)")
     args = ap.parse_args()
@@ -545,7 +553,7 @@ def run_rank(args):
     engine.TIMER = timer
     for _ in range(args.warmup):
         tr.step()
-    exchange = measure_exchange(tr, comm, K) if sharded_path else None
+    exchange = measure_exchange(tr, comm, K, slices=args.recon_chunks) if sharded_path else None
     # attribution pass (not timed): every kernel bracketed by events
     attrib = EventTimer()
     engine.TIMER = attrib

@@ -103,14 +103,16 @@ class _FakeShardedTrainer:
 
         self.rank, self.dist = rank, dist
         self.engine = type("E", (), {"comm": "all_reduce"})()
-        self.backend = type("Bk", (), {"row_chunks": staticmethod(lambda: [(0, 16), (16, 32)])})()
+        bk = self.backend = type("Bk", (), {"recon_chunks": 2})()
+        bk.row_chunks = lambda: [(r0, r0 + 32 // bk.recon_chunks) for r0 in range(0, 32, 32 // bk.recon_chunks)]
         self.comms = []
 
     def step(self):
         import torch
 
-        self.comms.append(self.engine.comm)
-        time.sleep(0.002 if self.engine.comm == "all_reduce" else 0.004 + 0.004 * self.rank)
+        self.comms.append((self.engine.comm, self.backend.recon_chunks))
+        ar = 0.002 if self.backend.recon_chunks == 2 else 0.004 + 0.002 * self.rank
+        time.sleep(ar if self.engine.comm == "all_reduce" else 0.006 + 0.004 * self.rank)
         t = torch.ones(4)
         self.dist.all_reduce(t)
 
@@ -127,14 +129,15 @@ def _exchange_rank(rank, world, port, q):
         ex = bench.measure_exchange(tr, "auto", K=8, dev="cpu", steps=3)
         kern = {"G1_encode": 0.5, "exchange_wait0": 0.12, "exchange_wait1": 0.01, "sums_allreduce": 0.02}
         bench.exchange_exposed(kern, ex)
-        q.put((rank, ex, kern, tr.engine.comm, sorted(set(tr.comms))))
+        q.put((rank, ex, kern, (tr.engine.comm, tr.backend.recon_chunks), sorted(set(tr.comms))))
     finally:
         dist.destroy_process_group()
 
 
 def test_sharded_bench_exchange_fields_over_two_gloo_ranks():
-    """The N > 1 line's exchange evidence, its host logic over 2 gloo ranks: both exchange
-    forms are timed in warm-up (max over ranks), the faster is left set on the trainer -- the same on every rank --,
+    """The N > 1 line's exchange evidence, its host logic over 2 gloo ranks: the exchange
+    forms (the all-reduce in 1, 2 and 4 batch slices, the reduce-scatter) are timed in warm-up (max over ranks), the
+    fastest is left set on the trainer -- the same on every rank --,
     one slice's all-reduce bandwidth is measured, and the attribution pass's exchange spans become the exposed time
     per step (removed from the kernel table)."""
     import random
@@ -153,10 +156,13 @@ def test_sharded_bench_exchange_fields_over_two_gloo_ranks():
         assert p.exitcode == 0
     for rank in range(world):
         ex, kern, comm, tried = res[rank]
-        assert tried == ["all_reduce", "reduce_scatter"] and comm == "all_reduce" == ex["comm"]
+        assert tried == [("all_reduce", 1), ("all_reduce", 2), ("all_reduce", 4), ("reduce_scatter", 2)]
+        assert comm == ("all_reduce", 2) and ex["comm"] == "all_reduce"
         assert set(ex) == {"comm", "chosen_by", "trial_ms_per_step", "slices", "slice_allreduce",
                            "exposed_ms_per_step", "exposed_ms_by_slice", "sums_allreduce_ms"}
-        assert ex["trial_ms_per_step"]["reduce_scatter"] > ex["trial_ms_per_step"]["all_reduce"] > 0
+        tr_ms = ex["trial_ms_per_step"]
+        assert set(tr_ms) == {"all_reduce x1", "all_reduce x2", "all_reduce x4", "reduce_scatter"}
+        assert min(tr_ms["reduce_scatter"], tr_ms["all_reduce x1"], tr_ms["all_reduce x4"]) > tr_ms["all_reduce x2"] > 0
         assert ex["slices"] == 2 and ex["slice_allreduce"]["bytes"] == 16 * 8 * 4
         assert ex["slice_allreduce"]["busbw_GB_s"] == pytest.approx(ex["slice_allreduce"]["algbw_GB_s"], rel=0.01)
         assert ex["exposed_ms_per_step"] == pytest.approx(0.13) and ex["sums_allreduce_ms"] == 0.02

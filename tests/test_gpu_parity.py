@@ -1240,19 +1240,19 @@ def test_decode_loss_on_wdec_matches_transposed(gpu, B, n, d, h):
 
 
 @pytest.mark.parametrize("comm", ["all_reduce", "reduce_scatter"])
-@pytest.mark.parametrize("chunks", [1, 2])
+@pytest.mark.parametrize("chunks", [1, 2, 4])
 def test_sharded_trainer_world1_matches_trainer(gpu, comm, chunks):
     """ShardedTrainer over a 1-rank RCCL group takes the same steps as the single-GPU Trainer, in the shipped
-    exchange forms: the all-reduce as one synchronous collective (1 slice, the world-1 default) or in the 2
-    batch slices of the world > 1 default (slice 2's exchange in flight during slice 1's loss rows + d_acts), and
-    the reduce-scatter + all-gather exchange."""
+    exchange forms: the all-reduce as one synchronous collective (1 slice, the world-1 default) or in 2 / 4
+    batch slices (slice c+1's exchange in flight during slice c's loss rows + d_acts; bench.py's warm-up picks the
+    count at N > 1), and the reduce-scatter + all-gather exchange."""
     import os
 
     import torch.distributed as dist
     from crosscoder_amd import sharded
 
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = str(29600 + os.getpid() % 1000 + 2 * (comm == "reduce_scatter") + chunks)
+    os.environ["MASTER_PORT"] = str(29600 + 10 * (os.getpid() % 100) + 5 * (comm == "reduce_scatter") + chunks)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
     try:
         B, n, d, h = 1024, 2, 256, 2048

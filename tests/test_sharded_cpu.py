@@ -36,8 +36,8 @@ class CpuShardBackend:
         return self.recon
 
     def row_chunks(self):
-        # two slices: the sliced (asynchronous) all-reduce; one: the synchronous one
-        return [(0, B // 2), (B // 2, B)] if self.slices == 2 else [(0, B)]
+        # several slices: the sliced (asynchronous) all-reduce; one: the synchronous one
+        return [(i * B // self.slices, (i + 1) * B // self.slices) for i in range(self.slices)]
 
     def rows_ready(self, r0, r1, l1c):
         pass  # the torch backend does all loss / backward work in loss_finalize / backward
@@ -159,11 +159,11 @@ def _worker(rank, world, port, q, comm, slices=2):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("comm,slices", [("all_reduce", 2), ("all_reduce", 1), ("reduce_scatter", 1)])
+@pytest.mark.parametrize("comm,slices", [("all_reduce", 2), ("all_reduce", 4), ("all_reduce", 1), ("reduce_scatter", 1)])
 @pytest.mark.parametrize("world", [2, 4])
 def test_sharded_step_matches_unsharded(world, comm, slices):
-    """Both exchanges of the partial reconstructions: the all-reduce (in two batch slices, or
-    one synchronous collective), and the reduce-scatter by batch rows -> loss on B/G rows -> all-gather
+    """Both exchanges of the partial reconstructions: the all-reduce (in two or four batch slices,
+    or one synchronous collective), and the reduce-scatter by batch rows -> loss on B/G rows -> all-gather
     of g_recon and the row terms."""
     port = 29500 + random.randint(0, 2000)
     ctx = mp.get_context("spawn")
